@@ -1,0 +1,96 @@
+# MI355X (gfx950) cipher engine -- native build.
+#
+#   make            -> our_tree_amd/lib/libotc.so (HIP kernels + runtime + CPU oracle)
+#                      our_tree_amd/lib/libotc_cpu.so (CPU oracle only, no ROCm deps)
+#                      bin/test bin/aes_test bin/aes_ecb_e bin/aes_ecb_d bin/otbench
+#   make cpu        -> CPU-only pieces (no hipcc needed)
+#   make SAN=1 cpu  -> CPU oracle with ASan/UBSan (host only)
+#
+# Reference build: Makefile:1-56 (gcc -O0), aes-modes/Makefile (clang -O0,
+# broken on current compilers), aes-gpu/Source/Makefile.asc (nvcc, no -arch).
+ROCM    ?= /opt/rocm
+HIPCC   ?= $(ROCM)/bin/hipcc
+ARCH    ?= gfx950
+CC      ?= gcc
+CXX     ?= g++
+
+INC      := -Icsrc/include -Icsrc/hip
+CFLAGS   ?= -O2 -g -Wall -Wextra -std=gnu99 -fPIC
+CXXFLAGS ?= -O2 -g -Wall -std=c++17 -fPIC
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wno-unused-result
+SANLD :=
+ifeq ($(SAN),1)
+CFLAGS   += -fsanitize=address,undefined -fno-omit-frame-pointer
+CXXFLAGS += -fsanitize=address,undefined -fno-omit-frame-pointer
+SANLD    := -fsanitize=address,undefined
+endif
+
+LIBDIR := our_tree_amd/lib
+OBJ    := build/obj
+
+CPU_SRC := csrc/cpu/aes.c csrc/cpu/arc4.c csrc/cpu/rc4.c csrc/cpu/aesni.c
+CPU_OBJ := $(patsubst csrc/cpu/%.c,$(OBJ)/cpu/%.o,$(CPU_SRC)) $(OBJ)/cpu/bs_selftest.o
+HIP_SRC := csrc/hip/aes_tt.hip csrc/hip/aes_bs.hip csrc/hip/stream_ops.hip
+HIP_OBJ := $(patsubst csrc/hip/%.hip,$(OBJ)/hip/%.o,$(HIP_SRC)) $(OBJ)/hip/engine.o
+
+BINS := bin/test bin/aes_test bin/aes_ecb_e bin/aes_ecb_d bin/otbench
+
+.PHONY: all cpu clean
+all: $(LIBDIR)/libotc.so $(LIBDIR)/libotc_cpu.so $(BINS)
+cpu: $(LIBDIR)/libotc_cpu.so bin/test_cpu
+
+$(OBJ)/cpu/aesni.o: csrc/cpu/aesni.c csrc/include/aesni.h
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS) -maes -msse4.1 -mssse3 $(INC) -c $< -o $@
+
+$(OBJ)/cpu/%.o: csrc/cpu/%.c $(wildcard csrc/include/*.h)
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS) $(INC) -c $< -o $@
+
+$(OBJ)/cpu/bs_selftest.o: csrc/cpu/bs_selftest.cpp csrc/include/otc_bitslice.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) $(INC) -c $< -o $@
+
+$(OBJ)/hip/%.o: csrc/hip/%.hip csrc/hip/otc_device.h csrc/include/otc.h csrc/include/otc_bitslice.h
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) $(INC) -c $< -o $@
+
+$(OBJ)/hip/engine.o: csrc/hip/engine.cpp csrc/hip/otc_device.h csrc/include/otc.h
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -x hip $(INC) -c $< -o $@
+
+$(LIBDIR)/libotc.so: $(HIP_OBJ) $(CPU_OBJ)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lpthread -Wl,-rpath,$(ROCM)/lib
+
+$(LIBDIR)/libotc_cpu.so: $(CPU_OBJ)
+	@mkdir -p $(LIBDIR)
+	$(CXX) -shared -fPIC -o $@ $^ -lpthread $(SANLD)
+
+# --- CLIs -------------------------------------------------------------------
+bin/test_cpu: csrc/cli/rc4_test.c $(CPU_OBJ)
+	@mkdir -p bin
+	$(CXX) -O2 $(INC) -x c -std=gnu99 $< -x none $(CPU_OBJ) -o $@ -lpthread $(SANLD)
+
+bin/test: csrc/cli/rc4_test.c $(LIBDIR)/libotc.so
+	@mkdir -p bin
+	$(CC) -O2 -std=gnu99 -DOTC_WITH_GPU $(INC) $< -o $@ -L$(LIBDIR) -lotc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
+
+bin/aes_test: csrc/cli/aes_test.c $(LIBDIR)/libotc.so
+	@mkdir -p bin
+	$(CC) -O2 -std=gnu99 -DOTC_WITH_GPU $(INC) $< -o $@ -L$(LIBDIR) -lotc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
+
+bin/aes_ecb_e: csrc/cli/aes_ecb_e.c $(LIBDIR)/libotc.so
+	@mkdir -p bin
+	$(CC) -O2 -std=gnu99 $(INC) $< -o $@ -L$(LIBDIR) -lotc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+
+bin/aes_ecb_d: csrc/cli/aes_ecb_d.c $(LIBDIR)/libotc.so
+	@mkdir -p bin
+	$(CC) -O2 -std=gnu99 $(INC) $< -o $@ -L$(LIBDIR) -lotc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+
+bin/otbench: csrc/cli/otbench.cpp $(LIBDIR)/libotc.so
+	@mkdir -p bin
+	$(CXX) -O2 -std=c++17 $(INC) $< -o $@ -L$(LIBDIR) -lotc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
+
+clean:
+	rm -rf build $(LIBDIR)/*.so $(BINS) bin/test_cpu

@@ -1,0 +1,155 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node AES-128-CTR throughput (GB/s) on MI355X.
+
+Metric and config come from BASELINE.json ("GB/s AES-128-CTR (whole node) at
+1/2/4/8 MI355X; cycles/byte per CU"; config "AES-128-CTR 64 GiB ... one
+MI355X").  One process per GPU (torchrun), each rank owns a 64 GiB shard of one
+logical plaintext stream in HBM (synthetic random bytes, random key) and
+encrypts it in place with the counter offset of its shard (rank * shard_blocks)
+-- weak scaling, 64 GiB per GPU.  A step = one full pass over every shard.
+Timing: W untimed warmup steps, barrier + synchronize, K timed steps,
+synchronize + barrier, MAX over ranks.  Correctness is checked on a sample of
+every shard against the CPU oracle before timing.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--gib 64]
+        torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_GBPS = 0.519  # BASELINE.md headline CTR: AES-NI CTR-256, 1000 MiB, 8 threads (frankchn)
+BASELINE_GPU_GBPS = 2.41  # BASELINE.md repo headline: CUDA "AES ECB" 1000 MiB (baryon)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--gib", type=float, default=64.0, help="per-GPU shard size in GiB")
+    ap.add_argument("--impl", default=os.environ.get("OTC_BENCH_IMPL", "auto"))
+    ap.add_argument("--no-aes256", action="store_true")
+    args = ap.parse_args()
+
+    from our_tree_amd import ops
+    from our_tree_amd.models import cpu_ref
+    from our_tree_amd.parallel import dist as pdist
+    from our_tree_amd.utils import device as dinfo
+
+    rank, world, local = pdist.init_from_env()
+    if world != args.gpus:
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    nbytes = int(args.gib * (1 << 30))
+    nbytes -= nbytes % 16
+    gen = torch.Generator().manual_seed(1337)
+    key = bytes(torch.randint(0, 256, (16,), generator=gen, dtype=torch.uint8).tolist())
+    key256 = bytes(torch.randint(0, 256, (32,), generator=gen, dtype=torch.uint8).tolist())
+    counter = bytes(torch.randint(0, 256, (16,), generator=gen, dtype=torch.uint8).tolist())
+    shard_blocks = nbytes // 16
+    my_block0 = rank * shard_blocks
+
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    ops.fill_random_(buf, seed=1000 + rank)
+
+    # ---- correctness on a sample (outside the timed region) ----------------
+    S = 1 << 16
+    head = buf[:S].cpu().numpy().tobytes()
+    tail_off = nbytes - S
+    tail = buf[tail_off:].cpu().numpy().tobytes()
+    ops.ctr(buf, key, counter, out=buf, block_offset=my_block0, impl=args.impl)
+    torch.cuda.synchronize()
+    ok = (buf[:S].cpu().numpy().tobytes() == cpu_ref.ctr(key, counter, head, my_block0)
+          and buf[tail_off:].cpu().numpy().tobytes()
+          == cpu_ref.ctr(key, counter, tail, my_block0 + tail_off // 16))
+    ok_all = pdist.allreduce_max(0.0 if ok else 1.0) == 0.0
+    if not ok_all:
+        if rank == 0:
+            print(json.dumps({"error": "verification failed"}))
+        sys.exit(1)
+
+    def step(k=key):
+        ops.ctr(buf, k, counter, out=buf, block_offset=my_block0, impl=args.impl)
+
+    def timed(nsteps, k):
+        for _ in range(args.warmup):
+            step(k)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(nsteps):
+            step(k)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t0
+        return pdist.allreduce_max(el)
+
+    elapsed = timed(args.steps, key)
+    ms_per_step = elapsed / args.steps * 1e3
+    total_bytes = nbytes * world * args.steps
+    value = total_bytes / elapsed / 1e9
+
+    info = dinfo.info(local)
+    cpb = (ms_per_step * 1e-3) * info["clock_hz"] * info["cus"] / nbytes
+
+    extra = {}
+    if not args.no_aes256:
+        k256_steps = max(1, min(args.steps, 5))
+        el256 = timed(k256_steps, key256)
+        extra["aes256_ctr_gbps_whole_node"] = round(nbytes * world * k256_steps / el256 / 1e9, 3)
+        extra["aes256_vs_cpu_aesni_ctr256"] = round(extra["aes256_ctr_gbps_whole_node"] / BASELINE_GBPS, 1)
+
+    if rank == 0:
+        line = {
+            "metric": "GB/s AES-128-CTR (whole node)",
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_GBPS, 2),
+            "dtype": "bf16",
+            "data": "synthetic random plaintext (splitmix64), random 128-bit key and counter",
+            "config": {
+                "model": "AES-128-CTR",
+                "global_batch": nbytes * world,
+                "seq_len": nbytes,
+                "parallelism": f"dp{world}",
+                "per_gpu_bytes": nbytes,
+                "in_place": True,
+                "impl": args.impl,
+            },
+            "cycles_per_byte_per_cu": round(cpb, 4),
+            "per_gpu_gbps": round(value / world, 3),
+            "baseline": {"value_gbps": BASELINE_GBPS, "what": "AES-NI CTR-256 1000MiB 8thr (BASELINE.md)",
+                         "gpu_headline_gbps": BASELINE_GPU_GBPS},
+            "verified_sample": True,
+            **extra,
+        }
+        line["dtype"] = "uint8"  # cipher engine: byte data (no floating-point compute)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

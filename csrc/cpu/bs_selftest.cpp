@@ -1,0 +1,116 @@
+/*
+ * bs_selftest.cpp -- host-side validation of the bitsliced AES core
+ * (include/otc_bitslice.h) against the table oracle (cpu/aes.c): exhaustive
+ * S-box check plus full AES-128/192/256 encryption of 32 random blocks.
+ * Exported as otc_bitslice_selftest() so both the C test binary and pytest
+ * can call it without a GPU.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "aes.h"
+#include "otc_bitslice.h"
+
+using namespace otc_bs;
+
+extern "C" int otc_bitslice_selftest(int verbose)
+{
+    const uint8_t *SB = aes_sbox();
+    int fails = 0;
+    /* S-box: 256 inputs as 8 batches of 32 slots */
+    for (int batch = 0; batch < 8; ++batch) {
+        W x[8] = {0};
+        for (int k = 0; k < 32; ++k) {
+            int v = batch * 32 + k;
+            for (int i = 0; i < 8; ++i) x[i] |= (W)((v >> i) & 1) << k;
+        }
+        sbox(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
+        for (int k = 0; k < 32; ++k) {
+            int v = batch * 32 + k, o = 0;
+            for (int i = 0; i < 8; ++i) o |= (int)((x[i] >> k) & 1) << i;
+            if (o != SB[v]) {
+                if (verbose) printf("  sbox mismatch at %02x: %02x vs %02x\n", v, o, SB[v]);
+                ++fails;
+            }
+        }
+    }
+    /* key-folded S-box: sbox_k(x, k) == sbox(x ^ k) */
+    for (int kv = 0; kv < 256; kv += 37) {
+        W k[8], x[8] = {0}, y[8];
+        for (int i = 0; i < 8; ++i) k[i] = ((kv >> i) & 1) ? ~0u : 0u;
+        for (int slot = 0; slot < 32; ++slot)
+            for (int i = 0; i < 8; ++i) x[i] |= (W)(((slot * 7 + kv) >> i) & 1) << slot;
+        for (int i = 0; i < 8; ++i) y[i] = x[i] ^ k[i];
+        sbox(y[0], y[1], y[2], y[3], y[4], y[5], y[6], y[7]);
+        sbox_k<false>(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7]);
+        for (int i = 0; i < 8; ++i)
+            if (x[i] != y[i]) {
+                if (verbose) printf("  sbox_k mismatch kv=%d bit %d\n", kv, i);
+                ++fails;
+            }
+    }
+    /* full cipher */
+    srand(7);
+    for (int bits = 128; bits <= 256; bits += 64) {
+        unsigned char key[32], pt[32][16], ref[32][16];
+        for (int i = 0; i < 32; ++i) key[i] = (unsigned char)rand();
+        for (int k = 0; k < 32; ++k)
+            for (int i = 0; i < 16; ++i) pt[k][i] = (unsigned char)rand();
+        aes_context ctx;
+        aes_setkey_enc(&ctx, key, (unsigned)bits);
+        for (int k = 0; k < 32; ++k) aes_crypt_ecb(&ctx, AES_ENCRYPT, pt[k], ref[k]);
+        uint32_t rk[60];
+        aes_export_rk32(&ctx, rk);
+        W s[128];
+        for (int w = 0; w < 4; ++w) {
+            W m[32];
+            for (int k = 0; k < 32; ++k) memcpy(&m[k], &pt[k][4 * w], 4);
+            transpose32(m);
+            for (int q = 0; q < 32; ++q) s[32 * w + q] = m[q];
+        }
+        W km[128];
+        key_masks(rk, km);
+        for (int p = 0; p < 128; ++p) s[p] ^= km[p];
+        for (int r = 1; r < ctx.nr; ++r) {
+            key_masks(rk + 4 * r, km);
+            round_full(s, km);
+        }
+        key_masks(rk + 4 * ctx.nr, km);
+        round_last(s, km);
+        int bad = 0;
+        for (int w = 0; w < 4; ++w) {
+            W m[32];
+            for (int q = 0; q < 32; ++q) m[q] = s[32 * w + q];
+            transpose32(m);
+            for (int k = 0; k < 32; ++k) bad += memcmp(&m[k], &ref[k][4 * w], 4) != 0;
+        }
+        if (verbose) printf("  bitsliced AES-%d (32 blocks): %s\n", bits, bad ? "failed" : "passed");
+        fails += bad;
+
+        /* kernel round structure (encrypt_planes, key folded into S-boxes) */
+        for (int w = 0; w < 4; ++w) {
+            W m[32];
+            for (int k = 0; k < 32; ++k) memcpy(&m[k], &pt[k][4 * w], 4);
+            transpose32(m);
+            for (int q = 0; q < 32; ++q) s[32 * w + q] = m[q];
+        }
+        auto kf = [&](int r, int p) -> W { return (W)(0u - ((rk[4 * r + (p >> 5)] >> (p & 31)) & 1u)); };
+        if (ctx.nr == 10) encrypt_planes<10, false>(s, kf);
+        else if (ctx.nr == 12) encrypt_planes<12, false>(s, kf);
+        else encrypt_planes<14, false>(s, kf);
+        bad = 0;
+        for (int w = 0; w < 4; ++w) {
+            W m[32];
+            for (int q = 0; q < 32; ++q) m[q] = s[32 * w + q];
+            transpose32(m);
+            for (int k = 0; k < 32; ++k) {
+                uint32_t v = m[k] ^ rk[4 * ctx.nr + w];
+                bad += memcmp(&v, &ref[k][4 * w], 4) != 0;
+            }
+        }
+        if (verbose) printf("  bitsliced AES-%d kernel schedule: %s\n", bits, bad ? "failed" : "passed");
+        fails += bad;
+    }
+    return fails ? 1 : 0;
+}

@@ -1,0 +1,223 @@
+/*
+ * aes_bs.hip -- wave-level bitsliced AES encryption (CTR / ECB-encrypt) on
+ * the gfx950 VALU.
+ *
+ * Each lane holds 32 blocks as 128 bit-planes (one VGPR per state bit, see
+ * include/otc_bitslice.h); a wave therefore processes 64 x 32 = 2048 blocks
+ * (32 KiB) per task.  Slot k of lane l is block task*2048 + 64*k + l, so every
+ * plaintext load / ciphertext store of one slot is a coalesced 1 KiB
+ * dwordx4 wave access.
+ *
+ * CTR never transposes its input: task boundaries are aligned to the counter
+ * (the first task starts (ctr0 mod 2048) blocks "early" with those slots
+ * masked), so inside a task the counter of slot (k, l) is C + 64k + l with no
+ * carry out of bit 10.  Counter plane n is then
+ *     n < 6   : bit n of the lane id        (per lane)
+ *     6..10   : 0xAAAAAAAA, 0xCCCCCCCC, ... (a constant pattern over slots)
+ *     n >= 11 : bit n of C                  (wave uniform -> SGPR)
+ * and hipcc's uniformity analysis keeps the uniform planes on the scalar ALU:
+ * in round 1 only state byte 15 is per-lane, in round 2 only column 0, so
+ * ~27 of the 160 S-box evaluations of AES-128 cost no VALU at all ("counter
+ * mode caching", done by the compiler instead of by hand).
+ *
+ * The last round key is folded into the output XOR (ks ^ rk ^ pt as one
+ * v_bitop3 per word) after the single output transpose.
+ *
+ * No reference counterpart (the reference has only a T-table CUDA kernel,
+ * /root/reference/aes-gpu/Source/AES.cu:284-392).
+ */
+#include <hip/hip_runtime.h>
+
+#include "otc_bitslice.h"
+#include "otc_device.h"
+
+using namespace otc_dev;
+using namespace otc_bs;
+
+namespace {
+
+struct BsParams {
+    const uint8_t *in;
+    uint8_t *out;
+    uint64_t nblocks;   /* full blocks */
+    uint32_t tail;      /* CTR: trailing partial block bytes */
+    uint32_t wrap64;    /* CTR: 64-bit counter increment */
+    uint64_t shift;     /* CTR: ctr0.lo mod 2048 (virtual index = i + shift) */
+    Ctr128 cbase;       /* CTR: ctr0 with the low 11 bits cleared */
+};
+
+enum : int { BS_CTR = 0, BS_ECB = 1 };
+
+__device__ __forceinline__ W lane_mask(uint32_t lane, int n) { return (W)(0u - ((lane >> n) & 1u)); }
+
+template <int NR, int MODE>
+__global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t gwave = (uint64_t)blockIdx.x * 4u + wave;
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint64_t total = P.nblocks + (P.tail ? 1u : 0u);
+    const uint64_t shift = (MODE == BS_CTR) ? P.shift : 0;
+    const uint64_t vtotal = total + shift;
+
+    for (uint64_t task = gwave; task * 2048u < vtotal; task += nwaves) {
+        const uint64_t vbase = task * 2048u;
+        /* block index of slot k = vbase - shift + 64k + lane (may be out of range) */
+        const bool full = vbase >= shift && vbase + 2048u - shift <= P.nblocks; /* uniform */
+        W s[128];
+
+        if (MODE == BS_CTR) {
+            /* C = cbase + vbase (128-bit, or 64-bit wrap) */
+            uint64_t clo = P.cbase.lo + vbase;
+            uint64_t chi = P.cbase.hi + ((!P.wrap64 && clo < P.cbase.lo) ? 1u : 0u);
+#pragma unroll
+            for (int b = 0; b < 16; ++b) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int n = 8 * (15 - b) + i; /* numeric counter bit */
+                    W v;
+                    if (n < 6) {
+                        v = lane_mask(lane, n);
+                    } else if (n < 11) {
+                        constexpr W pat[5] = {0xAAAAAAAAu, 0xCCCCCCCCu, 0xF0F0F0F0u, 0xFF00FF00u, 0xFFFF0000u};
+                        v = pat[n - 6];
+                    } else if (n < 64) {
+                        v = (W)(0u - (uint32_t)((clo >> n) & 1u));
+                    } else {
+                        v = (W)(0u - (uint32_t)((chi >> (n - 64)) & 1u));
+                    }
+                    s[8 * b + i] = v;
+                }
+            }
+        } else {
+            /* ECB: load 32 blocks and transpose each word column */
+            const uint64_t i0 = vbase + lane;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                W m[32];
+#pragma unroll
+                for (int k = 0; k < 32; ++k) {
+                    const uint64_t i = i0 + 64u * k;
+                    m[k] = (full || i < P.nblocks) ? *(const uint32_t *)(P.in + 16 * i + 4 * w) : 0u;
+                }
+                transpose32(m);
+#pragma unroll
+                for (int q = 0; q < 32; ++q) s[32 * w + q] = m[q];
+            }
+        }
+
+        /* Round keys are laundered through an empty asm inside the task loop:
+         * otherwise hipcc hoists all 128*NR key masks out of the loop and
+         * spills them (SGPR -> VGPR lanes), costing occupancy and readlanes. */
+        uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+        for (int q = 0; q < 4 * (NR + 1); ++q) {
+            uint32_t v = K.rk[q];
+            asm volatile("" : "+s"(v));
+            rk[q] = v;
+        }
+        /* rounds (AddRoundKey folded into the S-boxes; last key folded below) */
+        encrypt_planes<NR, MODE == BS_CTR>(s, [&](int r, int p) -> W {
+            /* plane p = 32*w + q  <->  bit q of round-key word w */
+            return (W)(0u - ((rk[4 * r + (p >> 5)] >> (p & 31)) & 1u));
+        });
+
+        /* planes -> blocks (keystream / ciphertext without the last key) */
+#pragma unroll
+        for (int w = 0; w < 4; ++w) transpose32(s + 32 * w);
+
+        const uint32_t k0 = rk[4 * NR + 0], k1 = rk[4 * NR + 1], k2 = rk[4 * NR + 2],
+                       k3 = rk[4 * NR + 3];
+        const int64_t ibase = (int64_t)vbase - (int64_t)shift + (int64_t)lane;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            if ((k & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+            const int64_t si = ibase + 64 * k;
+            const bool ok = full || (si >= 0 && (uint64_t)si < P.nblocks);
+            const uint64_t i = (uint64_t)si;
+            if (MODE == BS_CTR) {
+                if (ok) {
+                    const uint4 x = *(const uint4 *)(P.in + 16 * i);
+                    uint4 o;
+                    o.x = x3(x.x, s[k], k0);
+                    o.y = x3(x.y, s[32 + k], k1);
+                    o.z = x3(x.z, s[64 + k], k2);
+                    o.w = x3(x.w, s[96 + k], k3);
+                    *(uint4 *)(P.out + 16 * i) = o;
+                } else if (si >= 0 && i == P.nblocks && P.tail) {
+                    const uint32_t ks[4] = {s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3};
+                    for (uint32_t n = 0; n < P.tail; ++n)
+                        P.out[16 * i + n] = P.in[16 * i + n] ^ (uint8_t)(ks[n >> 2] >> (8 * (n & 3)));
+                }
+            } else {
+                if (ok) {
+                    uint4 o = make_uint4(s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3);
+                    *(uint4 *)(P.out + 16 * i) = o;
+                }
+            }
+        }
+    }
+}
+
+int g_cus = 0;
+
+template <int NR, int MODE>
+hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
+{
+    if (g_cus <= 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_cus <= 0) g_cus = 256;
+    }
+    const uint64_t vt = P.nblocks + (P.tail ? 1 : 0) + (MODE == BS_CTR ? P.shift : 0);
+    const uint64_t tasks = (vt + 2047) / 2048;
+    uint64_t wgs = (tasks + 3) / 4;
+    const uint64_t cap = (uint64_t)g_cus * 2; /* 8 waves per CU (2 per SIMD) */
+    if (wgs > cap) wgs = cap;
+    if (wgs < 1) wgs = 1;
+    hipLaunchKernelGGL((k_aes_bs<NR, MODE>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
+    return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t launch(const BsParams &P, const otc_aes_key &K, hipStream_t st)
+{
+    switch (K.nr) {
+    case 10: return launch_nr<10, MODE>(P, K, st);
+    case 12: return launch_nr<12, MODE>(P, K, st);
+    case 14: return launch_nr<14, MODE>(P, K, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+} // namespace
+
+namespace otc_impl {
+
+hipError_t bs_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
+                  hipStream_t st)
+{
+    BsParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nblocks = nbytes / 16;
+    P.tail = (uint32_t)(nbytes % 16);
+    P.wrap64 = wrap64 ? 1u : 0u;
+    P.shift = c.lo & 2047u;
+    P.cbase.lo = c.lo & ~(uint64_t)2047u;
+    P.cbase.hi = c.hi;
+    return launch<BS_CTR>(P, K, st);
+}
+
+hipError_t bs_ecb_encrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, hipStream_t st)
+{
+    BsParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nblocks = nblocks;
+    return launch<BS_ECB>(P, K, st);
+}
+
+} // namespace otc_impl

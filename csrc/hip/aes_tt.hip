@@ -1,0 +1,530 @@
+/*
+ * aes_tt.hip -- AES T-table kernels for gfx950 with the table resident in LDS.
+ *
+ * Reference counterpart: AES_encrypt / AES_decrypt
+ * (/root/reference/aes-gpu/Source/AES.cu:284-502), one CUDA thread per block
+ * with four T tables in uncached global memory, a __shared__ state shared by
+ * the whole block (data race) and a launch that asked for the whole buffer as
+ * dynamic shared memory (never ran).  This file is a gfx950-first design:
+ *
+ *  * ONE 1 KiB T0 table replicated 64 ways in LDS (64 KiB): entry x of lane l
+ *    lives at byte (x << 8) | (l << 2), so the 64 lanes of a ds_read_b32
+ *    always hit 64 distinct banks -- conflict free for any data.  T1..T3 are
+ *    byte rotations of T0 (one v_alignbit each).
+ *  * The LDS address of a lookup is ONE v_perm_b32: byte 1 <- the state byte,
+ *    byte 0 <- lane*4, bytes 2..3 <- table select.  So a round costs per block
+ *    16 ds_read_b32 + 16 v_perm + 12 v_alignbit + 8 v_xor3/v_bitop3.
+ *  * Last round reuses T0: byte 1 of T0[x] is S[x]; two v_perm + one bitop3
+ *    assemble a column.
+ *  * Round keys arrive BY VALUE in the kernel arguments (otc_aes_key), i.e.
+ *    they are wave-uniform SGPR operands of the v_xor3s.
+ *  * Each lane carries B independent blocks (ILP across LDS latency); block
+ *    index = chunk + wave*64*B + b*64 + lane, so every global access is a
+ *    fully coalesced 1 KiB dwordx4 wave access.  Persistent grid-stride loop
+ *    amortises the 64 KiB table fill.
+ *  * Decryption keeps Td0 (64 KiB) + the inverse S-box replicated as words
+ *    (64 KiB) = 128 KiB, addressed with the same one-op v_perm (byte 2 selects
+ *    the table).
+ */
+#include <hip/hip_runtime.h>
+
+#include "otc_device.h"
+
+using namespace otc_dev;
+
+namespace {
+
+__device__ const AesTables g_tab = make_tables();
+
+constexpr uint32_t SEL(int k) { return 0x0c0c0000u | ((uint32_t)(4 + k) << 8); }
+/* second table (byte 2 of the address taken from lane word byte 2 = 1) */
+constexpr uint32_t SEL_HI(int k) { return 0x0c020000u | ((uint32_t)(4 + k) << 8); }
+
+__device__ __forceinline__ uint32_t lds_at(const uint32_t *tbl, uint32_t byte_addr)
+{
+    return *(const uint32_t *)((const char *)tbl + byte_addr);
+}
+
+template <int THREADS>
+__device__ __forceinline__ void fill_rep64(uint32_t *lds, const uint32_t *src)
+{
+    uint4 *l4 = reinterpret_cast<uint4 *>(lds);
+    for (int q = threadIdx.x; q < 4096; q += THREADS) {
+        uint32_t v = src[q >> 4];
+        l4[q] = make_uint4(v, v, v, v);
+    }
+}
+
+/* ---------------------------------------------------------------------------
+ * Round functions for B blocks at once (arrays are compile-time indexed)
+ * ------------------------------------------------------------------------- */
+template <int NR, int B>
+__device__ __forceinline__ void enc_rounds(const uint32_t *tbl, uint32_t lane4, const otc_aes_key &K,
+                                           uint32_t (&s)[B][4])
+{
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+        uint32_t t[B][4];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lane4, SEL(0)));
+                uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lane4, SEL(1)));
+                uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lane4, SEL(2)));
+                uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lane4, SEL(3)));
+                t[b][j] = xor3(xor3(a0, rotl8(a1), rotl16(a2)), rotl24(a3), K.rk[4 * r + j]);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
+    }
+    uint32_t t[B][4];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lane4, SEL(0)));
+            uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lane4, SEL(1)));
+            uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lane4, SEL(2)));
+            uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lane4, SEL(3)));
+            /* byte 1 of T0[x] is S[x] */
+            uint32_t lo = __builtin_amdgcn_perm(a1, a0, 0x0c0c0501u);
+            uint32_t hi = __builtin_amdgcn_perm(a3, a2, 0x05010c0cu);
+            t[b][j] = xor3(lo, hi, K.rk[4 * NR + j]); /* lo, hi have disjoint bytes */
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
+}
+
+template <int NR, int B>
+__device__ __forceinline__ void dec_rounds(const uint32_t *tbl, uint32_t lane4, uint32_t lane4_hi,
+                                           const otc_aes_key &K, uint32_t (&s)[B][4])
+{
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+        uint32_t t[B][4];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lane4, SEL(0)));
+                uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lane4, SEL(1)));
+                uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lane4, SEL(2)));
+                uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lane4, SEL(3)));
+                t[b][j] = xor3(xor3(a0, rotl8(a1), rotl16(a2)), rotl24(a3), K.rk[4 * r + j]);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
+    }
+    uint32_t t[B][4];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lane4_hi, SEL_HI(0)));
+            uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lane4_hi, SEL_HI(1)));
+            uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lane4_hi, SEL_HI(2)));
+            uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lane4_hi, SEL_HI(3)));
+            uint32_t lo = __builtin_amdgcn_perm(a1, a0, 0x0c0c0400u);
+            uint32_t hi = __builtin_amdgcn_perm(a3, a2, 0x04000c0cu);
+            t[b][j] = xor3(lo, hi, K.rk[4 * NR + j]); /* lo, hi have disjoint bytes */
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
+}
+
+__device__ __forceinline__ uint4 ld16(const uint8_t *p, uint64_t blk)
+{
+    return *reinterpret_cast<const uint4 *>(p + 16 * blk);
+}
+__device__ __forceinline__ void st16(uint8_t *p, uint64_t blk, uint4 v)
+{
+    *reinterpret_cast<uint4 *>(p + 16 * blk) = v;
+}
+
+enum : int { E_ECB = 0, E_CTR = 1, E_CFB_DEC = 2 };
+enum : int { D_ECB = 0, D_CBC = 1, D_CBC_SEG = 2 };
+
+struct EncParams {
+    const uint8_t *in;
+    uint8_t *out;
+    uint64_t nfull;   /* full 16-byte blocks */
+    uint32_t tail;    /* bytes of a trailing partial block (CTR) */
+    uint32_t wrap64;  /* CTR: 64-bit (RFC 3686) increment */
+    Ctr128 ctr;
+    uint32_t iv[4];   /* CFB: IV as LE words */
+};
+
+struct DecParams {
+    const uint8_t *in;
+    uint8_t *out;
+    uint64_t nfull;
+    uint32_t seg_shift; /* D_CBC_SEG: log2(blocks per segment) */
+    uint32_t pad;
+    Ctr128 iv;          /* CBC: IV (numeric BE); CBC_SEG: IV of segment 0 */
+};
+
+/* ---------------------------------------------------------------------------
+ * Encryption-direction kernel: ECB-enc, CTR, CFB128-dec
+ * ------------------------------------------------------------------------- */
+template <int NR, int MODE, int B, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[256 * 64];
+    fill_rep64<THREADS>(tbl, g_tab.te0);
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t lane4 = lane << 2;
+    constexpr uint64_t PER = (uint64_t)THREADS * B;
+    const uint64_t ntotal = P.nfull + (P.tail ? 1u : 0u);
+
+    for (uint64_t base = (uint64_t)blockIdx.x * PER; base < ntotal; base += (uint64_t)gridDim.x * PER) {
+        const bool full = base + PER <= P.nfull; /* wave-uniform */
+        const uint64_t i0 = base + (uint64_t)wave * 64u * B + lane;
+        uint32_t s[B][4];
+        uint4 x[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const uint64_t i = i0 + 64u * b;
+            const bool ok = full || i < P.nfull;
+            if (MODE == E_CTR) {
+                ctr_words(P.ctr, i, P.wrap64 != 0, s[b][0], s[b][1], s[b][2], s[b][3]);
+                x[b] = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
+            } else if (MODE == E_ECB) {
+                uint4 v = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
+                s[b][0] = v.x; s[b][1] = v.y; s[b][2] = v.z; s[b][3] = v.w;
+            } else { /* CFB decrypt: cipher input is the previous ciphertext */
+                x[b] = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
+                uint4 v = (i == 0) ? make_uint4(P.iv[0], P.iv[1], P.iv[2], P.iv[3])
+                                   : (ok ? ld16(P.in, i - 1) : make_uint4(0, 0, 0, 0));
+                s[b][0] = v.x; s[b][1] = v.y; s[b][2] = v.z; s[b][3] = v.w;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[b][j] ^= K.rk[j];
+        }
+
+        enc_rounds<NR, B>(tbl, lane4, K, s);
+
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const uint64_t i = i0 + 64u * b;
+            uint4 o;
+            if (MODE == E_ECB) {
+                o = make_uint4(s[b][0], s[b][1], s[b][2], s[b][3]);
+            } else {
+                o = make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]);
+            }
+            if (full || i < P.nfull) {
+                st16(P.out, i, o);
+            } else if (MODE == E_CTR && i == P.nfull && P.tail) {
+                const uint32_t ks[4] = {s[b][0], s[b][1], s[b][2], s[b][3]};
+                for (uint32_t n = 0; n < P.tail; ++n)
+                    P.out[16 * i + n] = P.in[16 * i + n] ^ (uint8_t)(ks[n >> 2] >> (8 * (n & 3)));
+            }
+        }
+    }
+}
+
+/* ---------------------------------------------------------------------------
+ * Decryption-direction kernel: ECB-dec, CBC-dec (single stream or power-of-2
+ * segments with per-segment IVs)
+ * ------------------------------------------------------------------------- */
+template <int NR, int MODE, int B, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_aes_dec_tt(DecParams P, otc_aes_key K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
+    fill_rep64<THREADS>(tbl, g_tab.td0);
+    fill_rep64<THREADS>(tbl + 256 * 64, g_tab.is4);
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t lane4 = lane << 2;
+    const uint32_t lane4_hi = lane4 | 0x10000u;
+    constexpr uint64_t PER = (uint64_t)THREADS * B;
+
+    for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nfull; base += (uint64_t)gridDim.x * PER) {
+        const bool full = base + PER <= P.nfull;
+        const uint64_t i0 = base + (uint64_t)wave * 64u * B + lane;
+        uint32_t s[B][4];
+        uint4 prev[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const uint64_t i = i0 + 64u * b;
+            const bool ok = full || i < P.nfull;
+            uint4 v = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
+            s[b][0] = v.x ^ K.rk[0]; s[b][1] = v.y ^ K.rk[1];
+            s[b][2] = v.z ^ K.rk[2]; s[b][3] = v.w ^ K.rk[3];
+            if (MODE == D_CBC || MODE == D_CBC_SEG) {
+                bool first;
+                Ctr128 ivv = P.iv;
+                if (MODE == D_CBC) {
+                    first = (i == 0);
+                } else {
+                    first = (i & ((1ull << P.seg_shift) - 1)) == 0;
+                    const uint64_t seg = i >> P.seg_shift;
+                    ivv.lo = P.iv.lo + seg;
+                    ivv.hi = P.iv.hi + (ivv.lo < P.iv.lo ? 1 : 0);
+                }
+                if (first) {
+                    uint32_t w0, w1, w2, w3;
+                    ctr_words(ivv, 0, false, w0, w1, w2, w3);
+                    prev[b] = make_uint4(w0, w1, w2, w3);
+                } else {
+                    prev[b] = ok ? ld16(P.in, i - 1) : make_uint4(0, 0, 0, 0);
+                }
+            }
+        }
+
+        dec_rounds<NR, B>(tbl, lane4, lane4_hi, K, s);
+
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const uint64_t i = i0 + 64u * b;
+            uint4 o = make_uint4(s[b][0], s[b][1], s[b][2], s[b][3]);
+            if (MODE != D_ECB) {
+                o.x ^= prev[b].x; o.y ^= prev[b].y; o.z ^= prev[b].z; o.w ^= prev[b].w;
+            }
+            if (full || i < P.nfull) st16(P.out, i, o);
+        }
+    }
+}
+
+/* ---------------------------------------------------------------------------
+ * CBC encryption over independent contiguous segments: one segment per lane
+ * slot, B segments per lane for ILP.  IV_s = iv0 + s.  Next plaintext block
+ * is prefetched one step ahead.
+ * ------------------------------------------------------------------------- */
+struct CbcSegParams {
+    const uint8_t *in;
+    uint8_t *out;
+    uint64_t seg_blocks;
+    uint64_t nseg;
+    Ctr128 iv0;
+};
+
+template <int NR, int B, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg(CbcSegParams P, otc_aes_key K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[256 * 64];
+    fill_rep64<THREADS>(tbl, g_tab.te0);
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t lane4 = lane << 2;
+    constexpr uint64_t PER = (uint64_t)THREADS * B;
+
+    for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nseg; base += (uint64_t)gridDim.x * PER) {
+        uint64_t seg[B];
+        bool live[B];
+        uint32_t c[B][4];
+        uint4 nxt[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            seg[b] = base + (uint64_t)wave * 64u * B + 64u * b + lane;
+            live[b] = seg[b] < P.nseg;
+            Ctr128 ivv;
+            ivv.lo = P.iv0.lo + seg[b];
+            ivv.hi = P.iv0.hi + (ivv.lo < P.iv0.lo ? 1 : 0);
+            ctr_words(ivv, 0, false, c[b][0], c[b][1], c[b][2], c[b][3]);
+            nxt[b] = (live[b] && P.seg_blocks) ? ld16(P.in, seg[b] * P.seg_blocks) : make_uint4(0, 0, 0, 0);
+        }
+        for (uint64_t j = 0; j < P.seg_blocks; ++j) {
+            uint32_t s[B][4];
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const uint4 p = nxt[b];
+                s[b][0] = p.x ^ c[b][0] ^ K.rk[0];
+                s[b][1] = p.y ^ c[b][1] ^ K.rk[1];
+                s[b][2] = p.z ^ c[b][2] ^ K.rk[2];
+                s[b][3] = p.w ^ c[b][3] ^ K.rk[3];
+                nxt[b] = (live[b] && j + 1 < P.seg_blocks) ? ld16(P.in, seg[b] * P.seg_blocks + j + 1)
+                                                           : make_uint4(0, 0, 0, 0);
+            }
+            enc_rounds<NR, B>(tbl, lane4, K, s);
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) c[b][q] = s[b][q];
+                if (live[b]) st16(P.out, seg[b] * P.seg_blocks + j, make_uint4(s[b][0], s[b][1], s[b][2], s[b][3]));
+            }
+        }
+    }
+}
+
+/* ---------------------------------------------------------------------------
+ * Host-side launch helpers
+ * ------------------------------------------------------------------------- */
+int g_num_cus = 0;
+
+int grid_for(uint64_t work_items, uint64_t per_wg, int wg_per_cu)
+{
+    if (g_num_cus <= 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    uint64_t need = (work_items + per_wg - 1) / per_wg;
+    uint64_t cap = (uint64_t)g_num_cus * (uint64_t)wg_per_cu;
+    if (need < 1) need = 1;
+    return (int)(need < cap ? need : cap);
+}
+
+constexpr int ENC_THREADS = 512;
+constexpr int ENC_B = 2;
+constexpr int DEC_THREADS = 1024;
+constexpr int DEC_B = 2;
+constexpr int SEG_THREADS = 512;
+constexpr int SEG_B = 2;
+
+template <int NR, int MODE>
+hipError_t launch_enc_nr(const EncParams &P, const otc_aes_key &K, hipStream_t st)
+{
+    const uint64_t nt = P.nfull + (P.tail ? 1 : 0);
+    int grid = grid_for(nt, (uint64_t)ENC_THREADS * ENC_B, 2);
+    hipLaunchKernelGGL((k_aes_enc_tt<NR, MODE, ENC_B, ENC_THREADS>), dim3(grid), dim3(ENC_THREADS), 0, st, P, K);
+    return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t launch_enc(const EncParams &P, const otc_aes_key &K, hipStream_t st)
+{
+    switch (K.nr) {
+    case 10: return launch_enc_nr<10, MODE>(P, K, st);
+    case 12: return launch_enc_nr<12, MODE>(P, K, st);
+    case 14: return launch_enc_nr<14, MODE>(P, K, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <int NR, int MODE>
+hipError_t launch_dec_nr(const DecParams &P, const otc_aes_key &K, hipStream_t st)
+{
+    int grid = grid_for(P.nfull, (uint64_t)DEC_THREADS * DEC_B, 1);
+    hipLaunchKernelGGL((k_aes_dec_tt<NR, MODE, DEC_B, DEC_THREADS>), dim3(grid), dim3(DEC_THREADS), 0, st, P, K);
+    return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t launch_dec(const DecParams &P, const otc_aes_key &K, hipStream_t st)
+{
+    switch (K.nr) {
+    case 10: return launch_dec_nr<10, MODE>(P, K, st);
+    case 12: return launch_dec_nr<12, MODE>(P, K, st);
+    case 14: return launch_dec_nr<14, MODE>(P, K, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <int NR>
+hipError_t launch_seg_nr(const CbcSegParams &P, const otc_aes_key &K, hipStream_t st)
+{
+    int grid = grid_for(P.nseg, (uint64_t)SEG_THREADS * SEG_B, 2);
+    hipLaunchKernelGGL((k_aes_cbc_enc_seg<NR, SEG_B, SEG_THREADS>), dim3(grid), dim3(SEG_THREADS), 0, st, P, K);
+    return hipGetLastError();
+}
+
+} // namespace
+
+/* ---- internal entry points used by engine.cpp ---------------------------- */
+namespace otc_impl {
+
+hipError_t tt_ecb_encrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, hipStream_t st)
+{
+    EncParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nblocks;
+    return launch_enc<E_ECB>(P, K, st);
+}
+
+hipError_t tt_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
+                  hipStream_t st)
+{
+    EncParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nbytes / 16;
+    P.tail = (uint32_t)(nbytes % 16);
+    P.wrap64 = wrap64 ? 1u : 0u;
+    P.ctr = c;
+    return launch_enc<E_CTR>(P, K, st);
+}
+
+hipError_t tt_cfb_decrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K,
+                          const uint32_t iv_le[4], hipStream_t st)
+{
+    EncParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nblocks;
+    for (int i = 0; i < 4; ++i) P.iv[i] = iv_le[i];
+    return launch_enc<E_CFB_DEC>(P, K, st);
+}
+
+hipError_t tt_ecb_decrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, hipStream_t st)
+{
+    DecParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nblocks;
+    return launch_dec<D_ECB>(P, K, st);
+}
+
+hipError_t tt_cbc_decrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, Ctr128 iv,
+                          hipStream_t st)
+{
+    DecParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nblocks;
+    P.iv = iv;
+    return launch_dec<D_CBC>(P, K, st);
+}
+
+hipError_t tt_cbc_decrypt_seg(const void *in, void *out, uint64_t nblocks, uint32_t seg_shift,
+                              const otc_aes_key &K, Ctr128 iv0, hipStream_t st)
+{
+    DecParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nblocks;
+    P.seg_shift = seg_shift;
+    P.iv = iv0;
+    return launch_dec<D_CBC_SEG>(P, K, st);
+}
+
+hipError_t tt_cbc_encrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,
+                              const otc_aes_key &K, Ctr128 iv0, hipStream_t st)
+{
+    CbcSegParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.seg_blocks = seg_blocks;
+    P.nseg = nseg;
+    P.iv0 = iv0;
+    switch (K.nr) {
+    case 10: return launch_seg_nr<10>(P, K, st);
+    case 12: return launch_seg_nr<12>(P, K, st);
+    case 14: return launch_seg_nr<14>(P, K, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+} // namespace otc_impl

@@ -1,0 +1,721 @@
+/*
+ * engine.cpp -- host runtime of the MI355X cipher engine (C API in otc.h).
+ *
+ * Replaces the reference's BlockCipher/AES host class
+ * (/root/reference/aes-gpu/Source/AES.cu:50-282), which did a synchronous
+ * cudaMalloc -> pageable H2D -> launch -> D2H -> cudaFree per call, queried
+ * device properties inside the timed region and never checked an error.
+ * Here:
+ *   - kernels are launched asynchronously on the caller's stream with the
+ *     expanded key as a by-value kernel argument (no per-call copies);
+ *   - the streaming engine (otc_engine_*) owns a pinned staging ring and three
+ *     HIP streams per device, so H2D(k+1) | kernel(k) | D2H(k-1) overlap;
+ *   - the multi-GPU path (otc_multi_*) shards one stream over devices, either
+ *     by direct per-GPU ingest or by an RCCL scatter/gather over xGMI from a
+ *     root GPU, with CTR counter offsets and CBC halos computed by the planner.
+ */
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "aes.h"
+#include "otc.h"
+#include "otc_device.h"
+
+using otc_dev::Ctr128;
+
+namespace otc_impl {
+hipError_t tt_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
+hipError_t tt_ecb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
+hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
+hipError_t tt_cfb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, hipStream_t);
+hipError_t tt_cbc_decrypt(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
+hipError_t tt_cbc_decrypt_seg(const void *, void *, uint64_t, uint32_t, const otc_aes_key &, Ctr128, hipStream_t);
+hipError_t tt_cbc_encrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
+hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
+hipError_t bs_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
+hipError_t k_xor(const void *, const void *, void *, size_t, hipStream_t);
+hipError_t k_fill_random(void *, size_t, uint64_t, hipStream_t);
+hipError_t k_checksum(const void *, size_t, uint64_t *, hipStream_t);
+hipError_t k_rc4_multi(const uint8_t *, int, size_t, size_t, size_t, const void *, void *, hipStream_t);
+} // namespace otc_impl
+
+/* ------------------------------------------------------------------------- */
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what)
+{
+    return set_err(OTC_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(expr)                                          \
+    do {                                                      \
+        hipError_t _e = (expr);                               \
+        if (_e != hipSuccess) return hip_fail(_e, #expr);     \
+    } while (0)
+
+#define RCCLCHK(expr)                                                                      \
+    do {                                                                                   \
+        ncclResult_t _r = (expr);                                                          \
+        if (_r != ncclSuccess)                                                             \
+            return set_err(OTC_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+    } while (0)
+
+Ctr128 ctr_from_bytes(const uint8_t c[16])
+{
+    Ctr128 v{0, 0};
+    for (int i = 0; i < 8; ++i) v.hi = (v.hi << 8) | c[i];
+    for (int i = 8; i < 16; ++i) v.lo = (v.lo << 8) | c[i];
+    return v;
+}
+
+Ctr128 ctr_add(Ctr128 c, uint64_t n, bool wrap64)
+{
+    uint64_t lo = c.lo + n;
+    if (!wrap64 && lo < c.lo) c.hi += 1;
+    c.lo = lo;
+    return c;
+}
+
+void ctr_to_bytes(Ctr128 c, uint8_t out[16])
+{
+    for (int i = 0; i < 8; ++i) out[i] = (uint8_t)(c.hi >> (56 - 8 * i));
+    for (int i = 0; i < 8; ++i) out[8 + i] = (uint8_t)(c.lo >> (56 - 8 * i));
+}
+
+int pick_impl(int impl, int bits)
+{
+    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE) return impl;
+    const char *env = getenv("OTC_IMPL");
+    if (env) {
+        if (!strcmp(env, "ttable")) return OTC_IMPL_TTABLE;
+        if (!strcmp(env, "bitslice")) return OTC_IMPL_BITSLICE;
+    }
+    (void)bits;
+    return OTC_IMPL_TTABLE; /* default: the measured winner (see docs/PERF.md) */
+}
+
+int check_key(const otc_aes_key *k, int dir)
+{
+    if (!k) return set_err(OTC_ERR_ARG, "null key");
+    if (k->nr != 10 && k->nr != 12 && k->nr != 14) return set_err(OTC_ERR_ARG, "bad key (nr)");
+    if (k->dir != dir)
+        return set_err(OTC_ERR_ARG, dir == OTC_DIR_ENCRYPT ? "key schedule is not an encryption schedule"
+                                                           : "key schedule is not a decryption schedule");
+    return OTC_OK;
+}
+
+} // namespace
+
+/* ---- errors / keys ------------------------------------------------------ */
+extern "C" const char *otc_last_error(void) { return g_err.c_str(); }
+
+extern "C" int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir)
+{
+    if (!k || !key) return set_err(OTC_ERR_ARG, "null argument");
+    aes_context ctx;
+    int r = (dir == OTC_DIR_ENCRYPT) ? aes_setkey_enc(&ctx, key, (unsigned)bits)
+                                     : aes_setkey_dec(&ctx, key, (unsigned)bits);
+    if (r) return set_err(OTC_ERR_ARG, "invalid AES key size (must be 128/192/256)");
+    memset(k, 0, sizeof *k);
+    aes_export_rk32(&ctx, k->rk);
+    k->nr = ctx.nr;
+    k->dir = dir;
+    k->bits = bits;
+    return OTC_OK;
+}
+
+/* ---- device ops --------------------------------------------------------- */
+extern "C" int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_aes_key *k, int impl,
+                           void *stream)
+{
+    if (nbytes % 16) return set_err(OTC_ERR_ARG, "ECB length must be a multiple of 16");
+    if (!k) return set_err(OTC_ERR_ARG, "null key");
+    if (nbytes == 0) return OTC_OK;
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    if (k->dir == OTC_DIR_ENCRYPT) {
+        e = (pick_impl(impl, k->bits) == OTC_IMPL_BITSLICE) ? otc_impl::bs_ecb_encrypt(in, out, nbytes / 16, *k, st)
+                                                            : otc_impl::tt_ecb_encrypt(in, out, nbytes / 16, *k, st);
+    } else {
+        e = otc_impl::tt_ecb_decrypt(in, out, nbytes / 16, *k, st);
+    }
+    if (e != hipSuccess) return hip_fail(e, "aes_ecb launch");
+    return OTC_OK;
+}
+
+static int ctr_common(const void *in, void *out, size_t nbytes, const otc_aes_key *k, Ctr128 c, bool wrap64,
+                      int impl, void *stream)
+{
+    int r = check_key(k, OTC_DIR_ENCRYPT);
+    if (r) return r;
+    if (nbytes == 0) return OTC_OK;
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = (pick_impl(impl, k->bits) == OTC_IMPL_BITSLICE) ? otc_impl::bs_ctr(in, out, nbytes, *k, c, wrap64, st)
+                                                                   : otc_impl::tt_ctr(in, out, nbytes, *k, c, wrap64, st);
+    if (e != hipSuccess) return hip_fail(e, "aes_ctr launch");
+    return OTC_OK;
+}
+
+extern "C" int otc_aes_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key *k, const uint8_t ctr0[16],
+                           uint64_t block_offset, int impl, void *stream)
+{
+    if (!ctr0) return set_err(OTC_ERR_ARG, "null counter");
+    return ctr_common(in, out, nbytes, k, ctr_add(ctr_from_bytes(ctr0), block_offset, false), false, impl, stream);
+}
+
+extern "C" int otc_aes_ctr_rfc3686(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                                   const uint8_t nonce[4], const uint8_t ivec[8], uint64_t block_offset, int impl,
+                                   void *stream)
+{
+    if (!nonce || !ivec) return set_err(OTC_ERR_ARG, "null nonce/ivec");
+    uint8_t cb[16];
+    memcpy(cb, nonce, 4);
+    memcpy(cb + 4, ivec, 8);
+    cb[12] = 0; cb[13] = 0; cb[14] = 0; cb[15] = 1;
+    return ctr_common(in, out, nbytes, k, ctr_add(ctr_from_bytes(cb), block_offset, true), true, impl, stream);
+}
+
+extern "C" int otc_aes_cbc_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                                   const uint8_t iv[16], void *stream)
+{
+    int r = check_key(k, OTC_DIR_DECRYPT);
+    if (r) return r;
+    if (nbytes % 16) return set_err(OTC_ERR_ARG, "CBC length must be a multiple of 16");
+    if (in == out && nbytes > 16) return set_err(OTC_ERR_ARG, "in-place CBC decryption is not supported");
+    if (nbytes == 0) return OTC_OK;
+    hipError_t e = otc_impl::tt_cbc_decrypt(in, out, nbytes / 16, *k, ctr_from_bytes(iv), (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "cbc_decrypt launch");
+    return OTC_OK;
+}
+
+extern "C" int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                            const otc_aes_key *k, const uint8_t iv0[16], void *stream)
+{
+    int r = check_key(k, OTC_DIR_ENCRYPT);
+    if (r) return r;
+    if (seg_bytes % 16) return set_err(OTC_ERR_ARG, "segment length must be a multiple of 16");
+    if (nseg == 0 || seg_bytes == 0) return OTC_OK;
+    hipError_t e = otc_impl::tt_cbc_encrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
+                                                (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "cbc_encrypt_segments launch");
+    return OTC_OK;
+}
+
+extern "C" int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                            const otc_aes_key *k, const uint8_t iv0[16], void *stream)
+{
+    int r = check_key(k, OTC_DIR_DECRYPT);
+    if (r) return r;
+    if (seg_bytes % 16) return set_err(OTC_ERR_ARG, "segment length must be a multiple of 16");
+    size_t sb = seg_bytes / 16;
+    if (sb == 0 || (sb & (sb - 1))) return set_err(OTC_ERR_ARG, "segment blocks must be a power of two");
+    if (in == out) return set_err(OTC_ERR_ARG, "in-place CBC decryption is not supported");
+    if (nseg == 0) return OTC_OK;
+    uint32_t shift = 0;
+    while ((1ull << shift) < sb) ++shift;
+    hipError_t e = otc_impl::tt_cbc_decrypt_seg(in, out, sb * nseg, shift, *k, ctr_from_bytes(iv0),
+                                                (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "cbc_decrypt_segments launch");
+    return OTC_OK;
+}
+
+extern "C" int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                                      const uint8_t iv[16], void *stream)
+{
+    int r = check_key(k, OTC_DIR_ENCRYPT);
+    if (r) return r;
+    if (nbytes % 16) return set_err(OTC_ERR_ARG, "CFB128 device path needs a multiple of 16 bytes");
+    if (in == out && nbytes > 16) return set_err(OTC_ERR_ARG, "in-place CFB decryption is not supported");
+    if (nbytes == 0) return OTC_OK;
+    uint32_t ivw[4];
+    memcpy(ivw, iv, 16);
+    hipError_t e = otc_impl::tt_cfb_decrypt(in, out, nbytes / 16, *k, ivw, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "cfb_decrypt launch");
+    return OTC_OK;
+}
+
+extern "C" int otc_xor(const void *a, const void *b, void *out, size_t nbytes, void *stream)
+{
+    if (nbytes == 0) return OTC_OK;
+    hipError_t e = otc_impl::k_xor(a, b, out, nbytes, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "xor launch");
+    return OTC_OK;
+}
+
+extern "C" int otc_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t len, size_t drop,
+                             const void *in, void *out, void *stream)
+{
+    if (keylen < 1 || keylen > 256) return set_err(OTC_ERR_ARG, "RC4 key length must be 1..256");
+    if (nstreams == 0 || len == 0) return OTC_OK;
+    hipError_t e = otc_impl::k_rc4_multi(keys, keylen, nstreams, len, drop, in, out, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "rc4_multi launch");
+    return OTC_OK;
+}
+
+extern "C" int otc_fill_random(void *p, size_t nbytes, uint64_t seed, void *stream)
+{
+    if (nbytes == 0) return OTC_OK;
+    hipError_t e = otc_impl::k_fill_random(p, nbytes, seed, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "fill_random launch");
+    return OTC_OK;
+}
+
+extern "C" int otc_checksum(const void *p, size_t nbytes, uint64_t *out_dev, void *stream)
+{
+    if (nbytes % 8) return set_err(OTC_ERR_ARG, "checksum length must be a multiple of 8");
+    hipError_t e = otc_impl::k_checksum(p, nbytes, out_dev, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "checksum launch");
+    return OTC_OK;
+}
+
+/* ---- device info -------------------------------------------------------- */
+extern "C" int otc_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+extern "C" int otc_device_cus(int dev)
+{
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+    return v;
+}
+extern "C" int otc_device_clock_khz(int dev)
+{
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeClockRate, dev) != hipSuccess) return -1;
+    return v;
+}
+extern "C" int otc_set_device(int dev)
+{
+    HIPCHK(hipSetDevice(dev));
+    return OTC_OK;
+}
+extern "C" int otc_device_sync(void)
+{
+    HIPCHK(hipDeviceSynchronize());
+    return OTC_OK;
+}
+
+/* ---- device memory helpers --------------------------------------------- */
+extern "C" void *otc_dev_malloc(size_t nbytes)
+{
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, nbytes ? nbytes : 16);
+    if (e != hipSuccess) {
+        hip_fail(e, "hipMalloc");
+        return nullptr;
+    }
+    return p;
+}
+extern "C" void otc_dev_free(void *p)
+{
+    if (p) (void)hipFree(p);
+}
+extern "C" int otc_memcpy(void *dst, const void *src, size_t nbytes, int kind)
+{
+    hipMemcpyKind k = kind == OTC_H2D ? hipMemcpyHostToDevice : kind == OTC_D2H ? hipMemcpyDeviceToHost
+                                                                                : hipMemcpyDeviceToDevice;
+    HIPCHK(hipMemcpy(dst, src, nbytes, k));
+    return OTC_OK;
+}
+extern "C" int otc_memset(void *p, int v, size_t nbytes)
+{
+    HIPCHK(hipMemset(p, v, nbytes));
+    return OTC_OK;
+}
+extern "C" int otc_time_op(otc_op_fn op, void *arg, int iters, double *ms_per_iter)
+{
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipEventRecord(a, nullptr));
+    for (int i = 0; i < iters; ++i) {
+        int r = op(arg);
+        if (r) return r;
+    }
+    HIPCHK(hipEventRecord(b, nullptr));
+    HIPCHK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (ms_per_iter) *ms_per_iter = iters > 0 ? ms / iters : 0.0;
+    return OTC_OK;
+}
+
+/* ---- pinned host memory ------------------------------------------------- */
+extern "C" int otc_host_register(void *p, size_t nbytes)
+{
+    HIPCHK(hipHostRegister(p, nbytes, hipHostRegisterDefault));
+    return OTC_OK;
+}
+extern "C" int otc_host_unregister(void *p)
+{
+    HIPCHK(hipHostUnregister(p));
+    return OTC_OK;
+}
+extern "C" void *otc_host_alloc_pinned(size_t nbytes)
+{
+    void *p = nullptr;
+    if (hipHostMalloc(&p, nbytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+extern "C" void otc_host_free_pinned(void *p)
+{
+    if (p) (void)hipHostFree(p);
+}
+
+/* ---- L3 streaming engine ------------------------------------------------ */
+struct otc_engine {
+    int device = 0;
+    size_t chunk = 0;
+    int depth = 0;                  /* ring slots */
+    std::vector<void *> d_in, d_out; /* device ring */
+    std::vector<void *> h_in, h_out; /* pinned staging ring */
+    hipStream_t s_h2d = nullptr, s_k = nullptr, s_d2h = nullptr;
+    std::vector<hipEvent_t> ev_h2d, ev_k, ev_d2h, ev_k0;
+};
+
+extern "C" otc_engine *otc_engine_create(int device, size_t chunk_bytes, int depth)
+{
+    if (chunk_bytes == 0) chunk_bytes = 256ull << 20;
+    chunk_bytes = (chunk_bytes + 15) & ~(size_t)15;
+    if (depth < 2) depth = 3;
+    otc_engine *e = new otc_engine();
+    e->device = device;
+    e->chunk = chunk_bytes;
+    e->depth = depth;
+    if (hipSetDevice(device) != hipSuccess) { set_err(OTC_ERR_HIP, "hipSetDevice"); delete e; return nullptr; }
+    bool ok = hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&e->s_k, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&e->s_d2h, hipStreamNonBlocking) == hipSuccess;
+    e->d_in.assign(depth, nullptr);
+    e->d_out.assign(depth, nullptr);
+    e->h_in.assign(depth, nullptr);
+    e->h_out.assign(depth, nullptr);
+    e->ev_h2d.assign(depth, nullptr);
+    e->ev_k.assign(depth, nullptr);
+    e->ev_d2h.assign(depth, nullptr);
+    e->ev_k0.assign(depth, nullptr);
+    for (int i = 0; ok && i < depth; ++i) {
+        ok = hipMalloc(&e->d_in[i], chunk_bytes) == hipSuccess && hipMalloc(&e->d_out[i], chunk_bytes) == hipSuccess &&
+             hipHostMalloc(&e->h_in[i], chunk_bytes, hipHostMallocDefault) == hipSuccess &&
+             hipHostMalloc(&e->h_out[i], chunk_bytes, hipHostMallocDefault) == hipSuccess &&
+             hipEventCreateWithFlags(&e->ev_h2d[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreate(&e->ev_k[i]) == hipSuccess &&
+             hipEventCreateWithFlags(&e->ev_d2h[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreate(&e->ev_k0[i]) == hipSuccess;
+    }
+    if (!ok) {
+        set_err(OTC_ERR_NOMEM, "engine allocation failed");
+        otc_engine_destroy(e);
+        return nullptr;
+    }
+    return e;
+}
+
+extern "C" void otc_engine_destroy(otc_engine *e)
+{
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->s_k) (void)hipStreamSynchronize(e->s_k);
+    if (e->s_h2d) (void)hipStreamSynchronize(e->s_h2d);
+    if (e->s_d2h) (void)hipStreamSynchronize(e->s_d2h);
+    for (int i = 0; i < e->depth; ++i) {
+        if (e->d_in[i]) (void)hipFree(e->d_in[i]);
+        if (e->d_out[i]) (void)hipFree(e->d_out[i]);
+        if (e->h_in[i]) (void)hipHostFree(e->h_in[i]);
+        if (e->h_out[i]) (void)hipHostFree(e->h_out[i]);
+        if (e->ev_h2d[i]) (void)hipEventDestroy(e->ev_h2d[i]);
+        if (e->ev_k[i]) (void)hipEventDestroy(e->ev_k[i]);
+        if (e->ev_d2h[i]) (void)hipEventDestroy(e->ev_d2h[i]);
+        if (e->ev_k0[i]) (void)hipEventDestroy(e->ev_k0[i]);
+    }
+    if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
+    if (e->s_k) (void)hipStreamDestroy(e->s_k);
+    if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
+    delete e;
+}
+
+static bool is_pinned(const void *p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+/* Launch the cipher on one device chunk. `blk0` = block offset of the chunk
+ * inside the whole stream; `prev` = for CBC-dec, the 16-byte ciphertext block
+ * preceding the chunk (the halo), as counter-style numeric IV. */
+static int run_chunk(int mode, const void *din, void *dout, size_t n, const otc_aes_key *k, const uint8_t ivc[16],
+                     uint64_t blk0, const uint8_t *halo, int impl, hipStream_t st)
+{
+    switch (mode) {
+    case OTC_MODE_CTR: return otc_aes_ctr(din, dout, n, k, ivc, blk0, impl, st);
+    case OTC_MODE_ECB: return otc_aes_ecb(din, dout, n, k, impl, st);
+    case OTC_MODE_CBC_DEC: return otc_aes_cbc_decrypt(din, dout, n, k, halo ? halo : ivc, st);
+    default: return set_err(OTC_ERR_ARG, "unsupported engine mode");
+    }
+}
+
+extern "C" int otc_engine_run(otc_engine *e, int mode, const void *host_in, void *host_out, size_t nbytes,
+                              const otc_aes_key *k, const uint8_t ivc[16], uint64_t block_offset, int impl,
+                              otc_stream_stats *stats)
+{
+    if (!e) return set_err(OTC_ERR_ARG, "null engine");
+    if (mode != OTC_MODE_CTR && nbytes % 16) return set_err(OTC_ERR_ARG, "length must be a multiple of 16");
+    if (mode == OTC_MODE_CBC_DEC && block_offset) return set_err(OTC_ERR_ARG, "CBC: pass the halo as iv instead");
+    HIPCHK(hipSetDevice(e->device));
+    auto t0 = std::chrono::steady_clock::now();
+    const bool pin_in = is_pinned(host_in), pin_out = is_pinned(host_out);
+    const size_t C = e->chunk;
+    const size_t nchunks = (nbytes + C - 1) / C;
+    const uint8_t *hin = (const uint8_t *)host_in;
+    uint8_t *hout = (uint8_t *)host_out;
+    double kms = 0.0;
+    std::vector<int> slot_used(e->depth, 0);
+
+    for (size_t c = 0; c < nchunks; ++c) {
+        const int s = (int)(c % e->depth);
+        const size_t off = c * C;
+        const size_t n = std::min(C, nbytes - off);
+        /* slot reuse: wait until the D2H that last used this slot finished */
+        if (slot_used[s]) {
+            HIPCHK(hipEventSynchronize(e->ev_d2h[s]));
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, e->ev_k0[s], e->ev_k[s]) == hipSuccess) kms += ms;
+            if (!pin_out) {
+                const size_t poff = (c - e->depth) * C;
+                memcpy(hout + poff, e->h_out[s], std::min(C, nbytes - poff));
+            }
+        }
+        const void *src = hin + off;
+        if (!pin_in) {
+            memcpy(e->h_in[s], hin + off, n);
+            src = e->h_in[s];
+        }
+        HIPCHK(hipMemcpyAsync(e->d_in[s], src, n, hipMemcpyHostToDevice, e->s_h2d));
+        HIPCHK(hipEventRecord(e->ev_h2d[s], e->s_h2d));
+        HIPCHK(hipStreamWaitEvent(e->s_k, e->ev_h2d[s], 0));
+        HIPCHK(hipEventRecord(e->ev_k0[s], e->s_k));
+        uint8_t halo[16];
+        const uint8_t *hp = nullptr;
+        if (mode == OTC_MODE_CBC_DEC && off > 0) {
+            memcpy(halo, hin + off - 16, 16); /* previous ciphertext block */
+            hp = halo;
+        }
+        int r = run_chunk(mode, e->d_in[s], e->d_out[s], n, k, ivc, block_offset + off / 16, hp, impl, e->s_k);
+        if (r) return r;
+        HIPCHK(hipEventRecord(e->ev_k[s], e->s_k));
+        HIPCHK(hipStreamWaitEvent(e->s_d2h, e->ev_k[s], 0));
+        void *dst = pin_out ? (void *)(hout + off) : e->h_out[s];
+        HIPCHK(hipMemcpyAsync(dst, e->d_out[s], n, hipMemcpyDeviceToHost, e->s_d2h));
+        HIPCHK(hipEventRecord(e->ev_d2h[s], e->s_d2h));
+        slot_used[s] = 1;
+    }
+    /* drain */
+    for (size_t c = (nchunks > (size_t)e->depth ? nchunks - e->depth : 0); c < nchunks; ++c) {
+        const int s = (int)(c % e->depth);
+        HIPCHK(hipEventSynchronize(e->ev_d2h[s]));
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, e->ev_k0[s], e->ev_k[s]) == hipSuccess) kms += ms;
+        if (!pin_out) {
+            const size_t off = c * C;
+            memcpy(hout + off, e->h_out[s], std::min(C, nbytes - off));
+        }
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    if (stats) {
+        stats->total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        stats->kernel_ms = kms;
+        stats->h2d_ms = stats->d2h_ms = 0.0;
+        stats->bytes = nbytes;
+        stats->chunks = (int)nchunks;
+    }
+    return OTC_OK;
+}
+
+/* ---- L4 multi-GPU (single process) -------------------------------------- */
+extern "C" int otc_multi_run(int ngpus, int strategy, int mode, const void *host_in, void *host_out, size_t nbytes,
+                             const otc_aes_key *k, const uint8_t ivc[16], int impl, size_t chunk_bytes,
+                             otc_multi_stats *stats)
+{
+    int ndev = otc_device_count();
+    if (ngpus < 1 || ngpus > ndev) return set_err(OTC_ERR_ARG, "ngpus out of range");
+    if (nbytes % 16 && mode != OTC_MODE_CTR) return set_err(OTC_ERR_ARG, "length must be a multiple of 16");
+    const size_t nblk = (nbytes + 15) / 16;
+    /* planner: contiguous block-aligned shards, remainder spread over the
+     * first shards (nothing dropped, unlike reference test.c:50) */
+    std::vector<size_t> boff(ngpus + 1, 0);
+    for (int g = 0; g < ngpus; ++g) boff[g + 1] = boff[g] + nblk / ngpus + ((size_t)g < nblk % ngpus ? 1 : 0);
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = OTC_OK;
+
+    if (strategy == 0) {
+        std::vector<std::thread> th;
+        std::vector<int> res(ngpus, 0);
+        for (int g = 0; g < ngpus; ++g) {
+            th.emplace_back([&, g]() {
+                const size_t b0 = std::min(boff[g] * 16, nbytes), b1 = std::min(boff[g + 1] * 16, nbytes);
+                if (b1 <= b0) return;
+                otc_engine *e = otc_engine_create(g, chunk_bytes, 3);
+                if (!e) { res[g] = OTC_ERR_NOMEM; return; }
+                uint8_t iv_local[16];
+                const uint8_t *ivp = ivc;
+                uint64_t bo = 0;
+                if (mode == OTC_MODE_CBC_DEC) {
+                    if (b0 > 0) { memcpy(iv_local, (const uint8_t *)host_in + b0 - 16, 16); ivp = iv_local; }
+                } else if (mode == OTC_MODE_CTR) {
+                    bo = b0 / 16;
+                }
+                res[g] = otc_engine_run(e, mode, (const uint8_t *)host_in + b0, (uint8_t *)host_out + b0, b1 - b0, k,
+                                        ivp, bo, impl, nullptr);
+                otc_engine_destroy(e);
+            });
+        }
+        for (auto &t : th) t.join();
+        for (int g = 0; g < ngpus; ++g)
+            if (res[g]) rc = res[g];
+    } else {
+        /* RCCL root scatter/gather, chunked so the root never holds more than
+         * 2 x ngpus x per-GPU chunk.  ncclScatter needs equal counts: the
+         * stream is processed in rounds of ngpus*S bytes; the final partial
+         * round is padded. */
+        if (mode == OTC_MODE_CBC_DEC) {
+            /* halo handling needs the previous block per shard; done host side */
+        }
+        std::vector<ncclComm_t> comms(ngpus);
+        std::vector<int> devs(ngpus);
+        for (int g = 0; g < ngpus; ++g) devs[g] = g;
+        RCCLCHK(ncclCommInitAll(comms.data(), ngpus, devs.data()));
+        size_t S = chunk_bytes ? chunk_bytes : (size_t)64 << 20; /* per-GPU bytes per round */
+        S = (S + 15) & ~(size_t)15;
+        const size_t round = S * (size_t)ngpus;
+        std::vector<hipStream_t> st(ngpus);
+        std::vector<void *> dsh(ngpus), dsh_out(ngpus);
+        void *root_in = nullptr, *root_out = nullptr;
+        for (int g = 0; g < ngpus; ++g) {
+            HIPCHK(hipSetDevice(g));
+            HIPCHK(hipStreamCreateWithFlags(&st[g], hipStreamNonBlocking));
+            HIPCHK(hipMalloc(&dsh[g], S));
+            HIPCHK(hipMalloc(&dsh_out[g], S));
+            if (g == 0) {
+                HIPCHK(hipMalloc(&root_in, round));
+                HIPCHK(hipMalloc(&root_out, round));
+            }
+        }
+        const uint8_t *hin = (const uint8_t *)host_in;
+        uint8_t *hout = (uint8_t *)host_out;
+        for (size_t off = 0; off < nbytes && rc == OTC_OK; off += round) {
+            const size_t n = std::min(round, nbytes - off);
+            HIPCHK(hipSetDevice(0));
+            if (n < round) HIPCHK(hipMemsetAsync(root_in, 0, round, st[0]));
+            HIPCHK(hipMemcpyAsync(root_in, hin + off, n, hipMemcpyHostToDevice, st[0]));
+            RCCLCHK(ncclGroupStart());
+            for (int g = 0; g < ngpus; ++g)
+                RCCLCHK(ncclScatter(root_in, dsh[g], S, ncclUint8, 0, comms[g], st[g]));
+            RCCLCHK(ncclGroupEnd());
+            for (int g = 0; g < ngpus; ++g) {
+                HIPCHK(hipSetDevice(g));
+                const size_t goff = off + (size_t)g * S;
+                if (goff >= nbytes) continue;
+                const size_t gn = std::min(S, nbytes - goff);
+                uint8_t halo[16];
+                const uint8_t *hp = nullptr;
+                if (mode == OTC_MODE_CBC_DEC && goff > 0) {
+                    memcpy(halo, hin + goff - 16, 16);
+                    hp = halo;
+                }
+                int r = run_chunk(mode, dsh[g], dsh_out[g], gn, k, ivc, goff / 16, hp, impl, st[g]);
+                if (r) { rc = r; break; }
+            }
+            RCCLCHK(ncclGroupStart());
+            for (int g = 0; g < ngpus; ++g)
+                RCCLCHK(ncclGather(dsh_out[g], root_out, S, ncclUint8, 0, comms[g], st[g]));
+            RCCLCHK(ncclGroupEnd());
+            HIPCHK(hipSetDevice(0));
+            HIPCHK(hipMemcpyAsync(hout + off, root_out, n, hipMemcpyDeviceToHost, st[0]));
+            HIPCHK(hipStreamSynchronize(st[0]));
+        }
+        for (int g = 0; g < ngpus; ++g) {
+            (void)hipSetDevice(g);
+            (void)hipStreamSynchronize(st[g]);
+            (void)hipFree(dsh[g]);
+            (void)hipFree(dsh_out[g]);
+            (void)hipStreamDestroy(st[g]);
+            ncclCommDestroy(comms[g]);
+        }
+        (void)hipSetDevice(0);
+        (void)hipFree(root_in);
+        (void)hipFree(root_out);
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    if (stats) {
+        stats->total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        stats->gbps = stats->total_ms > 0 ? (double)nbytes / (stats->total_ms * 1e6) : 0.0;
+        stats->ngpus = ngpus;
+        stats->strategy = strategy;
+    }
+    return rc;
+}
+
+extern "C" int otc_multi_ctr_resident(int ngpus, void *const *dev_bufs, size_t shard_bytes, const otc_aes_key *k,
+                                      const uint8_t ctr0[16], int impl, double *elapsed_ms)
+{
+    if (ngpus < 1 || ngpus > otc_device_count()) return set_err(OTC_ERR_ARG, "ngpus out of range");
+    if (shard_bytes % 16) return set_err(OTC_ERR_ARG, "shard must be a multiple of 16");
+    std::vector<hipStream_t> st(ngpus);
+    for (int g = 0; g < ngpus; ++g) {
+        HIPCHK(hipSetDevice(g));
+        HIPCHK(hipStreamCreateWithFlags(&st[g], hipStreamNonBlocking));
+        HIPCHK(hipDeviceSynchronize());
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    for (int g = 0; g < ngpus; ++g) {
+        HIPCHK(hipSetDevice(g));
+        int r = otc_aes_ctr(dev_bufs[g], dev_bufs[g], shard_bytes, k, ctr0, (uint64_t)g * (shard_bytes / 16), impl, st[g]);
+        if (r) return r;
+    }
+    for (int g = 0; g < ngpus; ++g) {
+        HIPCHK(hipSetDevice(g));
+        HIPCHK(hipStreamSynchronize(st[g]));
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    for (int g = 0; g < ngpus; ++g) {
+        (void)hipSetDevice(g);
+        (void)hipStreamDestroy(st[g]);
+    }
+    if (elapsed_ms) *elapsed_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    return OTC_OK;
+}
+
+extern "C" const char *otc_build_info(void)
+{
+    return "otc: MI355X (gfx950) cipher engine; kernels: aes_tt (LDS T-table), aes_bs (bitsliced VALU), "
+           "rc4_multi, xor; runtime: pinned 3-stream pipeline, RCCL multi-GPU";
+}

@@ -1,0 +1,106 @@
+/*
+ * otc_device.h -- device-side helpers shared by the gfx950 kernels.
+ *
+ * AES tables are generated at COMPILE time (constexpr, FIPS-197 definition)
+ * into __device__ read-only globals; each workgroup replicates what it needs
+ * into LDS at kernel start (csrc/hip/aes_tt.hip).  Nothing is uploaded per
+ * launch, unlike the reference which re-copied the key schedule and kept the
+ * tables in uncached global memory (/root/reference/aes-gpu/Source/AES.tab:689,
+ * AES.cu:222).
+ */
+#ifndef OTC_DEVICE_H
+#define OTC_DEVICE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "otc.h"
+
+namespace otc_dev {
+
+struct AesTables {
+    uint8_t sb[256];
+    uint8_t isb[256];
+    uint32_t te0[256];
+    uint32_t td0[256];
+    uint32_t is4[256]; /* inverse S-box byte replicated into all 4 bytes */
+};
+
+constexpr uint8_t xt(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
+constexpr uint8_t gmul(uint8_t a, uint8_t b)
+{
+    uint8_t r = 0;
+    for (int i = 0; i < 8; ++i) {
+        if (b & 1) r ^= a;
+        a = xt(a);
+        b >>= 1;
+    }
+    return r;
+}
+
+constexpr AesTables make_tables()
+{
+    AesTables t{};
+    uint8_t ex[256]{}, lg[256]{};
+    uint8_t v = 1;
+    for (int i = 0; i < 255; ++i) {
+        ex[i] = v;
+        lg[v] = (uint8_t)i;
+        v = (uint8_t)(v ^ xt(v));
+    }
+    for (int a = 0; a < 256; ++a) {
+        uint8_t inv = a ? ex[(255 - lg[a]) % 255] : 0;
+        uint8_t s = inv, r = inv;
+        for (int k = 0; k < 4; ++k) {
+            r = (uint8_t)((r << 1) | (r >> 7));
+            s ^= r;
+        }
+        s ^= 0x63;
+        t.sb[a] = s;
+        t.isb[s] = (uint8_t)a;
+    }
+    for (int a = 0; a < 256; ++a) {
+        uint8_t s = t.sb[a];
+        t.te0[a] = (uint32_t)gmul(s, 2) | ((uint32_t)s << 8) | ((uint32_t)s << 16) |
+                   ((uint32_t)gmul(s, 3) << 24);
+        uint8_t u = t.isb[a];
+        t.td0[a] = (uint32_t)gmul(u, 14) | ((uint32_t)gmul(u, 9) << 8) |
+                   ((uint32_t)gmul(u, 13) << 16) | ((uint32_t)gmul(u, 11) << 24);
+        t.is4[a] = (uint32_t)u * 0x01010101u;
+    }
+    return t;
+}
+
+/* byte swap via v_perm_b32 (one VALU op) */
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); }
+/* 3-input XOR in one v_bitop3_b32 (gfx950 has no v_xor3_b32; hipcc does not
+ * fuse pure XOR chains by itself) */
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 24); }
+__device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+__device__ __forceinline__ uint32_t rotl24(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 8); }
+
+/* 128-bit counter value (numeric, big-endian semantics) */
+struct Ctr128 {
+    uint64_t hi, lo;
+};
+
+/* counter + idx; `wrap64` keeps the carry out of the high half (RFC 3686 /
+ * AES-NI layout of the reference, aesni.c:139-143). */
+__device__ __forceinline__ void ctr_words(const Ctr128 &c, uint64_t idx, bool wrap64, uint32_t &w0,
+                                          uint32_t &w1, uint32_t &w2, uint32_t &w3)
+{
+    uint64_t lo = c.lo + idx;
+    uint64_t hi = c.hi + ((!wrap64 && lo < c.lo) ? 1ull : 0ull);
+    w0 = bswap32((uint32_t)(hi >> 32));
+    w1 = bswap32((uint32_t)hi);
+    w2 = bswap32((uint32_t)(lo >> 32));
+    w3 = bswap32((uint32_t)lo);
+}
+
+} // namespace otc_dev
+
+#endif

@@ -1,0 +1,222 @@
+/*
+ * stream_ops.hip -- byte-stream kernels for gfx950:
+ *   * k_xor        : the device arc4_crypt combiner, out = in ^ keystream
+ *                    (reference arc4.c:101-112 / test.c:44-58 did this with
+ *                    pthreads); 16 B per lane, grid-stride, HBM-bound.
+ *   * k_rc4_multi  : many independent RC4 streams, one per lane, S-box in LDS
+ *                    (the "P3 many-stream" design of SURVEY.md section 2.4:
+ *                    RC4's PRGA is serial per stream, so GPU throughput comes
+ *                    from thousands of concurrent streams).
+ *   * k_fill_random / k_checksum: synthetic data + verification helpers.
+ *
+ * RC4 LDS layout: byte x of lane l's permutation lives in dword
+ * (x >> 2) * 64 + l, byte (x & 3) -- i.e. byte address
+ * ((x >> 2) << 8) | (l << 2) | (x & 3).  Every lane owns one bank (l mod 32),
+ * so the data-dependent S[j] / S[S[i]+S[j]] reads of a wave never conflict.
+ * 16 KiB per wave; one wave per workgroup, up to 10 workgroups per CU.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+__global__ __launch_bounds__(256) void k_xor_kernel(const uint8_t *a, const uint8_t *b, uint8_t *o, uint64_t n)
+{
+    const uint64_t n16 = n / 16;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+        uint4 x = reinterpret_cast<const uint4 *>(a)[i];
+        uint4 y = reinterpret_cast<const uint4 *>(b)[i];
+        reinterpret_cast<uint4 *>(o)[i] = make_uint4(x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 15)) {
+        const uint64_t j = n16 * 16 + threadIdx.x;
+        o[j] = a[j] ^ b[j];
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_fill_kernel(uint8_t *p, uint64_t n, uint64_t seed)
+{
+    const uint64_t n16 = n / 16;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t s = splitmix(seed);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+        uint64_t a = splitmix(s ^ (2 * i)), b = splitmix(s ^ (2 * i + 1));
+        reinterpret_cast<uint4 *>(p)[i] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 15)) {
+        const uint64_t j = n16 * 16 + threadIdx.x;
+        p[j] = (uint8_t)splitmix(s ^ (0xFFFFull << 48) ^ j);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_checksum_kernel(const uint64_t *p, uint64_t nw, unsigned long long *out)
+{
+    uint64_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += stride)
+        acc ^= p[i] * (0x9E3779B97F4A7C15ull | 1) + (i << 1); /* position-dependent fold */
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicXor(out, (unsigned long long)acc);
+}
+
+/* ---- RC4 many-stream --------------------------------------------------- */
+__device__ __forceinline__ uint32_t sbox_addr(uint32_t x, uint32_t lane4)
+{
+    /* ((x & 0xFC) << 6) | (x & 3) | lane4 ; bits of x above 7 are ignored */
+    uint32_t t = (x << 6) & 0x3F00u;
+    return t | (x & 3u) | lane4;
+}
+
+__global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keylen, uint64_t nstreams, uint64_t len,
+                                                   uint64_t drop, const uint8_t *in, uint8_t *out)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t S[64 * 256];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t lane4 = lane << 2;
+    const uint64_t sid = (uint64_t)blockIdx.x * 64 + lane;
+    const bool live = sid < nstreams;
+
+    /* identity permutation: dword q of lane l = bytes 4q..4q+3 */
+    for (uint32_t q = 0; q < 64; ++q)
+        *reinterpret_cast<uint32_t *>(S + ((q << 8) | lane4)) = 0x03020100u + 0x04040404u * q;
+
+    /* KSA */
+    const uint8_t *key = keys + (live ? sid : 0) * (uint64_t)keylen;
+    uint32_t j = 0;
+    int kpos = 0;
+    for (uint32_t i = 0; i < 256; ++i) {
+        const uint32_t ai = sbox_addr(i, lane4);
+        const uint32_t a = S[ai];
+        j = (j + a + key[kpos]) & 0xFFu;
+        if (++kpos == keylen) kpos = 0;
+        const uint32_t aj = sbox_addr(j, lane4);
+        const uint32_t b = S[aj];
+        S[ai] = (uint8_t)b;
+        S[aj] = (uint8_t)a;
+    }
+
+    /* PRGA */
+    uint32_t i = 0;
+    j = 0;
+    for (uint64_t n = 0; n < drop; ++n) {
+        i = (i + 1) & 0xFFu;
+        const uint32_t ai = sbox_addr(i, lane4);
+        const uint32_t a = S[ai];
+        j = (j + a) & 0xFFu;
+        const uint32_t aj = sbox_addr(j, lane4);
+        const uint32_t b = S[aj];
+        S[ai] = (uint8_t)b;
+        S[aj] = (uint8_t)a;
+    }
+    const uint64_t base = (live ? sid : 0) * len;
+    uint64_t n = 0;
+    for (; n + 16 <= len; n += 16) {
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int bidx = 0; bidx < 4; ++bidx) {
+                i = (i + 1) & 0xFFu;
+                const uint32_t ai = sbox_addr(i, lane4);
+                const uint32_t a = S[ai];
+                j = (j + a) & 0xFFu;
+                const uint32_t aj = sbox_addr(j, lane4);
+                const uint32_t b = S[aj];
+                S[ai] = (uint8_t)b;
+                S[aj] = (uint8_t)a;
+                v |= (uint32_t)S[sbox_addr(a + b, lane4)] << (8 * bidx);
+            }
+            w[q] = v;
+        }
+        if (live) {
+            uint4 o = make_uint4(w[0], w[1], w[2], w[3]);
+            if (((base + n) & 15) == 0) {
+                if (in) {
+                    const uint4 x = *reinterpret_cast<const uint4 *>(in + base + n);
+                    o.x ^= x.x; o.y ^= x.y; o.z ^= x.z; o.w ^= x.w;
+                }
+                *reinterpret_cast<uint4 *>(out + base + n) = o;
+            } else {
+                for (int q = 0; q < 16; ++q) {
+                    uint8_t kb = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+                    out[base + n + q] = in ? (uint8_t)(in[base + n + q] ^ kb) : kb;
+                }
+            }
+        }
+    }
+    for (; n < len; ++n) {
+        i = (i + 1) & 0xFFu;
+        const uint32_t ai = sbox_addr(i, lane4);
+        const uint32_t a = S[ai];
+        j = (j + a) & 0xFFu;
+        const uint32_t aj = sbox_addr(j, lane4);
+        const uint32_t b = S[aj];
+        S[ai] = (uint8_t)b;
+        S[aj] = (uint8_t)a;
+        const uint8_t kb = S[sbox_addr(a + b, lane4)];
+        if (live) out[base + n] = in ? (uint8_t)(in[base + n] ^ kb) : kb;
+    }
+}
+
+int g_cus_s = 0;
+int grid_stream(uint64_t items, int per_cu)
+{
+    if (g_cus_s <= 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&g_cus_s, hipDeviceAttributeMultiprocessorCount, dev);
+        if (g_cus_s <= 0) g_cus_s = 256;
+    }
+    uint64_t need = (items + 255) / 256;
+    uint64_t cap = (uint64_t)g_cus_s * per_cu;
+    if (need < 1) need = 1;
+    return (int)(need < cap ? need : cap);
+}
+
+} // namespace
+
+namespace otc_impl {
+
+hipError_t k_xor(const void *a, const void *b, void *out, size_t n, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_xor_kernel, dim3(grid_stream(n / 16, 8)), dim3(256), 0, st, (const uint8_t *)a,
+                       (const uint8_t *)b, (uint8_t *)out, (uint64_t)n);
+    return hipGetLastError();
+}
+
+hipError_t k_fill_random(void *p, size_t n, uint64_t seed, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_fill_kernel, dim3(grid_stream(n / 16, 8)), dim3(256), 0, st, (uint8_t *)p, (uint64_t)n, seed);
+    return hipGetLastError();
+}
+
+hipError_t k_checksum(const void *p, size_t n, uint64_t *out, hipStream_t st)
+{
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(uint64_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_checksum_kernel, dim3(grid_stream(n / 8, 8)), dim3(256), 0, st, (const uint64_t *)p,
+                       (uint64_t)(n / 8), (unsigned long long *)out);
+    return hipGetLastError();
+}
+
+hipError_t k_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t len, size_t drop, const void *in,
+                       void *out, hipStream_t st)
+{
+    const uint64_t wgs = (nstreams + 63) / 64;
+    hipLaunchKernelGGL(k_rc4_kernel, dim3((unsigned)wgs), dim3(64), 0, st, keys, keylen, (uint64_t)nstreams,
+                       (uint64_t)len, (uint64_t)drop, (const uint8_t *)in, (uint8_t *)out);
+    return hipGetLastError();
+}
+
+} // namespace otc_impl

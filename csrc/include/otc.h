@@ -1,0 +1,214 @@
+/*
+ * otc.h -- public C API of the MI355X (gfx950) bulk symmetric-cipher engine.
+ *
+ * Layers (re-designed MI355X-first):
+ *   L1/L2 device kernels  -> otc_aes_* / otc_rc4_* / otc_xor  (device pointers,
+ *                            asynchronous on a caller-supplied hipStream_t)
+ *   L3 engine runtime     -> otc_ctx_* (persistent per-device state, tables,
+ *                            streams, pinned staging ring) and otc_stream_*
+ *                            (host-memory pipelined H2D | kernel | D2H)
+ *   L4 multi-GPU          -> otc_multi_* (single-process RCCL over xGMI) ; the
+ *                            one-process-per-GPU path lives in
+ *                            our_tree_amd/parallel (torch.distributed / RCCL)
+ *
+ * Reference counterparts: BlockCipher/AES host class
+ * (/root/reference/aes-gpu/Source/BlockCipher.h:48-107, AES.h:84-147,
+ * AES.cu:50-282) and the CUDA kernels (AES.cu:284-502).  Unlike the reference,
+ * every entry point returns an error code (no silent launch failures,
+ * AES.cu:250), nothing is allocated per call, and any length is accepted.
+ *
+ * Streams are passed as `void *` (a hipStream_t; NULL = default stream) so the
+ * header is usable from plain C and from ctypes.
+ */
+#ifndef OTC_H
+#define OTC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- errors -------------------------------------------------------------- */
+#define OTC_OK 0
+#define OTC_ERR_ARG -1        /* bad argument (length, key size, alignment) */
+#define OTC_ERR_HIP -2        /* a HIP runtime call failed; see otc_last_error() */
+#define OTC_ERR_RCCL -3       /* an RCCL call failed */
+#define OTC_ERR_UNSUPPORTED -4
+#define OTC_ERR_NOMEM -5
+
+const char *otc_last_error(void);
+
+/* ---- keys ---------------------------------------------------------------- */
+#define OTC_DIR_ENCRYPT 1
+#define OTC_DIR_DECRYPT 0
+
+/* Expanded key passed BY VALUE as a kernel argument, so round keys land in
+ * SGPRs (wave-uniform) with no per-launch copy.  rk: LE column words as in
+ * aes_export_rk32(); for OTC_DIR_DECRYPT the equivalent-inverse schedule. */
+typedef struct {
+    uint32_t rk[60];
+    int32_t nr;   /* 10 / 12 / 14 */
+    int32_t dir;  /* OTC_DIR_* */
+    int32_t bits; /* 128 / 192 / 256 */
+    int32_t pad;
+} otc_aes_key;
+
+int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
+
+/* ---- implementation selection ------------------------------------------- */
+#define OTC_IMPL_AUTO 0
+#define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
+#define OTC_IMPL_BITSLICE 2 /* 32-block-per-lane bitsliced VALU kernel */
+
+/* ---- device ops (device pointers; async on `stream`) ---------------------
+ * All functions accept any byte length; the trailing partial block of CTR is
+ * handled inside the kernel.  ECB/CBC lengths must be multiples of 16.
+ * In-place (in == out) is allowed except for otc_aes_cbc_decrypt and
+ * otc_aes_cfb128_decrypt (they read the previous ciphertext block).
+ */
+int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_aes_key *k, int impl,
+                void *stream);
+
+/* CTR with a full 128-bit big-endian counter starting at ctr0 (the semantics
+ * of aes_crypt_ctr with nc_off == 0).  `block_offset` is added to ctr0 first
+ * (128-bit add with carry) -- this is how shards of one stream are encrypted
+ * independently. */
+int otc_aes_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                const uint8_t ctr0[16], uint64_t block_offset, int impl, void *stream);
+
+/* CTR with the AES-NI/RFC 3686 counter layout nonce[4] || ivec[8] || BE32(1),
+ * the low 8 bytes incremented as a 64-bit big-endian integer
+ * (reference aesni.c:120-152). */
+int otc_aes_ctr_rfc3686(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                        const uint8_t nonce[4], const uint8_t ivec[8], uint64_t block_offset,
+                        int impl, void *stream);
+
+/* CBC decryption (parallel): P_i = D(C_i) ^ C_{i-1}, C_{-1} = iv. */
+int otc_aes_cbc_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                        const uint8_t iv[16], void *stream);
+
+/* CBC encryption over `nseg` independent segments of `seg_bytes` each
+ * (contiguous, segment s at offset s*seg_bytes).  Segment s uses
+ * IV_s = iv0 + s (128-bit big-endian add), the "plain64"-style sector IV.
+ * A single segment (nseg == 1) is exact single-stream CBC, serial. */
+int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                 const otc_aes_key *k, const uint8_t iv0[16], void *stream);
+/* Same, decryption side (fully parallel). */
+int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                 const otc_aes_key *k, const uint8_t iv0[16], void *stream);
+
+/* CFB128 decryption (parallel): P_i = C_i ^ E(C_{i-1}); nbytes % 16 == 0. */
+int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                           const uint8_t iv[16], void *stream);
+
+/* out = a ^ b (the device arc4_crypt combiner). */
+int otc_xor(const void *a, const void *b, void *out, size_t nbytes, void *stream);
+
+/* Many independent RC4 streams, one per lane: stream s uses key
+ * keys[s*keylen .. +keylen) (device memory) and produces `len` bytes.
+ * If `in` is non-NULL: out[s*len + n] = in[s*len + n] ^ ks_s[n], else the raw
+ * keystream is written.  `drop` keystream bytes are discarded first
+ * (RC4-drop[n]). */
+int otc_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t len, size_t drop,
+                  const void *in, void *out, void *stream);
+
+/* Deterministic pseudo-random fill (synthetic plaintext). */
+int otc_fill_random(void *p, size_t nbytes, uint64_t seed, void *stream);
+
+/* 64-bit XOR-fold checksum of a device buffer (nbytes % 8 == 0) into
+ * *out_dev (device pointer to one uint64). */
+int otc_checksum(const void *p, size_t nbytes, uint64_t *out_dev, void *stream);
+
+/* ---- device memory / sync helpers (so C harnesses need no HIP headers) --- */
+void *otc_dev_malloc(size_t nbytes);
+void otc_dev_free(void *p);
+#define OTC_H2D 0
+#define OTC_D2H 1
+#define OTC_D2D 2
+int otc_memcpy(void *dst, const void *src, size_t nbytes, int kind);
+int otc_memset(void *p, int v, size_t nbytes);
+/* Elapsed device time of `op` run `iters` times on the default stream,
+ * bracketed by hipEvents (kernel-only timing). */
+typedef int (*otc_op_fn)(void *arg);
+int otc_time_op(otc_op_fn op, void *arg, int iters, double *ms_per_iter);
+
+/* ---- device info ------------------------------------------------------- */
+int otc_device_count(void);
+int otc_device_cus(int dev);           /* compute units */
+int otc_device_clock_khz(int dev);     /* peak shader clock */
+int otc_set_device(int dev);
+int otc_device_sync(void);
+
+/* ---- L3 engine: host-memory streaming pipeline -----------------------------
+ * Encrypt/decrypt a HOST buffer through one GPU with a pinned staging ring:
+ * H2D(k+1) | kernel(k) | D2H(k-1) on three HIP streams.  `host_in` /
+ * `host_out` may be pageable (staged through the pinned ring) or already
+ * pinned/registered (copied directly).  chunk_bytes: 0 = default (256 MiB).
+ */
+typedef struct otc_engine otc_engine;
+
+otc_engine *otc_engine_create(int device, size_t chunk_bytes, int depth);
+void otc_engine_destroy(otc_engine *e);
+
+#define OTC_MODE_ECB 0
+#define OTC_MODE_CTR 1
+#define OTC_MODE_CBC_DEC 2
+#define OTC_MODE_XOR 3
+
+typedef struct {
+    double total_ms;    /* wall time of the whole call */
+    double kernel_ms;   /* sum of kernel times (hipEvent) */
+    double h2d_ms, d2h_ms;
+    size_t bytes;
+    int chunks;
+} otc_stream_stats;
+
+int otc_engine_run(otc_engine *e, int mode, const void *host_in, void *host_out, size_t nbytes,
+                   const otc_aes_key *k, const uint8_t iv_or_ctr[16], uint64_t block_offset,
+                   int impl, otc_stream_stats *stats);
+
+/* Pin / unpin an existing host range (hipHostRegister) so the engine copies
+ * it without staging. */
+int otc_host_register(void *p, size_t nbytes);
+int otc_host_unregister(void *p);
+void *otc_host_alloc_pinned(size_t nbytes);
+void otc_host_free_pinned(void *p);
+
+/* ---- L4 multi-GPU (single process, RCCL over xGMI) -----------------------
+ * Shard one host-resident CTR/ECB/CBC-dec stream over `ngpus` devices.
+ * strategy 0 = direct ingest (each GPU streams its own shard from pinned host
+ * memory, engine pipeline per GPU, one host thread per GPU);
+ * strategy 1 = RCCL root scatter/gather (root H2D, ncclScatter over xGMI,
+ * per-GPU kernel, ncclGather, root D2H), chunked.
+ * CBC decryption shards receive a 16-byte halo (the previous shard's last
+ * ciphertext block).  Results are byte-identical to the 1-GPU path.
+ */
+typedef struct {
+    double total_ms;
+    double gbps;
+    int ngpus;
+    int strategy;
+} otc_multi_stats;
+
+int otc_multi_run(int ngpus, int strategy, int mode, const void *host_in, void *host_out,
+                  size_t nbytes, const otc_aes_key *k, const uint8_t iv_or_ctr[16], int impl,
+                  size_t chunk_bytes, otc_multi_stats *stats);
+
+/* Device-resident multi-GPU CTR: buffers dev_bufs[g] (already on GPU g) hold
+ * shard g of `shard_bytes`; all GPUs encrypt in place concurrently with the
+ * right counter offsets.  Returns elapsed ms (wall, all GPUs). */
+int otc_multi_ctr_resident(int ngpus, void *const *dev_bufs, size_t shard_bytes,
+                           const otc_aes_key *k, const uint8_t ctr0[16], int impl,
+                           double *elapsed_ms);
+
+/* Library self description / tests */
+int otc_bitslice_selftest(int verbose);
+const char *otc_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OTC_H */

@@ -1,0 +1,340 @@
+/*
+ * otc_bitslice.h -- bitsliced AES round functions, shared by the gfx950 HIP
+ * kernels (csrc/hip/aes_bs.hip) and the host unit test (csrc/cpu/bs_selftest.cpp).
+ *
+ * Representation: one 32-bit word per (state byte, bit) "plane".  Bit k of
+ * plane[8*b + i] is bit i of AES state byte b (b = row + 4*col, FIPS-197
+ * order) of block slot k, so one lane processes 32 blocks with 128 VGPRs of
+ * state.  ShiftRows is free (compile-time renaming under full unrolling);
+ * SubBytes is the Boyar-Peralta depth-16 circuit (113 XOR/XNOR/AND gates) which
+ * hipcc fuses into gfx950's 3-input v_bitop3_b32 / v_xor3_b32; MixColumns is
+ * the xtime formulation out_r = xt(a_r ^ a_{r+1}) ^ (a0^a1^a2^a3) ^ a_r.
+ *
+ * No reference counterpart: the reference's only GPU code is a T-table kernel
+ * (/root/reference/aes-gpu/Source/AES.cu:284-392).  This is the "wave-level
+ * bitsliced VALU path" of BASELINE.json's north star.
+ */
+#ifndef OTC_BITSLICE_H
+#define OTC_BITSLICE_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define OTC_HD __host__ __device__ __forceinline__
+#else
+#define OTC_HD inline
+#endif
+
+namespace otc_bs {
+
+typedef uint32_t W;
+
+/* Forward S-box on 8 planes x[0..7] (x[i] = bit i, i = 0 is the LSB). */
+OTC_HD void sbox(W &x0, W &x1, W &x2, W &x3, W &x4, W &x5, W &x6, W &x7)
+{
+    /* Boyar-Peralta naming: U0 is the most significant bit. */
+    const W U0 = x7, U1 = x6, U2 = x5, U3 = x4, U4 = x3, U5 = x2, U6 = x1, U7 = x0;
+    const W T1 = U0 ^ U3, T2 = U0 ^ U5, T3 = U0 ^ U6, T4 = U3 ^ U5, T5 = U4 ^ U6;
+    const W T6 = T1 ^ T5, T7 = U1 ^ U2, T8 = U7 ^ T6, T9 = U7 ^ T7, T10 = T6 ^ T7;
+    const W T11 = U1 ^ U5, T12 = U2 ^ U5, T13 = T3 ^ T4, T14 = T6 ^ T11, T15 = T5 ^ T11;
+    const W T16 = T5 ^ T12, T17 = T9 ^ T16, T18 = U3 ^ U7, T19 = T7 ^ T18, T20 = T1 ^ T19;
+    const W T21 = U6 ^ U7, T22 = T7 ^ T21, T23 = T2 ^ T22, T24 = T2 ^ T10, T25 = T20 ^ T17;
+    const W T26 = T3 ^ T16, T27 = T1 ^ T12;
+
+    const W M1 = T13 & T6, M2 = T23 & T8, M3 = T14 ^ M1, M4 = T19 & U7, M5 = M4 ^ M1;
+    const W M6 = T3 & T16, M7 = T22 & T9, M8 = T26 ^ M6, M9 = T20 & T17, M10 = M9 ^ M6;
+    const W M11 = T1 & T15, M12 = T4 & T27, M13 = M12 ^ M11, M14 = T2 & T10, M15 = M14 ^ M11;
+    const W M16 = M3 ^ M2, M17 = M5 ^ T24, M18 = M8 ^ M7, M19 = M10 ^ M15, M20 = M16 ^ M13;
+    const W M21 = M17 ^ M15, M22 = M18 ^ M13, M23 = M19 ^ T25, M24 = M22 ^ M23, M25 = M22 & M20;
+    const W M26 = M21 ^ M25, M27 = M20 ^ M21, M28 = M23 ^ M25, M29 = M28 & M27, M30 = M26 & M24;
+    const W M31 = M20 & M23, M32 = M27 & M31, M33 = M27 ^ M25, M34 = M21 & M22, M35 = M24 & M34;
+    const W M36 = M24 ^ M25, M37 = M21 ^ M29, M38 = M32 ^ M33, M39 = M23 ^ M30, M40 = M35 ^ M36;
+    const W M41 = M38 ^ M40, M42 = M37 ^ M39, M43 = M37 ^ M38, M44 = M39 ^ M40, M45 = M42 ^ M41;
+    const W M46 = M44 & T6, M47 = M40 & T8, M48 = M39 & U7, M49 = M43 & T16, M50 = M38 & T9;
+    const W M51 = M37 & T17, M52 = M42 & T15, M53 = M45 & T27, M54 = M41 & T10, M55 = M44 & T13;
+    const W M56 = M40 & T23, M57 = M39 & T19, M58 = M43 & T3, M59 = M38 & T22, M60 = M37 & T20;
+    const W M61 = M42 & T1, M62 = M45 & T4, M63 = M41 & T2;
+
+    const W L0 = M61 ^ M62, L1 = M50 ^ M56, L2 = M46 ^ M48, L3 = M47 ^ M55, L4 = M54 ^ M58;
+    const W L5 = M49 ^ M61, L6 = M62 ^ L5, L7 = M46 ^ L3, L8 = M51 ^ M59, L9 = M52 ^ M53;
+    const W L10 = M53 ^ L4, L11 = M60 ^ L2, L12 = M48 ^ M51, L13 = M50 ^ L0, L14 = M52 ^ M61;
+    const W L15 = M55 ^ L1, L16 = M56 ^ L0, L17 = M57 ^ L1, L18 = M58 ^ L8, L19 = M63 ^ L4;
+    const W L20 = L0 ^ L1, L21 = L1 ^ L7, L22 = L3 ^ L12, L23 = L18 ^ L2, L24 = L15 ^ L9;
+    const W L25 = L6 ^ L10, L26 = L7 ^ L9, L27 = L8 ^ L10, L28 = L11 ^ L14, L29 = L11 ^ L17;
+
+    const W S0 = L6 ^ L24, S1 = ~(L16 ^ L26), S2 = ~(L19 ^ L28), S3 = L6 ^ L21;
+    const W S4 = L20 ^ L22, S5 = L25 ^ L29, S6 = ~(L13 ^ L27), S7 = ~(L6 ^ L23);
+    x7 = S0; x6 = S1; x5 = S2; x4 = S3; x3 = S4; x2 = S5; x1 = S6; x0 = S7;
+}
+
+OTC_HD void sub_bytes(W *s)
+{
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+        sbox(s[8 * b + 0], s[8 * b + 1], s[8 * b + 2], s[8 * b + 3], s[8 * b + 4], s[8 * b + 5],
+             s[8 * b + 6], s[8 * b + 7]);
+}
+
+/* 3-input XOR.  VEC: one v_bitop3_b32 on gfx950 (hipcc does not fuse pure
+ * XOR chains itself).  !VEC: plain C, so hipcc can keep wave-uniform planes
+ * on the scalar ALU. */
+template <bool VEC>
+OTC_HD W xx3(W a, W b, W c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (VEC) return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#endif
+    return a ^ b ^ c;
+}
+
+/* S-box of (x ^ k) with the round-key masks k0..k7 (wave-uniform, 0 or ~0)
+ * folded into the top linear layer: every first-level XOR of two inputs
+ * becomes a 3-input XOR with the uniform constant k_a ^ k_b (free: the third
+ * bitop3 operand is an SGPR), and only U7, used raw by two ANDs, needs an
+ * explicit XOR.  AddRoundKey thus costs 1 VALU op per S-box instead of 8. */
+template <bool VEC>
+OTC_HD void sbox_k(W &x0, W &x1, W &x2, W &x3, W &x4, W &x5, W &x6, W &x7, W k0, W k1, W k2, W k3,
+                   W k4, W k5, W k6, W k7)
+{
+    const W U0 = x7, U1 = x6, U2 = x5, U3 = x4, U4 = x3, U5 = x2, U6 = x1, U7 = x0;
+    const W K0 = k7, K1 = k6, K2 = k5, K3 = k4, K4 = k3, K5 = k2, K6 = k1, K7 = k0;
+    const W U7k = U7 ^ K7;
+    const W T1 = xx3<VEC>(U0, U3, K0 ^ K3), T2 = xx3<VEC>(U0, U5, K0 ^ K5);
+    const W T3 = xx3<VEC>(U0, U6, K0 ^ K6), T4 = xx3<VEC>(U3, U5, K3 ^ K5);
+    const W T5 = xx3<VEC>(U4, U6, K4 ^ K6);
+    const W T6 = T1 ^ T5, T7 = xx3<VEC>(U1, U2, K1 ^ K2), T8 = U7k ^ T6, T9 = U7k ^ T7, T10 = T6 ^ T7;
+    const W T11 = xx3<VEC>(U1, U5, K1 ^ K5), T12 = xx3<VEC>(U2, U5, K2 ^ K5), T13 = T3 ^ T4;
+    const W T14 = T6 ^ T11, T15 = T5 ^ T11;
+    const W T16 = T5 ^ T12, T17 = T9 ^ T16, T18 = xx3<VEC>(U3, U7, K3 ^ K7), T19 = T7 ^ T18,
+            T20 = T1 ^ T19;
+    const W T21 = xx3<VEC>(U6, U7, K6 ^ K7), T22 = T7 ^ T21, T23 = T2 ^ T22, T24 = T2 ^ T10,
+            T25 = T20 ^ T17;
+    const W T26 = T3 ^ T16, T27 = T1 ^ T12;
+
+    const W M1 = T13 & T6, M2 = T23 & T8, M3 = T14 ^ M1, M4 = T19 & U7k, M5 = M4 ^ M1;
+    const W M6 = T3 & T16, M7 = T22 & T9, M8 = T26 ^ M6, M9 = T20 & T17, M10 = M9 ^ M6;
+    const W M11 = T1 & T15, M12 = T4 & T27, M13 = M12 ^ M11, M14 = T2 & T10, M15 = M14 ^ M11;
+    const W M16 = M3 ^ M2, M17 = M5 ^ T24, M18 = M8 ^ M7, M19 = M10 ^ M15, M20 = M16 ^ M13;
+    const W M21 = M17 ^ M15, M22 = M18 ^ M13, M23 = M19 ^ T25, M24 = M22 ^ M23, M25 = M22 & M20;
+    const W M26 = M21 ^ M25, M27 = M20 ^ M21, M28 = M23 ^ M25, M29 = M28 & M27, M30 = M26 & M24;
+    const W M31 = M20 & M23, M32 = M27 & M31, M33 = M27 ^ M25, M34 = M21 & M22, M35 = M24 & M34;
+    const W M36 = M24 ^ M25, M37 = M21 ^ M29, M38 = M32 ^ M33, M39 = M23 ^ M30, M40 = M35 ^ M36;
+    const W M41 = M38 ^ M40, M42 = M37 ^ M39, M43 = M37 ^ M38, M44 = M39 ^ M40, M45 = M42 ^ M41;
+    const W M46 = M44 & T6, M47 = M40 & T8, M48 = M39 & U7k, M49 = M43 & T16, M50 = M38 & T9;
+    const W M51 = M37 & T17, M52 = M42 & T15, M53 = M45 & T27, M54 = M41 & T10, M55 = M44 & T13;
+    const W M56 = M40 & T23, M57 = M39 & T19, M58 = M43 & T3, M59 = M38 & T22, M60 = M37 & T20;
+    const W M61 = M42 & T1, M62 = M45 & T4, M63 = M41 & T2;
+
+    const W L0 = M61 ^ M62, L1 = M50 ^ M56, L2 = M46 ^ M48, L3 = M47 ^ M55, L4 = M54 ^ M58;
+    const W L5 = M49 ^ M61, L6 = M62 ^ L5, L7 = M46 ^ L3, L8 = M51 ^ M59, L9 = M52 ^ M53;
+    const W L10 = M53 ^ L4, L11 = M60 ^ L2, L12 = M48 ^ M51, L13 = M50 ^ L0, L14 = M52 ^ M61;
+    const W L15 = M55 ^ L1, L16 = M56 ^ L0, L17 = M57 ^ L1, L18 = M58 ^ L8, L19 = M63 ^ L4;
+    const W L20 = L0 ^ L1, L21 = L1 ^ L7, L22 = L3 ^ L12, L23 = L18 ^ L2, L24 = L15 ^ L9;
+    const W L25 = L6 ^ L10, L26 = L7 ^ L9, L27 = L8 ^ L10, L28 = L11 ^ L14, L29 = L11 ^ L17;
+
+    x7 = L6 ^ L24;
+    x6 = ~(L16 ^ L26);
+    x5 = ~(L19 ^ L28);
+    x4 = L6 ^ L21;
+    x3 = L20 ^ L22;
+    x2 = L25 ^ L29;
+    x1 = ~(L13 ^ L27);
+    x0 = ~(L6 ^ L23);
+}
+
+/* MixColumns of one column (bytes a0..a3 = 4 x 8 planes, rows 0..3):
+ * d_r = a_r ^ a_{r+1};  out_r = xtime(d_r) ^ a_{r+1} ^ d_{r+2}
+ * (= 2a_r ^ 3a_{r+1} ^ a_{r+2} ^ a_{r+3}); 76 ops with 3-input XORs. */
+template <bool VEC>
+OTC_HD void mix_column(const W *in, W *out)
+{
+    W d[4][8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d[r][i] = in[8 * r + i] ^ in[8 * ((r + 1) & 3) + i];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const W *an = in + 8 * ((r + 1) & 3);
+        const W *dr = d[r], *d2 = d[(r + 2) & 3];
+        W *o = out + 8 * r;
+        o[0] = xx3<VEC>(dr[7], an[0], d2[0]);
+        o[1] = xx3<VEC>(dr[0], dr[7], an[1] ^ d2[1]);
+        o[2] = xx3<VEC>(dr[1], an[2], d2[2]);
+        o[3] = xx3<VEC>(dr[2], dr[7], an[3] ^ d2[3]);
+        o[4] = xx3<VEC>(dr[3], dr[7], an[4] ^ d2[4]);
+        o[5] = xx3<VEC>(dr[4], an[5], d2[5]);
+        o[6] = xx3<VEC>(dr[5], an[6], d2[6]);
+        o[7] = xx3<VEC>(dr[6], an[7], d2[7]);
+    }
+}
+
+/* ShiftRows: new byte (r,c) = old byte (r, c+r mod 4). */
+OTC_HD void shift_rows(const W *in, W *out)
+{
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) out[8 * (r + 4 * c) + i] = in[8 * (r + 4 * ((c + r) & 3)) + i];
+}
+
+/* 3-input XOR: one v_bitop3_b32 on gfx950 (hipcc does not fuse XOR chains). */
+OTC_HD W x3(W a, W b, W c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+    return a ^ b ^ c;
+#endif
+}
+
+/* MixColumns on a ShiftRows'd state `in`, result into `out`, with the round
+ * key folded in: kf(p) returns the 0 / ~0 mask of plane p.  Per column:
+ * t = a0^a1^a2^a3, d_r = a_r ^ a_{r+1}, out_r = xtime(d_r) ^ t ^ a_r ^ k. */
+template <class KF>
+OTC_HD void mix_columns_ark(const W *in, W *out, KF kf)
+{
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const W *a0 = in + 32 * c, *a1 = a0 + 8, *a2 = a0 + 16, *a3 = a0 + 24;
+        W t[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = x3(a0[i], a1[i], a2[i]) ^ a3[i];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const W *ar = in + 32 * c + 8 * r;
+            const W *an = in + 32 * c + 8 * ((r + 1) & 3);
+            W d[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) d[i] = ar[i] ^ an[i];
+            W *o = out + 32 * c + 8 * r;
+            const int p = 32 * c + 8 * r;
+            /* u_i = t_i ^ a_r,i ^ k_i  (a_r ^ t = a_{r+1} ^ a_{r+2} ^ a_{r+3}) */
+            o[0] = x3(d[7], x3(t[0], ar[0], kf(p + 0)), 0);
+            o[1] = x3(d[0], d[7], x3(t[1], ar[1], kf(p + 1)));
+            o[2] = x3(d[1], t[2], ar[2]) ^ kf(p + 2);
+            o[3] = x3(d[2], d[7], x3(t[3], ar[3], kf(p + 3)));
+            o[4] = x3(d[3], d[7], x3(t[4], ar[4], kf(p + 4)));
+            o[5] = x3(d[4], t[5], ar[5]) ^ kf(p + 5);
+            o[6] = x3(d[5], t[6], ar[6]) ^ kf(p + 6);
+            o[7] = x3(d[6], t[7], ar[7]) ^ kf(p + 7);
+        }
+    }
+}
+
+/* Rounds 1..NR of AES on bitsliced planes s[128] (AddRoundKey r folded into
+ * the S-box of round r+1; the LAST round key is NOT applied -- callers fold it
+ * into their output XOR).  kf(r, p) returns the mask of plane p of round key r.
+ * CTR_CACHE: the caller guarantees bytes 0..14 of the input are wave-uniform
+ * (counter-mode caching) so rounds 1 and 2 evaluate their uniform S-boxes and
+ * columns with plain C ops that hipcc keeps on the scalar ALU. */
+template <int R, int NR, bool CTR_CACHE, class KF>
+OTC_HD void encrypt_round(W *s, KF &kf)
+{
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        W *x = s + 8 * b;
+        const int p = 8 * b;
+        /* which S-boxes see per-lane data under CTR caching:
+         * round 0: only byte 15; round 1: bytes 0..3 (column 0) */
+        const bool vec = !CTR_CACHE || R >= 2 || (R == 0 && b == 15) || (R == 1 && b < 4);
+        if (vec)
+            sbox_k<true>(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kf(R, p), kf(R, p + 1),
+                         kf(R, p + 2), kf(R, p + 3), kf(R, p + 4), kf(R, p + 5), kf(R, p + 6),
+                         kf(R, p + 7));
+        else
+            sbox_k<false>(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kf(R, p), kf(R, p + 1),
+                          kf(R, p + 2), kf(R, p + 3), kf(R, p + 4), kf(R, p + 5), kf(R, p + 6),
+                          kf(R, p + 7));
+    }
+    W t[128];
+    shift_rows(s, t);
+    if constexpr (R + 1 < NR) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (CTR_CACHE && R == 0)
+                mix_column<false>(t + 32 * c, s + 32 * c);
+            else
+                mix_column<true>(t + 32 * c, s + 32 * c);
+        }
+        /* explicit compile-time recursion: a `#pragma unroll` loop over rounds
+         * exceeds LLVM's pragma-unroll size threshold and is left rolled
+         * (dynamic key indexing, spills) */
+        encrypt_round<R + 1, NR, CTR_CACHE>(s, kf);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 128; ++q) s[q] = t[q];
+    }
+}
+
+/* Rounds 1..NR of AES on bitsliced planes s[128] (AddRoundKey r folded into
+ * the S-box of round r+1; the LAST round key is NOT applied -- callers fold it
+ * into their output XOR).  kf(r, p) returns the mask of plane p of round key r.
+ * CTR_CACHE: the caller guarantees bytes 0..14 of the input are wave-uniform
+ * (counter-mode caching) so rounds 1 and 2 evaluate their uniform S-boxes and
+ * columns with plain C ops that hipcc keeps on the scalar ALU. */
+template <int NR, bool CTR_CACHE, class KF>
+OTC_HD void encrypt_planes(W *s, KF kf)
+{
+    encrypt_round<0, NR, CTR_CACHE>(s, kf);
+}
+
+/* Expand one 16-byte round key (4 LE words, as produced by aes_export_rk32)
+ * into 128 plane masks. */
+OTC_HD void key_masks(const uint32_t *rk4, W *k)
+{
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        uint32_t byte = (rk4[b >> 2] >> (8 * (b & 3))) & 0xffu;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) k[8 * b + i] = ((byte >> i) & 1u) ? ~0u : 0u;
+    }
+}
+
+/* Full-round helper for host tests: s <- MixColumns(ShiftRows(SubBytes(s))) ^ k */
+struct ArrayKey {
+    const W *k;
+    OTC_HD W operator()(int p) const { return k[p]; }
+};
+
+OTC_HD void round_full(W *s, const W *k)
+{
+    W t[128];
+    sub_bytes(s);
+    shift_rows(s, t);
+    mix_columns_ark(t, s, ArrayKey{k});
+}
+
+OTC_HD void round_last(W *s, const W *k)
+{
+    W t[128];
+    sub_bytes(s);
+    shift_rows(s, t);
+#pragma unroll
+    for (int p = 0; p < 128; ++p) s[p] = t[p] ^ k[p];
+}
+
+/* Transpose 32 blocks (blk[k][0..3] = 4 LE words of block slot k) into planes,
+ * and back.  Plane 8*b+i, bit k  <->  block k, byte b, bit i, i.e. word
+ * w = b/4, bit 8*(b%4)+i of blk[k][w].  Each word-column w is an independent
+ * 32x32 bit-matrix transpose. */
+OTC_HD void transpose32(W *m)
+{
+    /* in-place 32x32 transpose: m[r] bit c  ->  m[c] bit r */
+    W mask = 0x0000FFFFu;
+#pragma unroll
+    for (int j = 16; j != 0; j >>= 1, mask ^= (mask << j)) {
+#pragma unroll
+        for (int k = 0; k < 32; k = ((k | j) + 1) & ~j) {
+            W t = ((m[k] >> j) ^ m[k | j]) & mask;
+            m[k] ^= t << j;
+            m[k | j] ^= t;
+        }
+    }
+}
+
+} /* namespace otc_bs */
+
+#endif

@@ -1,0 +1,65 @@
+"""Byte-stream device ops: XOR combiner (device ``arc4_crypt``), many-stream
+RC4, synthetic fill and checksum -- kernels in ``csrc/hip/stream_ops.hip``."""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from .. import _native
+from .aes_ops import _check_dev, _nbytes, _stream
+
+
+def xor(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out = a ^ b (bytewise).  Reference arc4_crypt (arc4.c:101-112) on the GPU."""
+    _check_dev(a, "a")
+    _check_dev(b, "b")
+    if _nbytes(a) != _nbytes(b):
+        raise ValueError("a and b must have the same byte size")
+    out = torch.empty_like(a) if out is None else out
+    with torch.cuda.device(a.device):
+        rc = _native.require_gpu_lib().otc_xor(a.data_ptr(), b.data_ptr(), out.data_ptr(), _nbytes(a), _stream(a))
+    _native.check(rc, "otc_xor")
+    return out
+
+
+def rc4_multi(keys: torch.Tensor, length: int, x: torch.Tensor | None = None, drop: int = 0,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """Run ``keys.shape[0]`` independent RC4 streams (one per GPU lane).
+
+    keys: uint8 [nstreams, keylen] on the GPU.  Returns uint8 [nstreams, length]:
+    the keystream, or ``x ^ keystream`` when ``x`` (same shape) is given."""
+    _check_dev(keys, "keys")
+    if keys.dtype != torch.uint8 or keys.dim() != 2:
+        raise ValueError("keys must be uint8 [nstreams, keylen]")
+    ns, kl = keys.shape
+    if x is not None:
+        _check_dev(x, "x")
+        if _nbytes(x) != ns * length:
+            raise ValueError("x must hold nstreams*length bytes")
+    out = torch.empty((ns, length), dtype=torch.uint8, device=keys.device) if out is None else out
+    with torch.cuda.device(keys.device):
+        rc = _native.require_gpu_lib().otc_rc4_multi(keys.data_ptr(), kl, ns, length, drop,
+                                                     x.data_ptr() if x is not None else None, out.data_ptr(),
+                                                     _stream(keys))
+    _native.check(rc, "otc_rc4_multi")
+    return out
+
+
+def fill_random_(t: torch.Tensor, seed: int = 0) -> torch.Tensor:
+    """Fill ``t`` in place with deterministic pseudo-random bytes (splitmix64)."""
+    _check_dev(t, "t")
+    with torch.cuda.device(t.device):
+        rc = _native.require_gpu_lib().otc_fill_random(t.data_ptr(), _nbytes(t), seed & (2**64 - 1), _stream(t))
+    _native.check(rc, "otc_fill_random")
+    return t
+
+
+def checksum(t: torch.Tensor) -> int:
+    """Position-dependent 64-bit XOR fold of a device buffer (byte size % 8 == 0)."""
+    _check_dev(t, "t")
+    acc = torch.zeros(1, dtype=torch.int64, device=t.device)
+    with torch.cuda.device(t.device):
+        rc = _native.require_gpu_lib().otc_checksum(t.data_ptr(), _nbytes(t), acc.data_ptr(), _stream(t))
+    _native.check(rc, "otc_checksum")
+    return int(acc.item()) & (2**64 - 1)

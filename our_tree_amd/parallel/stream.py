@@ -1,0 +1,120 @@
+"""Host-memory streaming through the native pinned pipeline (otc_engine_*:
+H2D(k+1) | kernel(k) | D2H(k-1) on three HIP streams, csrc/hip/engine.cpp) and
+the single-process multi-GPU planner (otc_multi_run: direct per-GPU ingest or
+RCCL root scatter/gather over xGMI).
+
+Replaces the reference's synchronous pageable cudaMemcpy around every launch
+(/root/reference/aes-gpu/Source/AES.cu:230-282).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from .. import _native
+from ..ops.keys import expand_key
+
+MODES = {"ecb": 0, "ctr": 1, "cbc-dec": 2}
+STRATEGIES = {"direct": 0, "rccl": 1}
+
+
+def _ptr(a):
+    if isinstance(a, np.ndarray):
+        if not a.flags["C_CONTIGUOUS"]:
+            raise ValueError("host buffers must be contiguous")
+        return a.ctypes.data
+    try:
+        import torch
+
+        if isinstance(a, torch.Tensor):
+            if a.device.type != "cpu" or not a.is_contiguous():
+                raise ValueError("host buffers must be contiguous CPU tensors")
+            return a.data_ptr()
+    except ImportError:
+        pass
+    raise TypeError("host buffer must be a numpy array or CPU tensor")
+
+
+def _nb(a):
+    return a.nbytes if isinstance(a, np.ndarray) else a.numel() * a.element_size()
+
+
+class StreamEngine:
+    """Pinned double/triple-buffered host<->GPU pipeline on one device."""
+
+    def __init__(self, device: int = 0, chunk_bytes: int = 256 << 20, depth: int = 3):
+        self._lib = _native.require_gpu_lib()
+        self._h = self._lib.otc_engine_create(device, chunk_bytes, depth)
+        if not self._h:
+            _native.check(-5, "otc_engine_create")
+        self.device = device
+
+    def close(self):
+        if self._h:
+            self._lib.otc_engine_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, mode: str, host_in, host_out, key: bytes, iv_or_counter: bytes = bytes(16),
+            block_offset: int = 0, impl: str = "auto") -> dict:
+        n = _nb(host_in)
+        if _nb(host_out) < n:
+            raise ValueError("output buffer too small")
+        k = expand_key(key, decrypt=(mode == "cbc-dec"))
+        st = _native.StreamStats()
+        ivb = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(iv_or_counter))
+        rc = self._lib.otc_engine_run(self._h, MODES[mode], _ptr(host_in), _ptr(host_out), n, ctypes.byref(k), ivb,
+                                      block_offset, {"auto": 0, "ttable": 1, "bitslice": 2}[impl], ctypes.byref(st))
+        _native.check(rc, "otc_engine_run")
+        return {"total_ms": st.total_ms, "kernel_ms": st.kernel_ms, "bytes": st.bytes, "chunks": st.chunks,
+                "gbps": st.bytes / (st.total_ms * 1e6) if st.total_ms else 0.0}
+
+
+def multi_gpu_run(mode: str, host_in, host_out, key: bytes, iv_or_counter: bytes = bytes(16), ngpus: int = 1,
+                  strategy: str = "direct", chunk_bytes: int = 256 << 20, impl: str = "auto") -> dict:
+    """Single-process multi-GPU processing of one host-resident stream."""
+    lib = _native.require_gpu_lib()
+    k = expand_key(key, decrypt=(mode == "cbc-dec"))
+    st = _native.MultiStats()
+    ivb = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(iv_or_counter))
+    rc = lib.otc_multi_run(ngpus, STRATEGIES[strategy], MODES[mode], _ptr(host_in), _ptr(host_out), _nb(host_in),
+                           ctypes.byref(k), ivb, {"auto": 0, "ttable": 1, "bitslice": 2}[impl], chunk_bytes,
+                           ctypes.byref(st))
+    _native.check(rc, "otc_multi_run")
+    return {"total_ms": st.total_ms, "gbps": st.gbps, "ngpus": st.ngpus, "strategy": strategy}
+
+
+def pinned_empty(nbytes: int) -> np.ndarray:
+    """A numpy view over hipHostMalloc'd (pinned) memory; freed with the array's
+    owner object."""
+    lib = _native.require_gpu_lib()
+    p = lib.otc_host_alloc_pinned(nbytes)
+    if not p:
+        raise MemoryError("hipHostMalloc failed")
+    buf = (ctypes.c_uint8 * nbytes).from_address(p)
+    arr = np.frombuffer(buf, dtype=np.uint8)
+
+    class _Owner:
+        def __del__(self_inner):
+            lib.otc_host_free_pinned(p)
+
+    arr_owner = _Owner()
+    arr = arr.view()
+    arr.flags.writeable = True
+    _PINNED_OWNERS[id(arr)] = arr_owner
+    return arr
+
+
+_PINNED_OWNERS: dict = {}

@@ -1,0 +1,210 @@
+"""Numerics of every gfx950 kernel against the C oracle (csrc/cpu/aes.c, the
+reference-compatible PolarSSL-API implementation) on random data, random keys,
+odd lengths, unaligned counters and counter carries."""
+import os
+
+import pytest
+import torch
+
+from our_tree_amd import ops
+from our_tree_amd.models import cpu_ref
+from our_tree_amd.parallel import shard as sh
+
+pytestmark = pytest.mark.gpu
+
+IMPLS = ["ttable", "bitslice"]
+KEYBITS = [128, 192, 256]
+
+
+def rnd(n, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(0, 256, (n,), dtype=torch.uint8, generator=g).to(dev)
+
+
+def host(t):
+    return t.cpu().numpy().tobytes()
+
+
+@pytest.mark.parametrize("impl", IMPLS)
+@pytest.mark.parametrize("bits", KEYBITS)
+@pytest.mark.parametrize("n", [16, 1000, 4096 * 16 + 5, (1 << 20) + 3, 3 * (1 << 20) + 16 * 777])
+def test_ctr_matches_oracle(gpu, impl, bits, n):
+    key = os.urandom(bits // 8)
+    ctr0 = os.urandom(16)
+    x = rnd(n, gpu, n + bits)
+    y = ops.ctr(x, key, ctr0, impl=impl)
+    torch.cuda.synchronize()
+    assert host(y) == cpu_ref.ctr(key, ctr0, host(x))
+
+
+@pytest.mark.parametrize("impl", IMPLS)
+@pytest.mark.parametrize("ctr_low", [0, 1, 2047, 2048, 0xFFFFFFFF, (1 << 64) - 5, (1 << 64) - 3000])
+def test_ctr_counter_carries(gpu, impl, ctr_low):
+    """Counters near 2^11 task boundaries, 2^32 and the 2^64 carry into the
+    high half (128-bit add)."""
+    key = os.urandom(16)
+    hi = os.urandom(8)
+    ctr0 = hi + ctr_low.to_bytes(8, "big")
+    x = rnd(16 * 5000 + 9, gpu, 7)
+    y = ops.ctr(x, key, ctr0, impl=impl)
+    torch.cuda.synchronize()
+    assert host(y) == cpu_ref.ctr(key, ctr0, host(x))
+
+
+@pytest.mark.parametrize("impl", IMPLS)
+def test_ctr_block_offset_and_inplace(gpu, impl):
+    key = os.urandom(16)
+    ctr0 = os.urandom(16)
+    x = rnd(1 << 18, gpu, 3)
+    ref = cpu_ref.ctr(key, ctr0, host(x), block_offset=123457)
+    ops.ctr(x, key, ctr0, out=x, block_offset=123457, impl=impl)
+    torch.cuda.synchronize()
+    assert host(x) == ref
+
+
+@pytest.mark.parametrize("impl", IMPLS)
+def test_ctr_rfc3686(gpu, impl):
+    """AES-NI counter layout with 64-bit wrap, against the AES-NI CPU baseline."""
+    if not cpu_ref.aesni_supported():
+        pytest.skip("no AES-NI on this host")
+    key, nonce, ivec = os.urandom(32), os.urandom(4), b"\xff" * 4 + b"\xff\xff\xff\xf0"
+    x = rnd(16 * 300 + 3, gpu, 11)
+    y = ops.ctr_rfc3686(x, key, nonce, ivec, impl=impl)
+    torch.cuda.synchronize()
+    assert host(y) == cpu_ref.aesni_ctr(key, nonce, ivec, host(x))
+
+
+@pytest.mark.parametrize("impl", IMPLS)
+@pytest.mark.parametrize("bits", KEYBITS)
+def test_ecb_roundtrip(gpu, impl, bits):
+    key = os.urandom(bits // 8)
+    x = rnd(16 * 100003, gpu, bits)
+    y = ops.ecb_encrypt(x, key, impl=impl)
+    torch.cuda.synchronize()
+    assert host(y) == cpu_ref.ecb(key, host(x), threads=8)
+    z = ops.ecb_decrypt(y, key)
+    torch.cuda.synchronize()
+    assert torch.equal(z, x)
+
+
+def test_fips197_appendix_c(gpu):
+    pt = bytes.fromhex("00112233445566778899aabbccddeeff")
+    exp = {16: "69c4e0d86a7b0430d8cdb78070b4c55a", 24: "dda97ca4864cdfe06eaf70a0ec0d7191",
+           32: "8ea2b7ca516745bfeafc49904b496089"}
+    for kl, ct in exp.items():
+        x = torch.tensor(list(pt), dtype=torch.uint8, device=gpu)
+        for impl in IMPLS:
+            assert host(ops.ecb_encrypt(x, bytes(range(kl)), impl=impl)).hex() == ct
+        assert host(ops.ecb_decrypt(torch.tensor(list(bytes.fromhex(ct)), dtype=torch.uint8, device=gpu),
+                                    bytes(range(kl)))) == pt
+
+
+@pytest.mark.parametrize("bits", KEYBITS)
+def test_cbc_decrypt(gpu, bits):
+    key, iv = os.urandom(bits // 8), os.urandom(16)
+    pt = os.urandom(16 * 70001)
+    ct = cpu_ref.cbc(key, iv, pt)
+    x = torch.frombuffer(bytearray(ct), dtype=torch.uint8).to(gpu)
+    y = ops.cbc_decrypt(x, key, iv)
+    torch.cuda.synchronize()
+    assert host(y) == pt
+
+
+@pytest.mark.parametrize("seg", [16, 512, 4096])
+def test_cbc_segments_roundtrip(gpu, seg):
+    key, iv0 = os.urandom(32), (2**128 - 3).to_bytes(16, "big")  # IV carry across segments
+    nseg = 1000
+    pt = os.urandom(seg * nseg)
+    x = torch.frombuffer(bytearray(pt), dtype=torch.uint8).to(gpu)
+    y = ops.cbc_encrypt_segments(x, key, iv0, seg)
+    torch.cuda.synchronize()
+    assert host(y) == cpu_ref.cbc_segments(key, iv0, pt, seg)
+    z = ops.cbc_decrypt_segments(y, key, iv0, seg)
+    torch.cuda.synchronize()
+    assert host(z) == pt
+
+
+def test_cbc_single_segment_is_exact_cbc(gpu):
+    key, iv = os.urandom(16), os.urandom(16)
+    pt = os.urandom(16 * 333)
+    x = torch.frombuffer(bytearray(pt), dtype=torch.uint8).to(gpu)
+    y = ops.cbc_encrypt_segments(x, key, iv, len(pt))
+    assert host(y) == cpu_ref.cbc(key, iv, pt)
+
+
+def test_cfb128_decrypt(gpu):
+    key, iv = os.urandom(24), os.urandom(16)
+    pt = os.urandom(16 * 5001)
+    ct = cpu_ref.cfb128(key, iv, pt)
+    x = torch.frombuffer(bytearray(ct), dtype=torch.uint8).to(gpu)
+    assert host(ops.cfb128_decrypt(x, key, iv)) == pt
+
+
+def test_sp800_38a_ctr_vector(gpu):
+    key = bytes.fromhex("2b7e151628aed2a6abf7158809cf4f3c")
+    ctr0 = bytes.fromhex("f0f1f2f3f4f5f6f7f8f9fafbfcfdfeff")
+    pt = bytes.fromhex("6bc1bee22e409f96e93d7e117393172aae2d8a571e03ac9c9eb76fac45af8e51"
+                       "30c81c46a35ce411e5fbc1191a0a52eff69f2445df4f9b17ad2b417be66c3710")
+    exp = ("874d6191b620e3261bef6864990db6ce9806f66b7970fdff8617187bb9fffdff"
+           "5ae4df3edbd5d35e5b4f09020db03eab1e031dda2fbe03d1792170a0f3009cee")
+    x = torch.tensor(list(pt), dtype=torch.uint8, device=gpu)
+    for impl in IMPLS:
+        assert host(ops.ctr(x, key, ctr0, impl=impl)).hex() == exp
+
+
+def test_sharded_ctr_equals_single_stream(gpu):
+    """Device shards with planner offsets == one stream (the DP invariant)."""
+    key, ctr0 = os.urandom(16), os.urandom(16)
+    n = 16 * 12345 + 11
+    x = rnd(n, gpu, 5)
+    ref = host(ops.ctr(x, key, ctr0))
+    parts = []
+    for s in sh.plan(n, 7):
+        parts.append(host(ops.ctr(x[s.offset:s.end].contiguous(), key, ctr0, block_offset=s.block_offset)))
+    assert b"".join(parts) == ref
+
+
+def test_xor_and_arc4(gpu):
+    key = os.urandom(16)
+    n = (1 << 20) + 13
+    ks = cpu_ref.arc4_keystream(key, n)
+    x = rnd(n, gpu, 9)
+    k = torch.frombuffer(bytearray(ks), dtype=torch.uint8).to(gpu)
+    y = ops.xor(x, k)
+    assert host(y) == cpu_ref.arc4_crypt(host(x), ks)
+
+
+@pytest.mark.parametrize("keylen,length,drop", [(16, 4096, 0), (5, 1000, 3), (256, 37, 768)])
+def test_rc4_multi(gpu, keylen, length, drop):
+    ns = 200
+    keys = rnd(ns * keylen, gpu, keylen).view(ns, keylen)
+    ks = ops.rc4_multi(keys, length, drop=drop)
+    torch.cuda.synchronize()
+    kh = keys.cpu().numpy()
+    for s in [0, 1, 63, 64, 199]:
+        assert host(ks[s]) == cpu_ref.arc4_keystream(bytes(kh[s]), length, drop=drop)
+    x = rnd(ns * length, gpu, 1).view(ns, length)
+    y = ops.rc4_multi(keys, length, x=x, drop=drop)
+    assert torch.equal(y, x ^ ks)
+
+
+def test_fill_and_checksum(gpu):
+    a = torch.empty(1 << 20, dtype=torch.uint8, device=gpu)
+    b = torch.empty(1 << 20, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(a, 5)
+    ops.fill_random_(b, 5)
+    assert torch.equal(a, b)
+    assert ops.checksum(a) == ops.checksum(b)
+    b[12345] ^= 1
+    assert ops.checksum(a) != ops.checksum(b)
+
+
+def test_errors_are_loud(gpu):
+    x = rnd(17, gpu)
+    with pytest.raises(RuntimeError):
+        ops.ecb_encrypt(x, os.urandom(16))  # not a multiple of 16
+    with pytest.raises(ValueError):
+        ops.ctr(x, os.urandom(15), os.urandom(16))
+    y = rnd(32, gpu)
+    with pytest.raises(RuntimeError):
+        ops.cbc_decrypt(y, os.urandom(16), os.urandom(16), out=y)  # in-place unsupported
