@@ -36,8 +36,8 @@ HIP_OBJ := $(patsubst csrc/hip/%.hip,$(OBJ)/hip/%.o,$(HIP_SRC)) $(OBJ)/hip/engin
 BINS := bin/test bin/aes_test bin/aes_ecb_e bin/aes_ecb_d bin/otbench
 
 .PHONY: all cpu clean
-all: $(LIBDIR)/libotc.so $(LIBDIR)/libotc_cpu.so $(BINS)
-cpu: $(LIBDIR)/libotc_cpu.so bin/test_cpu
+all: $(LIBDIR)/libotc.so $(LIBDIR)/libotc_cpu.so $(BINS) bin/test_cpu bin/aes_test_cpu
+cpu: $(LIBDIR)/libotc_cpu.so bin/test_cpu bin/aes_test_cpu
 
 $(OBJ)/cpu/aesni.o: csrc/cpu/aesni.c csrc/include/aesni.h
 	@mkdir -p $(dir $@)
@@ -50,6 +50,11 @@ $(OBJ)/cpu/%.o: csrc/cpu/%.c $(wildcard csrc/include/*.h)
 $(OBJ)/cpu/bs_selftest.o: csrc/cpu/bs_selftest.cpp csrc/include/otc_bitslice.h
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) $(INC) -c $< -o $@
+
+# -fno-slp-vectorize: the SLP vectorizer packs the 4 independent transposes /
+# 16 S-boxes of the bitsliced kernel into lock-stepped vector ops, which doubles
+# the live register set (1 wave/SIMD + AGPR spills).  See docs/PERF.md.
+$(OBJ)/hip/aes_bs.o: HIPFLAGS += -fno-slp-vectorize
 
 $(OBJ)/hip/%.o: csrc/hip/%.hip csrc/hip/otc_device.h csrc/include/otc.h csrc/include/otc_bitslice.h
 	@mkdir -p $(dir $@)
@@ -69,6 +74,10 @@ $(LIBDIR)/libotc_cpu.so: $(CPU_OBJ)
 
 # --- CLIs -------------------------------------------------------------------
 bin/test_cpu: csrc/cli/rc4_test.c $(CPU_OBJ)
+	@mkdir -p bin
+	$(CXX) -O2 $(INC) -x c -std=gnu99 $< -x none $(CPU_OBJ) -o $@ -lpthread $(SANLD)
+
+bin/aes_test_cpu: csrc/cli/aes_test.c $(CPU_OBJ)
 	@mkdir -p bin
 	$(CXX) -O2 $(INC) -x c -std=gnu99 $< -x none $(CPU_OBJ) -o $@ -lpthread $(SANLD)
 
@@ -93,4 +102,4 @@ bin/otbench: csrc/cli/otbench.cpp $(LIBDIR)/libotc.so
 	$(CXX) -O2 -std=c++17 $(INC) $< -o $@ -L$(LIBDIR) -lotc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
 
 clean:
-	rm -rf build $(LIBDIR)/*.so $(BINS) bin/test_cpu
+	rm -rf build $(LIBDIR)/*.so $(BINS) bin/test_cpu bin/aes_test_cpu

@@ -43,10 +43,13 @@ extern "C" int otc_bitslice_selftest(int verbose)
             for (int i = 0; i < 8; ++i) x[i] |= (W)(((slot * 7 + kv) >> i) & 1) << slot;
         for (int i = 0; i < 8; ++i) y[i] = x[i] ^ k[i];
         sbox(y[0], y[1], y[2], y[3], y[4], y[5], y[6], y[7]);
+        W z[8];
+        for (int i = 0; i < 8; ++i) z[i] = x[i];
         sbox_k<false>(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7]);
+        sbox_lut3(z[0], z[1], z[2], z[3], z[4], z[5], z[6], z[7], k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7]);
         for (int i = 0; i < 8; ++i)
-            if (x[i] != y[i]) {
-                if (verbose) printf("  sbox_k mismatch kv=%d bit %d\n", kv, i);
+            if (x[i] != y[i] || z[i] != y[i]) {
+                if (verbose) printf("  sbox_k/sbox_lut3 mismatch kv=%d bit %d\n", kv, i);
                 ++fails;
             }
     }

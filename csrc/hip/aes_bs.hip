@@ -56,12 +56,17 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * 4u + wave;
-    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
-    const uint64_t total = P.nblocks + (P.tail ? 1u : 0u);
     const uint64_t shift = (MODE == BS_CTR) ? P.shift : 0;
-    const uint64_t vtotal = total + shift;
+    const uint64_t vtotal = P.nblocks + shift; /* full blocks only; the host
+                                                  routes a trailing partial block
+                                                  to the T-table kernel */
 
-    for (uint64_t task = gwave; task * 2048u < vtotal; task += nwaves) {
+    /* One 2048-block task per wave, no grid-stride loop: a loop lets hipcc
+     * hoist loop-invariant plane/mask values out of it, which costs more
+     * registers than the 128-plane state leaves. */
+    {
+        const uint64_t task = gwave;
+        if (task * 2048u >= vtotal) return;
         const uint64_t vbase = task * 2048u;
         /* block index of slot k = vbase - shift + 64k + lane (may be out of range) */
         const bool full = vbase >= shift && vbase + 2048u - shift <= P.nblocks; /* uniform */
@@ -91,25 +96,33 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
                 }
             }
         } else {
-            /* ECB: load 32 blocks and transpose each word column */
-            const uint64_t i0 = vbase + lane;
+            /* ECB: load 32 blocks (uniform task base + 32-bit lane offsets:
+             * 64-bit per-slot addresses would be CSE'd with the stores and
+             * kept live across the rounds) and transpose each word column */
+            const uint8_t *tb = P.in + vbase * 16;
+            const uint32_t lo = lane * 16u;
+            uint4 blk[32];
+#pragma unroll
+            for (int k = 0; k < 32; ++k) {
+                const uint64_t i = vbase + lane + 64u * k;
+                blk[k] = (full || i < P.nblocks) ? *(const uint4 *)(tb + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
+            }
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
                 W m[32];
 #pragma unroll
-                for (int k = 0; k < 32; ++k) {
-                    const uint64_t i = i0 + 64u * k;
-                    m[k] = (full || i < P.nblocks) ? *(const uint32_t *)(P.in + 16 * i + 4 * w) : 0u;
-                }
+                for (int k = 0; k < 32; ++k) m[k] = w == 0 ? blk[k].x : w == 1 ? blk[k].y : w == 2 ? blk[k].z : blk[k].w;
                 transpose32(m);
+                pin_n(m, 32);
 #pragma unroll
                 for (int q = 0; q < 32; ++q) s[32 * w + q] = m[q];
+                sched_fence();
             }
         }
 
-        /* Round keys are laundered through an empty asm inside the task loop:
-         * otherwise hipcc hoists all 128*NR key masks out of the loop and
-         * spills them (SGPR -> VGPR lanes), costing occupancy and readlanes. */
+        sched_fence();
+        /* Round keys are laundered through an empty asm so hipcc materialises
+         * each key mask next to its use instead of all 128*NR up front. */
         uint32_t rk[4 * (NR + 1)];
 #pragma unroll
         for (int q = 0; q < 4 * (NR + 1); ++q) {
@@ -123,38 +136,44 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
             return (W)(0u - ((rk[4 * r + (p >> 5)] >> (p & 31)) & 1u));
         });
 
+        pin_n(s, 128);
+        sched_fence();
         /* planes -> blocks (keystream / ciphertext without the last key) */
 #pragma unroll
-        for (int w = 0; w < 4; ++w) transpose32(s + 32 * w);
+        for (int w = 0; w < 4; ++w) {
+            transpose32(s + 32 * w);
+            pin_n(s + 32 * w, 32);
+            sched_fence();
+        }
 
         const uint32_t k0 = rk[4 * NR + 0], k1 = rk[4 * NR + 1], k2 = rk[4 * NR + 2],
                        k3 = rk[4 * NR + 3];
-        const int64_t ibase = (int64_t)vbase - (int64_t)shift + (int64_t)lane;
+        /* uniform task base (may point before the buffer for the first CTR
+         * task; those slots are masked) + 32-bit per-lane offsets */
+        const int64_t tstart = (int64_t)vbase - (int64_t)shift;
+        const uint8_t *ib = P.in + tstart * 16;
+        uint8_t *ob = P.out + tstart * 16;
+        const uint32_t lo = lane * 16u;
 #pragma unroll
         for (int k = 0; k < 32; ++k) {
-            if ((k & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-            const int64_t si = ibase + 64 * k;
+            /* bound the plaintext loads in flight (else all 32 x 16 B are
+             * hoisted and double the live registers) */
+            if ((k & 3) == 0) sched_fence();
+            const int64_t si = tstart + (int64_t)lane + 64 * k;
             const bool ok = full || (si >= 0 && (uint64_t)si < P.nblocks);
-            const uint64_t i = (uint64_t)si;
-            if (MODE == BS_CTR) {
-                if (ok) {
-                    const uint4 x = *(const uint4 *)(P.in + 16 * i);
-                    uint4 o;
+            const uint32_t off = lo + 1024u * k;
+            if (ok) {
+                uint4 o;
+                if (MODE == BS_CTR) {
+                    const uint4 x = *(const uint4 *)(ib + off);
                     o.x = x3(x.x, s[k], k0);
                     o.y = x3(x.y, s[32 + k], k1);
                     o.z = x3(x.z, s[64 + k], k2);
                     o.w = x3(x.w, s[96 + k], k3);
-                    *(uint4 *)(P.out + 16 * i) = o;
-                } else if (si >= 0 && i == P.nblocks && P.tail) {
-                    const uint32_t ks[4] = {s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3};
-                    for (uint32_t n = 0; n < P.tail; ++n)
-                        P.out[16 * i + n] = P.in[16 * i + n] ^ (uint8_t)(ks[n >> 2] >> (8 * (n & 3)));
+                } else {
+                    o = make_uint4(s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3);
                 }
-            } else {
-                if (ok) {
-                    uint4 o = make_uint4(s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3);
-                    *(uint4 *)(P.out + 16 * i) = o;
-                }
+                *(uint4 *)(ob + off) = o;
             }
         }
     }
@@ -171,12 +190,11 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
         (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (g_cus <= 0) g_cus = 256;
     }
-    const uint64_t vt = P.nblocks + (P.tail ? 1 : 0) + (MODE == BS_CTR ? P.shift : 0);
+    const uint64_t vt = P.nblocks + (MODE == BS_CTR ? P.shift : 0);
     const uint64_t tasks = (vt + 2047) / 2048;
     uint64_t wgs = (tasks + 3) / 4;
-    const uint64_t cap = (uint64_t)g_cus * 2; /* 8 waves per CU (2 per SIMD) */
-    if (wgs > cap) wgs = cap;
     if (wgs < 1) wgs = 1;
+    if (wgs > 0xFFFFFFFFull) return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_aes_bs<NR, MODE>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
     return hipGetLastError();
 }
@@ -186,8 +204,10 @@ hipError_t launch(const BsParams &P, const otc_aes_key &K, hipStream_t st)
 {
     switch (K.nr) {
     case 10: return launch_nr<10, MODE>(P, K, st);
+#ifndef OTC_BS_ONLY_NR10
     case 12: return launch_nr<12, MODE>(P, K, st);
     case 14: return launch_nr<14, MODE>(P, K, st);
+#endif
     default: return hipErrorInvalidValue;
     }
 }
@@ -196,9 +216,22 @@ hipError_t launch(const BsParams &P, const otc_aes_key &K, hipStream_t st)
 
 namespace otc_impl {
 
+hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
+
 hipError_t bs_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
                   hipStream_t st)
 {
+    if (nbytes % 16) {
+        /* trailing partial block: T-table kernel, same counter stream */
+        const size_t full = nbytes - nbytes % 16;
+        Ctr128 ct = c;
+        ct.lo = c.lo + full / 16;
+        if (!wrap64 && ct.lo < c.lo) ct.hi += 1;
+        hipError_t e = tt_ctr((const uint8_t *)in + full, (uint8_t *)out + full, nbytes % 16, K, ct, wrap64, st);
+        if (e != hipSuccess) return e;
+        nbytes = full;
+        if (nbytes == 0) return hipSuccess;
+    }
     BsParams P{};
     P.in = (const uint8_t *)in;
     P.out = (uint8_t *)out;

@@ -28,6 +28,9 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "otc_device.h"
 
 using namespace otc_dev;
@@ -386,20 +389,55 @@ int grid_for(uint64_t work_items, uint64_t per_wg, int wg_per_cu)
     return (int)(need < cap ? need : cap);
 }
 
-constexpr int ENC_THREADS = 512;
+constexpr int ENC_THREADS = 1024; /* measured best of 256..1024 x B=1..4 (docs/PERF.md) */
 constexpr int ENC_B = 2;
 constexpr int DEC_THREADS = 1024;
 constexpr int DEC_B = 2;
 constexpr int SEG_THREADS = 512;
 constexpr int SEG_B = 2;
 
+/* Tuning variants of the encryption kernel (threads per workgroup x blocks
+ * per lane), selectable with OTC_TT_VARIANT=<threads>x<B> for measurement;
+ * 64 KiB LDS per workgroup, so 2 workgroups per CU. */
+struct TTVariant {
+    int threads, b;
+};
+TTVariant tt_variant()
+{
+    static TTVariant v = [] {
+        TTVariant d{ENC_THREADS, ENC_B};
+        const char *e = getenv("OTC_TT_VARIANT");
+        if (e) {
+            int t = 0, b = 0;
+            if (sscanf(e, "%dx%d", &t, &b) == 2) d = TTVariant{t, b};
+        }
+        return d;
+    }();
+    return v;
+}
+
+template <int NR, int MODE, int T, int B>
+hipError_t launch_enc_tb(const EncParams &P, const otc_aes_key &K, hipStream_t st)
+{
+    const uint64_t nt = P.nfull + (P.tail ? 1 : 0);
+    int grid = grid_for(nt, (uint64_t)T * B, 2);
+    hipLaunchKernelGGL((k_aes_enc_tt<NR, MODE, B, T>), dim3(grid), dim3(T), 0, st, P, K);
+    return hipGetLastError();
+}
+
 template <int NR, int MODE>
 hipError_t launch_enc_nr(const EncParams &P, const otc_aes_key &K, hipStream_t st)
 {
-    const uint64_t nt = P.nfull + (P.tail ? 1 : 0);
-    int grid = grid_for(nt, (uint64_t)ENC_THREADS * ENC_B, 2);
-    hipLaunchKernelGGL((k_aes_enc_tt<NR, MODE, ENC_B, ENC_THREADS>), dim3(grid), dim3(ENC_THREADS), 0, st, P, K);
-    return hipGetLastError();
+    if (MODE == E_CTR || MODE == E_ECB) {
+        const TTVariant v = tt_variant();
+        if (v.threads == 1024 && v.b == 2) return launch_enc_tb<NR, MODE, 1024, 2>(P, K, st);
+        if (v.threads == 512 && v.b == 4) return launch_enc_tb<NR, MODE, 512, 4>(P, K, st);
+        if (v.threads == 1024 && v.b == 4) return launch_enc_tb<NR, MODE, 1024, 4>(P, K, st);
+        if (v.threads == 256 && v.b == 4) return launch_enc_tb<NR, MODE, 256, 4>(P, K, st);
+        if (v.threads == 512 && v.b == 1) return launch_enc_tb<NR, MODE, 512, 1>(P, K, st);
+        if (v.threads == 1024 && v.b == 1) return launch_enc_tb<NR, MODE, 1024, 1>(P, K, st);
+    }
+    return launch_enc_tb<NR, MODE, ENC_THREADS, ENC_B>(P, K, st);
 }
 
 template <int MODE>

@@ -25,6 +25,13 @@
 #define OTC_HD inline
 #endif
 
+#ifndef OTC_BS_FENCE_SBOX
+#define OTC_BS_FENCE_SBOX 0
+#endif
+#ifndef OTC_BS_FENCE_MC
+#define OTC_BS_FENCE_MC 0
+#endif
+
 namespace otc_bs {
 
 typedef uint32_t W;
@@ -73,6 +80,34 @@ OTC_HD void sub_bytes(W *s)
     for (int b = 0; b < 16; ++b)
         sbox(s[8 * b + 0], s[8 * b + 1], s[8 * b + 2], s[8 * b + 3], s[8 * b + 4], s[8 * b + 5],
              s[8 * b + 6], s[8 * b + 7]);
+}
+
+/* Scheduling fence on the device: keeps hipcc's machine scheduler from
+ * interleaving independent S-boxes / columns, which otherwise blows the live
+ * register set far past the 128-plane state (1 wave/SIMD + spills). */
+OTC_HD void sched_fence()
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
+/* Pin values in VGPRs at this program point: an empty volatile asm that
+ * "modifies" them.  Volatile asms keep their relative order and everything
+ * computed from a pinned value must follow it, so this orders whole phases
+ * for the SelectionDAG scheduler too (sched_barrier only binds the machine
+ * scheduler; pure ALU ops float across it in the DAG). */
+OTC_HD void pin8(W *x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]));
+#else
+    (void)x;
+#endif
+}
+OTC_HD void pin_n(W *x, int n)
+{
+    for (int i = 0; i + 8 <= n; i += 8) pin8(x + i);
 }
 
 /* 3-input XOR.  VEC: one v_bitop3_b32 on gfx950 (hipcc does not fuse pure
@@ -148,6 +183,9 @@ OTC_HD void sbox_k(W &x0, W &x1, W &x2, W &x3, W &x4, W &x5, W &x6, W &x7, W k0,
 template <bool VEC>
 OTC_HD void mix_column(const W *in, W *out)
 {
+    /* Register-frugal order: d_0..d_3 first (the inputs a_r stay live only
+     * for the a_{r+1} term), then rows 0..3 -- row r is the last reader of
+     * a_{r+1}, so each finished row frees 8 input planes. */
     W d[4][8];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -166,6 +204,7 @@ OTC_HD void mix_column(const W *in, W *out)
         o[5] = xx3<VEC>(dr[4], an[5], d2[5]);
         o[6] = xx3<VEC>(dr[5], an[6], d2[6]);
         o[7] = xx3<VEC>(dr[6], an[7], d2[7]);
+        if (OTC_BS_FENCE_MC) sched_fence();
     }
 }
 
@@ -224,46 +263,66 @@ OTC_HD void mix_columns_ark(const W *in, W *out, KF kf)
     }
 }
 
-/* Rounds 1..NR of AES on bitsliced planes s[128] (AddRoundKey r folded into
- * the S-box of round r+1; the LAST round key is NOT applied -- callers fold it
- * into their output XOR).  kf(r, p) returns the mask of plane p of round key r.
- * CTR_CACHE: the caller guarantees bytes 0..14 of the input are wave-uniform
- * (counter-mode caching) so rounds 1 and 2 evaluate their uniform S-boxes and
- * columns with plain C ops that hipcc keeps on the scalar ALU. */
+} /* namespace otc_bs */
+#include "otc_sbox_lut3.h"
+namespace otc_bs {
+
+template <bool CTR_CACHE, int R, class KF>
+OTC_HD void sbox_byte(W *s, int b, KF &kf)
+{
+    W *x = s + 8 * b;
+    const int p = 8 * b;
+    /* which S-boxes see per-lane data under CTR caching:
+     * round 0: only byte 15; round 1: bytes 0..3 (column 0) */
+    const bool vec = !CTR_CACHE || R >= 2 || (R == 0 && b == 15) || (R == 1 && b < 4);
+    if (vec) /* 86-LUT3 mapping of the same circuit (tools/sbox_lut3.py) */
+        sbox_lut3(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kf(R, p), kf(R, p + 1), kf(R, p + 2),
+                  kf(R, p + 3), kf(R, p + 4), kf(R, p + 5), kf(R, p + 6), kf(R, p + 7));
+    else
+        sbox_k<false>(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kf(R, p), kf(R, p + 1), kf(R, p + 2),
+                      kf(R, p + 3), kf(R, p + 4), kf(R, p + 5), kf(R, p + 6), kf(R, p + 7));
+    if (vec) pin8(x); /* uniform (SALU) bytes must not be forced into VGPRs */
+    if (OTC_BS_FENCE_SBOX) sched_fence();
+}
+
+/* One AES round on the planes.  Streaming order per OUTPUT column c:
+ * S-box the four bytes that ShiftRows brings into column c, then MixColumns
+ * them into a fresh array.  Each input byte feeds exactly one output column,
+ * so the live set stays ~128 planes + one column of temporaries (keeps the
+ * kernel at 2 waves/SIMD; the textbook SubBytes -> ShiftRows -> MixColumns
+ * order keeps old and new state live together). */
 template <int R, int NR, bool CTR_CACHE, class KF>
 OTC_HD void encrypt_round(W *s, KF &kf)
 {
-#pragma unroll
-    for (int b = 0; b < 16; ++b) {
-        W *x = s + 8 * b;
-        const int p = 8 * b;
-        /* which S-boxes see per-lane data under CTR caching:
-         * round 0: only byte 15; round 1: bytes 0..3 (column 0) */
-        const bool vec = !CTR_CACHE || R >= 2 || (R == 0 && b == 15) || (R == 1 && b < 4);
-        if (vec)
-            sbox_k<true>(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kf(R, p), kf(R, p + 1),
-                         kf(R, p + 2), kf(R, p + 3), kf(R, p + 4), kf(R, p + 5), kf(R, p + 6),
-                         kf(R, p + 7));
-        else
-            sbox_k<false>(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kf(R, p), kf(R, p + 1),
-                          kf(R, p + 2), kf(R, p + 3), kf(R, p + 4), kf(R, p + 5), kf(R, p + 6),
-                          kf(R, p + 7));
-    }
-    W t[128];
-    shift_rows(s, t);
     if constexpr (R + 1 < NR) {
+        W ns[128];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
+            W col[32];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int b = r + 4 * ((c + r) & 3); /* ShiftRows source byte */
+                sbox_byte<CTR_CACHE, R>(s, b, kf);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) col[8 * r + i] = s[8 * b + i];
+            }
             if (CTR_CACHE && R == 0)
-                mix_column<false>(t + 32 * c, s + 32 * c);
+                mix_column<false>(col, ns + 32 * c);
             else
-                mix_column<true>(t + 32 * c, s + 32 * c);
+                mix_column<true>(col, ns + 32 * c);
+            if (OTC_BS_FENCE_MC) sched_fence();
         }
+#pragma unroll
+        for (int q = 0; q < 128; ++q) s[q] = ns[q];
         /* explicit compile-time recursion: a `#pragma unroll` loop over rounds
          * exceeds LLVM's pragma-unroll size threshold and is left rolled
          * (dynamic key indexing, spills) */
         encrypt_round<R + 1, NR, CTR_CACHE>(s, kf);
     } else {
+#pragma unroll
+        for (int b = 0; b < 16; ++b) sbox_byte<CTR_CACHE, R>(s, b, kf);
+        W t[128];
+        shift_rows(s, t);
 #pragma unroll
         for (int q = 0; q < 128; ++q) s[q] = t[q];
     }
