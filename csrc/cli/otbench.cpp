@@ -175,6 +175,7 @@ int main(int argc, char **argv)
         }
         for (size_t i = 0; i < c.bytes; i += 4096) hin[i] = (uint8_t)i;
         int mode = c.mode == "ctr" ? OTC_MODE_CTR : c.mode == "cbc-dec" ? OTC_MODE_CBC_DEC : OTC_MODE_ECB;
+        otc_engine *eng = (c.gpus > 1 || c.strategy == 1) ? nullptr : otc_engine_create(0, c.chunk, 3);
         for (int w = 0; w <= c.warmup; ++w) {
             auto t0 = std::chrono::steady_clock::now();
             int r;
@@ -182,9 +183,7 @@ int main(int argc, char **argv)
                 otc_multi_stats st{};
                 r = otc_multi_run(c.gpus, c.strategy, mode, hin, hout, c.bytes, &k, a.iv, c.impl, c.chunk, &st);
             } else {
-                otc_engine *e = otc_engine_create(0, c.chunk, 3);
-                r = e ? otc_engine_run(e, mode, hin, hout, c.bytes, &k, a.iv, 0, c.impl, nullptr) : OTC_ERR_NOMEM;
-                otc_engine_destroy(e);
+                r = eng ? otc_engine_run(eng, mode, hin, hout, c.bytes, &k, a.iv, 0, c.impl, nullptr) : OTC_ERR_NOMEM;
             }
             auto t1 = std::chrono::steady_clock::now();
             if (r) {
@@ -197,6 +196,7 @@ int main(int argc, char **argv)
                "\"chunk\": %zu, \"ms\": %.3f, \"gbps\": %.3f}\n",
                c.mode.c_str(), c.bits, c.bytes, c.gpus, c.strategy ? "rccl" : "direct", c.chunk, ms,
                c.bytes / (ms * 1e6));
+        otc_engine_destroy(eng);
         otc_host_free_pinned(hin);
         otc_host_free_pinned(hout);
         return 0;

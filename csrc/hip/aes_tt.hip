@@ -370,6 +370,26 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg(CbcSegParams P, otc
     }
 }
 
+/* CBC-decrypt over segments of ANY length: the plain CBC kernel XORs every
+ * block with its predecessor; this fix-up swaps that predecessor for IV_s at
+ * each segment start s >= 1 (touches nseg blocks only). */
+__global__ __launch_bounds__(256) void k_cbc_seg_fixup(const uint8_t *in, uint8_t *out, uint64_t seg_blocks,
+                                                       uint64_t nseg, Ctr128 iv0)
+{
+    const uint64_t s = 1 + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= nseg) return;
+    const uint64_t i = s * seg_blocks;
+    Ctr128 ivv;
+    ivv.lo = iv0.lo + s;
+    ivv.hi = iv0.hi + (ivv.lo < iv0.lo ? 1 : 0);
+    uint32_t w0, w1, w2, w3;
+    ctr_words(ivv, 0, false, w0, w1, w2, w3);
+    const uint4 prev = ld16(in, i - 1);
+    uint4 o = ld16(out, i);
+    o.x ^= prev.x ^ w0; o.y ^= prev.y ^ w1; o.z ^= prev.z ^ w2; o.w ^= prev.w ^ w3;
+    st16(out, i, o);
+}
+
 /* ---------------------------------------------------------------------------
  * Host-side launch helpers
  * ------------------------------------------------------------------------- */
@@ -536,16 +556,26 @@ hipError_t tt_cbc_decrypt(const void *in, void *out, uint64_t nblocks, const otc
     return launch_dec<D_CBC>(P, K, st);
 }
 
-hipError_t tt_cbc_decrypt_seg(const void *in, void *out, uint64_t nblocks, uint32_t seg_shift,
+hipError_t tt_cbc_decrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,
                               const otc_aes_key &K, Ctr128 iv0, hipStream_t st)
 {
     DecParams P{};
     P.in = (const uint8_t *)in;
     P.out = (uint8_t *)out;
-    P.nfull = nblocks;
-    P.seg_shift = seg_shift;
+    P.nfull = seg_blocks * nseg;
     P.iv = iv0;
-    return launch_dec<D_CBC_SEG>(P, K, st);
+    if (seg_blocks && (seg_blocks & (seg_blocks - 1)) == 0) { /* power of two: in-kernel IVs */
+        uint32_t sh = 0;
+        while ((1ull << sh) < seg_blocks) ++sh;
+        P.seg_shift = sh;
+        return launch_dec<D_CBC_SEG>(P, K, st);
+    }
+    hipError_t e = launch_dec<D_CBC>(P, K, st);
+    if (e != hipSuccess || nseg < 2) return e;
+    const uint64_t nfix = nseg - 1;
+    hipLaunchKernelGGL(k_cbc_seg_fixup, dim3((unsigned)((nfix + 255) / 256)), dim3(256), 0, st,
+                       (const uint8_t *)in, (uint8_t *)out, seg_blocks, nseg, iv0);
+    return hipGetLastError();
 }
 
 hipError_t tt_cbc_encrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,

@@ -40,7 +40,7 @@ hipError_t tt_ecb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, h
 hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
 hipError_t tt_cfb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, hipStream_t);
 hipError_t tt_cbc_decrypt(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
-hipError_t tt_cbc_decrypt_seg(const void *, void *, uint64_t, uint32_t, const otc_aes_key &, Ctr128, hipStream_t);
+hipError_t tt_cbc_decrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t tt_cbc_encrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
 hipError_t bs_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
@@ -227,13 +227,10 @@ extern "C" int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t se
     if (r) return r;
     if (seg_bytes % 16) return set_err(OTC_ERR_ARG, "segment length must be a multiple of 16");
     size_t sb = seg_bytes / 16;
-    if (sb == 0 || (sb & (sb - 1))) return set_err(OTC_ERR_ARG, "segment blocks must be a power of two");
+    if (sb == 0) return set_err(OTC_ERR_ARG, "empty segments");
     if (in == out) return set_err(OTC_ERR_ARG, "in-place CBC decryption is not supported");
     if (nseg == 0) return OTC_OK;
-    uint32_t shift = 0;
-    while ((1ull << shift) < sb) ++shift;
-    hipError_t e = otc_impl::tt_cbc_decrypt_seg(in, out, sb * nseg, shift, *k, ctr_from_bytes(iv0),
-                                                (hipStream_t)stream);
+    hipError_t e = otc_impl::tt_cbc_decrypt_seg(in, out, sb, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "cbc_decrypt_segments launch");
     return OTC_OK;
 }
@@ -419,10 +416,10 @@ extern "C" otc_engine *otc_engine_create(int device, size_t chunk_bytes, int dep
     e->ev_k.assign(depth, nullptr);
     e->ev_d2h.assign(depth, nullptr);
     e->ev_k0.assign(depth, nullptr);
+    /* pinned staging (h_in/h_out) is allocated lazily, only for pageable
+     * host buffers */
     for (int i = 0; ok && i < depth; ++i) {
         ok = hipMalloc(&e->d_in[i], chunk_bytes) == hipSuccess && hipMalloc(&e->d_out[i], chunk_bytes) == hipSuccess &&
-             hipHostMalloc(&e->h_in[i], chunk_bytes, hipHostMallocDefault) == hipSuccess &&
-             hipHostMalloc(&e->h_out[i], chunk_bytes, hipHostMallocDefault) == hipSuccess &&
              hipEventCreateWithFlags(&e->ev_h2d[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreate(&e->ev_k[i]) == hipSuccess &&
              hipEventCreateWithFlags(&e->ev_d2h[i], hipEventDisableTiming) == hipSuccess &&
@@ -493,6 +490,10 @@ extern "C" int otc_engine_run(otc_engine *e, int mode, const void *host_in, void
     HIPCHK(hipSetDevice(e->device));
     auto t0 = std::chrono::steady_clock::now();
     const bool pin_in = is_pinned(host_in), pin_out = is_pinned(host_out);
+    for (int i = 0; i < e->depth; ++i) {
+        if (!pin_in && !e->h_in[i]) HIPCHK(hipHostMalloc(&e->h_in[i], e->chunk, hipHostMallocDefault));
+        if (!pin_out && !e->h_out[i]) HIPCHK(hipHostMalloc(&e->h_out[i], e->chunk, hipHostMallocDefault));
+    }
     const size_t C = e->chunk;
     const size_t nchunks = (nbytes + C - 1) / C;
     const uint8_t *hin = (const uint8_t *)host_in;

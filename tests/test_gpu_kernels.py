@@ -110,7 +110,7 @@ def test_cbc_decrypt(gpu, bits):
     assert host(y) == pt
 
 
-@pytest.mark.parametrize("seg", [16, 512, 4096])
+@pytest.mark.parametrize("seg", [16, 48, 512, 4096, 16 * 37])
 def test_cbc_segments_roundtrip(gpu, seg):
     key, iv0 = os.urandom(32), (2**128 - 3).to_bytes(16, "big")  # IV carry across segments
     nseg = 1000
