@@ -128,7 +128,7 @@ int main(int argc, char **argv)
         else if (a == "--warmup") c.warmup = atoi(nx());
         else if (a == "--impl") {
             std::string v = nx();
-            c.impl = v == "ttable" ? OTC_IMPL_TTABLE : v == "bitslice" ? OTC_IMPL_BITSLICE : OTC_IMPL_AUTO;
+            c.impl = v == "ttable" ? OTC_IMPL_TTABLE : v == "bitslice" ? OTC_IMPL_BITSLICE : v == "hybrid" ? OTC_IMPL_HYBRID : OTC_IMPL_AUTO;
         } else if (a == "--inplace") c.inplace = true;
         else if (a == "--verify") c.verify = true;
         else if (a == "--e2e") c.e2e = true;
@@ -238,7 +238,7 @@ int main(int argc, char **argv)
            "\"ms\": %.4f, \"gbps\": %.2f, \"cycles_per_byte_per_cu\": %.3f, \"cus\": %d, \"clock_mhz\": %.0f, "
            "\"verified\": %s}\n",
            c.mode.c_str(), c.bits, c.bytes,
-           c.impl == OTC_IMPL_TTABLE ? "ttable" : c.impl == OTC_IMPL_BITSLICE ? "bitslice" : "auto",
+           c.impl == OTC_IMPL_TTABLE ? "ttable" : c.impl == OTC_IMPL_BITSLICE ? "bitslice" : c.impl == OTC_IMPL_HYBRID ? "hybrid" : "auto",
            c.inplace ? "true" : "false", c.iters, ms, gbps, cpb, cus, clk_hz / 1e6,
            c.verify ? (ok ? "true" : "false") : "null");
     otc_dev_free(a.in);

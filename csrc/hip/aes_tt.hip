@@ -58,15 +58,151 @@ __device__ __forceinline__ void fill_rep64(uint32_t *lds, const uint32_t *src)
     }
 }
 
-/* ---------------------------------------------------------------------------
- * Round functions for B blocks at once (arrays are compile-time indexed)
- * ------------------------------------------------------------------------- */
+/* 4-table layout (TBL4): T_k (k = 0..3, T_k = rotl(T0, 8k)) each replicated
+ * 32 ways.  Row x of region r (r = k >> 1, 64 KiB each) holds T_{2r} for lanes
+ * 0..31 in bytes 0..127 and T_{2r+1} in bytes 128..255:
+ *   addr(k, x, lane) = (k >> 1) << 16 | x << 8 | (k & 1) << 7 | (lane & 31) << 2
+ * so again one v_perm per lookup (byte 1 <- x, bytes 0/2 <- a per-lane,
+ * per-table constant) and no rotations: 16 perm + 8 bitop3 per round instead
+ * of 16 + 12 + 8.  Bank = lane & 31 for every lookup -> conflict free. */
+template <int THREADS>
+__device__ __forceinline__ void fill_tbl4(uint32_t *lds, const uint32_t *te0)
+{
+    uint4 *l4 = reinterpret_cast<uint4 *>(lds);
+    for (int q = threadIdx.x; q < 8192; q += THREADS) {
+        const int r = q >> 12, x = (q >> 4) & 255, half = (q >> 3) & 1;
+        const int k = 2 * r + half;
+        const uint32_t t = te0[x];
+        const uint32_t v = k ? ((t << (8 * k)) | (t >> (32 - 8 * k))) : t;
+        l4[q] = make_uint4(v, v, v, v);
+    }
+}
+
+__device__ __forceinline__ void tbl4_lane_consts(uint32_t lane, uint32_t (&lk)[4])
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lk[k] = ((uint32_t)(k >> 1) << 16) | ((uint32_t)(k & 1) << 7) | ((lane & 31u) << 2);
+}
+
+template <int R0, int NR, int B>
+__device__ __forceinline__ void enc_rounds4_from(const uint32_t *tbl, const uint32_t (&lk)[4], const otc_aes_key &K,
+                                                 uint32_t (&s)[B][4])
+{
+#pragma unroll
+    for (int r = R0; r < NR; ++r) {
+        uint32_t t[B][4];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lk[0], SEL_HI(0)));
+                uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lk[1], SEL_HI(1)));
+                uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lk[2], SEL_HI(2)));
+                uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lk[3], SEL_HI(3)));
+                t[b][j] = xor3(xor3(a0, a1, a2), a3, K.rk[4 * r + j]);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
+    }
+    uint32_t t[B][4];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lk[0], SEL_HI(0)));
+            uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lk[1], SEL_HI(1)));
+            uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lk[2], SEL_HI(2)));
+            uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lk[3], SEL_HI(3)));
+            /* S[x] sits in byte 1 of T0, byte 2 of T1, byte 3 of T2, byte 0 of T3 */
+            uint32_t lo = __builtin_amdgcn_perm(a1, a0, 0x0c0c0601u);
+            uint32_t hi = __builtin_amdgcn_perm(a3, a2, 0x04030c0cu);
+            t[b][j] = xor3(lo, hi, K.rk[4 * NR + j]);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
+}
+
+/* Decryption 4-table layout: Td0..Td3 as above (128 KiB) plus the inverse
+ * S-box replicated 32 ways as byte-splatted words at 0x20000 + x*128 + lane*4
+ * (32 KiB): 160 KiB, the whole LDS of a CU.  The final-round address is one
+ * v_perm + one shift: perm gives 0x40000 | x << 8 | lane*8, >> 1 gives the
+ * row-128 address. */
+template <int THREADS>
+__device__ __forceinline__ void fill_dtbl4(uint32_t *lds, const uint32_t *td0, const uint32_t *is4)
+{
+    uint4 *l4 = reinterpret_cast<uint4 *>(lds);
+    for (int q = threadIdx.x; q < 8192 + 2048; q += THREADS) {
+        uint32_t v;
+        if (q < 8192) {
+            const int r = q >> 12, x = (q >> 4) & 255, half = (q >> 3) & 1;
+            const int k = 2 * r + half;
+            const uint32_t t = td0[x];
+            v = k ? ((t << (8 * k)) | (t >> (32 - 8 * k))) : t;
+        } else {
+            v = is4[(q - 8192) >> 3]; /* 8 uint4 (32 dwords) per 128-byte row */
+        }
+        l4[q] = make_uint4(v, v, v, v);
+    }
+}
+
 template <int NR, int B>
-__device__ __forceinline__ void enc_rounds(const uint32_t *tbl, uint32_t lane4, const otc_aes_key &K,
-                                           uint32_t (&s)[B][4])
+__device__ __forceinline__ void dec_rounds4(const uint32_t *tbl, const uint32_t (&lk)[4], uint32_t lk_is2,
+                                            const otc_aes_key &K, uint32_t (&s)[B][4])
 {
 #pragma unroll
     for (int r = 1; r < NR; ++r) {
+        uint32_t t[B][4];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lk[0], SEL_HI(0)));
+                uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lk[1], SEL_HI(1)));
+                uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lk[2], SEL_HI(2)));
+                uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lk[3], SEL_HI(3)));
+                t[b][j] = xor3(xor3(a0, a1, a2), a3, K.rk[4 * r + j]);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
+    }
+    uint32_t t[B][4];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lk_is2, SEL_HI(0)) >> 1);
+            uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lk_is2, SEL_HI(1)) >> 1);
+            uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lk_is2, SEL_HI(2)) >> 1);
+            uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lk_is2, SEL_HI(3)) >> 1);
+            uint32_t lo = __builtin_amdgcn_perm(a1, a0, 0x0c0c0400u);
+            uint32_t hi = __builtin_amdgcn_perm(a3, a2, 0x04000c0cu);
+            t[b][j] = xor3(lo, hi, K.rk[4 * NR + j]);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
+}
+
+/* ---------------------------------------------------------------------------
+ * Round functions for B blocks at once (arrays are compile-time indexed)
+ * ------------------------------------------------------------------------- */
+template <int R0, int NR, int B>
+__device__ __forceinline__ void enc_rounds_from(const uint32_t *tbl, uint32_t lane4, const otc_aes_key &K,
+                                                uint32_t (&s)[B][4])
+{
+#pragma unroll
+    for (int r = R0; r < NR; ++r) {
         uint32_t t[B][4];
 #pragma unroll
         for (int b = 0; b < B; ++b) {
@@ -103,6 +239,13 @@ __device__ __forceinline__ void enc_rounds(const uint32_t *tbl, uint32_t lane4, 
     for (int b = 0; b < B; ++b)
 #pragma unroll
         for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
+}
+
+template <int NR, int B>
+__device__ __forceinline__ void enc_rounds(const uint32_t *tbl, uint32_t lane4, const otc_aes_key &K,
+                                           uint32_t (&s)[B][4])
+{
+    enc_rounds_from<1, NR, B>(tbl, lane4, K, s);
 }
 
 template <int NR, int B>
@@ -185,13 +328,14 @@ struct DecParams {
 template <int NR, int MODE, int B, int THREADS>
 __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key K)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t tbl[256 * 64];
-    fill_rep64<THREADS>(tbl, g_tab.te0);
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
+    fill_tbl4<THREADS>(tbl, g_tab.te0);
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t lane4 = lane << 2;
+    uint32_t lk[4];
+    tbl4_lane_consts(lane, lk);
     constexpr uint64_t PER = (uint64_t)THREADS * B;
     const uint64_t ntotal = P.nfull + (P.tail ? 1u : 0u);
 
@@ -220,7 +364,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key
             for (int j = 0; j < 4; ++j) s[b][j] ^= K.rk[j];
         }
 
-        enc_rounds<NR, B>(tbl, lane4, K, s);
+        enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
 
 #pragma unroll
         for (int b = 0; b < B; ++b) {
@@ -243,21 +387,135 @@ __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key
 }
 
 /* ---------------------------------------------------------------------------
+ * CTR with counter-mode caching.
+ *
+ * Chunks are aligned to the counter (virtual index v = i + shift, shift =
+ * ctr0 mod PER; the first chunk starts `shift` blocks early with those blocks
+ * masked), so within one wave-iteration the counter of block (b, lane) is
+ * C + 64b + lane with no carry out of the low byte: bytes 0..14 of the counter
+ * block are WAVE-UNIFORM.  Hence in round 1 only the T3 lookup of byte 15
+ * differs between lanes, and in round 2 only the four lookups fed by column 0.
+ * The 15 + 12 uniform lookups are done once per wave-iteration on the scalar
+ * unit (s_load from the constant table); LDS reads per AES-128 block drop from
+ * 160 to 133.
+ * ------------------------------------------------------------------------- */
+struct CtrParams {
+    const uint8_t *in;
+    uint8_t *out;
+    uint64_t nfull;   /* full blocks */
+    uint32_t tail;    /* trailing partial block bytes */
+    uint32_t wrap64;
+    uint64_t shift;   /* ctr0.lo mod PER */
+    Ctr128 cbase;     /* ctr0 - shift (low log2(PER) bits zero) */
+};
+
+__device__ __forceinline__ uint32_t te_u(uint32_t idx) { return g_tab.te0[idx & 0xFFu]; } /* uniform lookup */
+
+template <int NR, int B, int THREADS, bool TBL4>
+__global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_aes_key K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[TBL4 ? 2 * 256 * 64 : 256 * 64];
+    if (TBL4)
+        fill_tbl4<THREADS>(tbl, g_tab.te0);
+    else
+        fill_rep64<THREADS>(tbl, g_tab.te0);
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane4 = lane << 2;
+    uint32_t lk[4];
+    tbl4_lane_consts(lane, lk);
+    constexpr uint64_t PER = (uint64_t)THREADS * B;
+    const uint64_t ntotal = P.nfull + (P.tail ? 1u : 0u);
+    const uint64_t vtotal = ntotal + P.shift;
+
+    for (uint64_t vbase = (uint64_t)blockIdx.x * PER; vbase < vtotal; vbase += (uint64_t)gridDim.x * PER) {
+        const uint64_t vw = vbase + (uint64_t)wave * 64u * B; /* wave's first virtual block (uniform) */
+        /* uniform counter C = cbase + vw */
+        uint64_t clo = P.cbase.lo + vw;
+        uint64_t chi = P.cbase.hi + ((!P.wrap64 && clo < P.cbase.lo) ? 1u : 0u);
+        const uint32_t w0 = bswap32((uint32_t)(chi >> 32)) ^ K.rk[0];
+        const uint32_t w1 = bswap32((uint32_t)chi) ^ K.rk[1];
+        const uint32_t w2 = bswap32((uint32_t)(clo >> 32)) ^ K.rk[2];
+        const uint32_t w3u = bswap32((uint32_t)clo) ^ K.rk[3]; /* byte 15 (top byte) patched per block */
+        /* round 1, uniform parts */
+        const uint32_t U0 = te_u(w0) ^ rotl8(te_u(w1 >> 8)) ^ rotl16(te_u(w2 >> 16)) ^ K.rk[4];
+        const uint32_t t1 = te_u(w1) ^ rotl8(te_u(w2 >> 8)) ^ rotl16(te_u(w3u >> 16)) ^ rotl24(te_u(w0 >> 24)) ^ K.rk[5];
+        const uint32_t t2 = te_u(w2) ^ rotl8(te_u(w3u >> 8)) ^ rotl16(te_u(w0 >> 16)) ^ rotl24(te_u(w1 >> 24)) ^ K.rk[6];
+        const uint32_t t3 = te_u(w3u) ^ rotl8(te_u(w0 >> 8)) ^ rotl16(te_u(w1 >> 16)) ^ rotl24(te_u(w2 >> 24)) ^ K.rk[7];
+        /* round 2, uniform parts */
+        const uint32_t V0 = rotl8(te_u(t1 >> 8)) ^ rotl16(te_u(t2 >> 16)) ^ rotl24(te_u(t3 >> 24)) ^ K.rk[8];
+        const uint32_t V1 = te_u(t1) ^ rotl8(te_u(t2 >> 8)) ^ rotl16(te_u(t3 >> 16)) ^ K.rk[9];
+        const uint32_t V2 = te_u(t2) ^ rotl8(te_u(t3 >> 8)) ^ rotl24(te_u(t1 >> 24)) ^ K.rk[10];
+        const uint32_t V3 = te_u(t3) ^ rotl16(te_u(t1 >> 16)) ^ rotl24(te_u(t2 >> 24)) ^ K.rk[11];
+        const uint32_t b15 = (uint32_t)(clo & 0xFFu); /* low byte of C (low 6+log2(B) bits are 0) */
+
+        const int64_t i0 = (int64_t)vw - (int64_t)P.shift + lane; /* real block index of (b=0, lane) */
+        const bool full = vw >= P.shift && vw - P.shift + 64u * B <= P.nfull; /* uniform */
+        uint32_t s[B][4];
+        uint4 x[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int64_t i = i0 + 64 * b;
+            const bool ok = full || (i >= 0 && (uint64_t)i < P.nfull);
+            x[b] = ok ? ld16(P.in, (uint64_t)i) : make_uint4(0, 0, 0, 0);
+            /* round 1: only T3[byte 15] varies */
+            const uint32_t c15 = (b15 | (uint32_t)(64 * b) | lane) ^ (K.rk[3] >> 24);
+            if (TBL4) {
+                const uint32_t s0 = U0 ^ lds_at(tbl, (c15 << 8) | lk[3]);
+                s[b][0] = V0 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[0], SEL_HI(0)));
+                s[b][1] = V1 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[3], SEL_HI(3)));
+                s[b][2] = V2 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[2], SEL_HI(2)));
+                s[b][3] = V3 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[1], SEL_HI(1)));
+            } else {
+                const uint32_t a = lds_at(tbl, (c15 << 8) | lane4);
+                const uint32_t s0 = U0 ^ rotl24(a);
+                /* round 2: the four lookups fed by s0 */
+                s[b][0] = V0 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lane4, SEL(0)));
+                s[b][1] = V1 ^ rotl24(lds_at(tbl, __builtin_amdgcn_perm(s0, lane4, SEL(3))));
+                s[b][2] = V2 ^ rotl16(lds_at(tbl, __builtin_amdgcn_perm(s0, lane4, SEL(2))));
+                s[b][3] = V3 ^ rotl8(lds_at(tbl, __builtin_amdgcn_perm(s0, lane4, SEL(1))));
+            }
+        }
+        /* rounds 3..NR */
+        if (TBL4)
+            enc_rounds4_from<3, NR, B>(tbl, lk, K, s);
+        else
+            enc_rounds_from<3, NR, B>(tbl, lane4, K, s);
+
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int64_t i = i0 + 64 * b;
+            const bool ok = full || (i >= 0 && (uint64_t)i < P.nfull);
+            if (ok) {
+                st16(P.out, (uint64_t)i,
+                     make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
+            } else if (i >= 0 && (uint64_t)i == P.nfull && P.tail) {
+                const uint32_t ks[4] = {s[b][0], s[b][1], s[b][2], s[b][3]};
+                for (uint32_t n = 0; n < P.tail; ++n)
+                    P.out[16 * (uint64_t)i + n] = P.in[16 * (uint64_t)i + n] ^ (uint8_t)(ks[n >> 2] >> (8 * (n & 3)));
+            }
+        }
+    }
+}
+
+/* ---------------------------------------------------------------------------
  * Decryption-direction kernel: ECB-dec, CBC-dec (single stream or power-of-2
  * segments with per-segment IVs)
  * ------------------------------------------------------------------------- */
 template <int NR, int MODE, int B, int THREADS>
 __global__ __launch_bounds__(THREADS) void k_aes_dec_tt(DecParams P, otc_aes_key K)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
-    fill_rep64<THREADS>(tbl, g_tab.td0);
-    fill_rep64<THREADS>(tbl + 256 * 64, g_tab.is4);
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64 + 256 * 32]; /* 160 KiB */
+    fill_dtbl4<THREADS>(tbl, g_tab.td0, g_tab.is4);
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t lane4 = lane << 2;
-    const uint32_t lane4_hi = lane4 | 0x10000u;
+    uint32_t lk[4];
+    tbl4_lane_consts(lane, lk);
+    const uint32_t lk_is2 = 0x40000u | ((lane & 31u) << 3);
     constexpr uint64_t PER = (uint64_t)THREADS * B;
 
     for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nfull; base += (uint64_t)gridDim.x * PER) {
@@ -293,7 +551,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_dec_tt(DecParams P, otc_aes_key
             }
         }
 
-        dec_rounds<NR, B>(tbl, lane4, lane4_hi, K, s);
+        dec_rounds4<NR, B>(tbl, lk, lk_is2, K, s);
 
 #pragma unroll
         for (int b = 0; b < B; ++b) {
@@ -323,13 +581,14 @@ struct CbcSegParams {
 template <int NR, int B, int THREADS>
 __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg(CbcSegParams P, otc_aes_key K)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t tbl[256 * 64];
-    fill_rep64<THREADS>(tbl, g_tab.te0);
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
+    fill_tbl4<THREADS>(tbl, g_tab.te0);
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t lane4 = lane << 2;
+    uint32_t lk[4];
+    tbl4_lane_consts(lane, lk);
     constexpr uint64_t PER = (uint64_t)THREADS * B;
 
     for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nseg; base += (uint64_t)gridDim.x * PER) {
@@ -359,7 +618,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg(CbcSegParams P, otc
                 nxt[b] = (live[b] && j + 1 < P.seg_blocks) ? ld16(P.in, seg[b] * P.seg_blocks + j + 1)
                                                            : make_uint4(0, 0, 0, 0);
             }
-            enc_rounds<NR, B>(tbl, lane4, K, s);
+            enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
 #pragma unroll
             for (int b = 0; b < B; ++b) {
 #pragma unroll
@@ -410,15 +669,14 @@ int grid_for(uint64_t work_items, uint64_t per_wg, int wg_per_cu)
 }
 
 constexpr int ENC_THREADS = 1024; /* measured best of 256..1024 x B=1..4 (docs/PERF.md) */
-constexpr int ENC_B = 2;
+constexpr int ENC_B = 4;
 constexpr int DEC_THREADS = 1024;
-constexpr int DEC_B = 2;
-constexpr int SEG_THREADS = 512;
+constexpr int DEC_B = 4;
+constexpr int SEG_THREADS = 1024;
 constexpr int SEG_B = 2;
 
-/* Tuning variants of the encryption kernel (threads per workgroup x blocks
- * per lane), selectable with OTC_TT_VARIANT=<threads>x<B> for measurement;
- * 64 KiB LDS per workgroup, so 2 workgroups per CU. */
+/* Tuning variants (threads per workgroup x blocks per lane), selectable with
+ * OTC_TT_VARIANT=<threads>x<B> for A/B measurements in one binary. */
 struct TTVariant {
     int threads, b;
 };
@@ -440,7 +698,7 @@ template <int NR, int MODE, int T, int B>
 hipError_t launch_enc_tb(const EncParams &P, const otc_aes_key &K, hipStream_t st)
 {
     const uint64_t nt = P.nfull + (P.tail ? 1 : 0);
-    int grid = grid_for(nt, (uint64_t)T * B, 2);
+    int grid = grid_for(nt, (uint64_t)T * B, 1); /* 128 KiB LDS: one workgroup per CU */
     hipLaunchKernelGGL((k_aes_enc_tt<NR, MODE, B, T>), dim3(grid), dim3(T), 0, st, P, K);
     return hipGetLastError();
 }
@@ -448,15 +706,9 @@ hipError_t launch_enc_tb(const EncParams &P, const otc_aes_key &K, hipStream_t s
 template <int NR, int MODE>
 hipError_t launch_enc_nr(const EncParams &P, const otc_aes_key &K, hipStream_t st)
 {
-    if (MODE == E_CTR || MODE == E_ECB) {
-        const TTVariant v = tt_variant();
-        if (v.threads == 1024 && v.b == 2) return launch_enc_tb<NR, MODE, 1024, 2>(P, K, st);
-        if (v.threads == 512 && v.b == 4) return launch_enc_tb<NR, MODE, 512, 4>(P, K, st);
-        if (v.threads == 1024 && v.b == 4) return launch_enc_tb<NR, MODE, 1024, 4>(P, K, st);
-        if (v.threads == 256 && v.b == 4) return launch_enc_tb<NR, MODE, 256, 4>(P, K, st);
-        if (v.threads == 512 && v.b == 1) return launch_enc_tb<NR, MODE, 512, 1>(P, K, st);
-        if (v.threads == 1024 && v.b == 1) return launch_enc_tb<NR, MODE, 1024, 1>(P, K, st);
-    }
+    const TTVariant v = tt_variant();
+    if (v.threads == 1024 && v.b == 2) return launch_enc_tb<NR, MODE, 1024, 2>(P, K, st);
+    if (v.threads == 512 && v.b == 4) return launch_enc_tb<NR, MODE, 512, 4>(P, K, st);
     return launch_enc_tb<NR, MODE, ENC_THREADS, ENC_B>(P, K, st);
 }
 
@@ -493,7 +745,7 @@ hipError_t launch_dec(const DecParams &P, const otc_aes_key &K, hipStream_t st)
 template <int NR>
 hipError_t launch_seg_nr(const CbcSegParams &P, const otc_aes_key &K, hipStream_t st)
 {
-    int grid = grid_for(P.nseg, (uint64_t)SEG_THREADS * SEG_B, 2);
+    int grid = grid_for(P.nseg, (uint64_t)SEG_THREADS * SEG_B, 1);
     hipLaunchKernelGGL((k_aes_cbc_enc_seg<NR, SEG_B, SEG_THREADS>), dim3(grid), dim3(SEG_THREADS), 0, st, P, K);
     return hipGetLastError();
 }
@@ -512,9 +764,52 @@ hipError_t tt_ecb_encrypt(const void *in, void *out, uint64_t nblocks, const otc
     return launch_enc<E_ECB>(P, K, st);
 }
 
+int g_tt_wg_per_cu = 2; /* lowered to 1 while a co-resident bitsliced kernel runs (hybrid impl) */
+
+template <int NR, int T, int B, bool TBL4 = false>
+hipError_t launch_ctr_cached_tb(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo, hipStream_t st)
+{
+    constexpr uint64_t PER = (uint64_t)T * B;
+    P.shift = ctr_lo & (PER - 1);
+    P.cbase.lo = ctr_lo - P.shift;
+    const uint64_t vt = P.nfull + (P.tail ? 1 : 0) + P.shift;
+    int grid = grid_for(vt, PER, TBL4 ? 1 : g_tt_wg_per_cu);
+    hipLaunchKernelGGL((k_aes_ctr_tt_cached<NR, B, T, TBL4>), dim3(grid), dim3(T), 0, st, P, K);
+    return hipGetLastError();
+}
+
+template <int NR>
+hipError_t launch_ctr_cached(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo, hipStream_t st)
+{
+    /* OTC_TT_VARIANT=<threads>x<B>: negative threads = 1-table layout (A/B
+     * measurements); default = 4-table layout, 1024 threads x 4 blocks/lane */
+    const TTVariant v = tt_variant();
+    if (v.threads == 1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, true>(P, K, ctr_lo, st);
+    if (v.threads == -1024 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, false>(P, K, ctr_lo, st);
+    if (v.threads == -1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, false>(P, K, ctr_lo, st);
+    return launch_ctr_cached_tb<NR, 1024, 4, true>(P, K, ctr_lo, st);
+}
+
+void tt_set_wg_per_cu(int n) { g_tt_wg_per_cu = n < 1 ? 1 : n; }
+
 hipError_t tt_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
                   hipStream_t st)
 {
+    if (getenv("OTC_TT_NOCACHE") == nullptr) {
+        CtrParams P{};
+        P.in = (const uint8_t *)in;
+        P.out = (uint8_t *)out;
+        P.nfull = nbytes / 16;
+        P.tail = (uint32_t)(nbytes % 16);
+        P.wrap64 = wrap64 ? 1u : 0u;
+        P.cbase.hi = c.hi;
+        switch (K.nr) {
+        case 10: return launch_ctr_cached<10>(P, K, c.lo, st);
+        case 12: return launch_ctr_cached<12>(P, K, c.lo, st);
+        case 14: return launch_ctr_cached<14>(P, K, c.lo, st);
+        default: return hipErrorInvalidValue;
+        }
+    }
     EncParams P{};
     P.in = (const uint8_t *)in;
     P.out = (uint8_t *)out;

@@ -44,6 +44,7 @@ hipError_t tt_cbc_decrypt_seg(const void *, void *, uint64_t, uint64_t, const ot
 hipError_t tt_cbc_encrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
 hipError_t bs_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
+void tt_set_wg_per_cu(int);
 hipError_t k_xor(const void *, const void *, void *, size_t, hipStream_t);
 hipError_t k_fill_random(void *, size_t, uint64_t, hipStream_t);
 hipError_t k_checksum(const void *, size_t, uint64_t *, hipStream_t);
@@ -103,11 +104,12 @@ void ctr_to_bytes(Ctr128 c, uint8_t out[16])
 
 int pick_impl(int impl, int bits)
 {
-    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE) return impl;
+    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_HYBRID) return impl;
     const char *env = getenv("OTC_IMPL");
     if (env) {
         if (!strcmp(env, "ttable")) return OTC_IMPL_TTABLE;
         if (!strcmp(env, "bitslice")) return OTC_IMPL_BITSLICE;
+        if (!strcmp(env, "hybrid")) return OTC_IMPL_HYBRID;
     }
     (void)bits;
     return OTC_IMPL_TTABLE; /* default: the measured winner (see docs/PERF.md) */
@@ -162,6 +164,62 @@ extern "C" int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_a
     return OTC_OK;
 }
 
+/* Hybrid CTR: the T-table kernel (LDS-bound, ~40% VALU) and the bitsliced
+ * kernel (VALU-only) run CONCURRENTLY on two streams over disjoint ranges, so
+ * each CU hosts one T-table workgroup (16 waves, 64 KiB LDS, 49 VGPRs) beside
+ * bitsliced waves (1 per SIMD, 256 VGPRs): the bitsliced waves soak up the
+ * VALU slack of the LDS-bound kernel.  OTC_HYBRID_TT = fraction of blocks
+ * given to the T-table kernel. */
+struct AuxStream {
+    int dev = -1;
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+thread_local AuxStream g_aux[16];
+
+hipError_t hybrid_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
+                      hipStream_t st)
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    AuxStream &a = g_aux[dev & 15];
+    if (a.dev != dev) {
+        if ((e = hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&a.e0, hipEventDisableTiming)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&a.e1, hipEventDisableTiming)) != hipSuccess) return e;
+        a.dev = dev;
+    }
+    double frac = 0.6;
+    if (const char *f = getenv("OTC_HYBRID_TT")) frac = atof(f);
+    const uint64_t nblk = nbytes / 16;
+    uint64_t ntt = (uint64_t)(nblk * frac);
+    ntt -= ntt % 2048;
+    if (ntt > nblk) ntt = nblk;
+    const size_t tt_bytes = ntt * 16;
+    /* order the aux stream after prior work on st */
+    if ((e = hipEventRecord(a.e0, st)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(a.s, a.e0, 0)) != hipSuccess) return e;
+    Ctr128 c2 = c;
+    c2.lo = c.lo + ntt;
+    if (!wrap64 && c2.lo < c.lo) c2.hi += 1;
+    /* persistent T-table grid (1 workgroup per CU) first, so its workgroups
+     * are resident before the bitsliced waves fill the remaining VGPRs */
+    if (tt_bytes) {
+        otc_impl::tt_set_wg_per_cu(1);
+        e = otc_impl::tt_ctr(in, out, tt_bytes, K, c, wrap64, st);
+        otc_impl::tt_set_wg_per_cu(2);
+        if (e != hipSuccess) return e;
+    }
+    if (nbytes > tt_bytes) {
+        e = otc_impl::bs_ctr((const uint8_t *)in + tt_bytes, (uint8_t *)out + tt_bytes, nbytes - tt_bytes, K, c2,
+                             wrap64, a.s);
+        if (e != hipSuccess) return e;
+    }
+    if ((e = hipEventRecord(a.e1, a.s)) != hipSuccess) return e;
+    return hipStreamWaitEvent(st, a.e1, 0);
+}
+
 static int ctr_common(const void *in, void *out, size_t nbytes, const otc_aes_key *k, Ctr128 c, bool wrap64,
                       int impl, void *stream)
 {
@@ -169,8 +227,10 @@ static int ctr_common(const void *in, void *out, size_t nbytes, const otc_aes_ke
     if (r) return r;
     if (nbytes == 0) return OTC_OK;
     hipStream_t st = (hipStream_t)stream;
-    hipError_t e = (pick_impl(impl, k->bits) == OTC_IMPL_BITSLICE) ? otc_impl::bs_ctr(in, out, nbytes, *k, c, wrap64, st)
-                                                                   : otc_impl::tt_ctr(in, out, nbytes, *k, c, wrap64, st);
+    const int im = pick_impl(impl, k->bits);
+    hipError_t e = im == OTC_IMPL_BITSLICE ? otc_impl::bs_ctr(in, out, nbytes, *k, c, wrap64, st)
+                   : im == OTC_IMPL_HYBRID ? hybrid_ctr(in, out, nbytes, *k, c, wrap64, st)
+                                           : otc_impl::tt_ctr(in, out, nbytes, *k, c, wrap64, st);
     if (e != hipSuccess) return hip_fail(e, "aes_ctr launch");
     return OTC_OK;
 }

@@ -61,6 +61,7 @@ int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 #define OTC_IMPL_AUTO 0
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
 #define OTC_IMPL_BITSLICE 2 /* 32-block-per-lane bitsliced VALU kernel */
+#define OTC_IMPL_HYBRID 3   /* CTR: T-table + bitsliced kernels co-resident on every CU */
 
 /* ---- device ops (device pointers; async on `stream`) ---------------------
  * All functions accept any byte length; the trailing partial block of CTR is

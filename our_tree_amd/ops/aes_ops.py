@@ -16,7 +16,7 @@ import torch
 from .. import _native
 from .keys import expand_key
 
-IMPLS = {"auto": 0, "ttable": 1, "bitslice": 2}
+IMPLS = {"auto": 0, "ttable": 1, "bitslice": 2, "hybrid": 3}
 
 
 def _impl(impl) -> int:
