@@ -28,6 +28,8 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "otc_bitslice.h"
 #include "otc_device.h"
 
@@ -50,7 +52,7 @@ enum : int { BS_CTR = 0, BS_ECB = 1 };
 
 __device__ __forceinline__ W lane_mask(uint32_t lane, int n) { return (W)(0u - ((lane >> n) & 1u)); }
 
-template <int NR, int MODE>
+template <int NR, int MODE, bool CACHE>
 __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
 {
     const uint32_t lane = threadIdx.x & 63u;
@@ -131,7 +133,7 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
             rk[q] = v;
         }
         /* rounds (AddRoundKey folded into the S-boxes; last key folded below) */
-        encrypt_planes<NR, MODE == BS_CTR>(s, [&](int r, int p) -> W {
+        encrypt_planes<NR, MODE == BS_CTR && CACHE>(s, [&](int r, int p) -> W {
             /* plane p = 32*w + q  <->  bit q of round-key word w */
             return (W)(0u - ((rk[4 * r + (p >> 5)] >> (p & 31)) & 1u));
         });
@@ -195,7 +197,11 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     uint64_t wgs = (tasks + 3) / 4;
     if (wgs < 1) wgs = 1;
     if (wgs > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_aes_bs<NR, MODE>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
+    static const bool cache = getenv("OTC_BS_CTR_CACHE") && atoi(getenv("OTC_BS_CTR_CACHE")) != 0;
+    if (MODE == BS_CTR && cache)
+        hipLaunchKernelGGL((k_aes_bs<NR, MODE, true>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
+    else
+        hipLaunchKernelGGL((k_aes_bs<NR, MODE, false>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
     return hipGetLastError();
 }
 

@@ -39,6 +39,8 @@ namespace {
 
 __device__ const AesTables g_tab = make_tables();
 
+
+
 constexpr uint32_t SEL(int k) { return 0x0c0c0000u | ((uint32_t)(4 + k) << 8); }
 /* second table (byte 2 of the address taken from lane word byte 2 = 1) */
 constexpr uint32_t SEL_HI(int k) { return 0x0c020000u | ((uint32_t)(4 + k) << 8); }

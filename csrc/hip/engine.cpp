@@ -206,6 +206,8 @@ hipError_t hybrid_ctr(const void *in, void *out, size_t nbytes, const otc_aes_ke
     /* persistent T-table grid (1 workgroup per CU) first, so its workgroups
      * are resident before the bitsliced waves fill the remaining VGPRs */
     if (tt_bytes) {
+        /* the T-table variant for co-residency is chosen by OTC_TT_VARIANT
+         * (B=2 keeps it at <= 64 VGPRs so a 256-VGPR bitsliced wave fits) */
         otc_impl::tt_set_wg_per_cu(1);
         e = otc_impl::tt_ctr(in, out, tt_bytes, K, c, wrap64, st);
         otc_impl::tt_set_wg_per_cu(2);
