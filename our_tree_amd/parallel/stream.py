@@ -96,25 +96,26 @@ def multi_gpu_run(mode: str, host_in, host_out, key: bytes, iv_or_counter: bytes
     return {"total_ms": st.total_ms, "gbps": st.gbps, "ngpus": st.ngpus, "strategy": strategy}
 
 
+class _PinnedOwner:
+    """Frees a hipHostMalloc allocation when the last numpy view dies."""
+
+    def __init__(self, lib, ptr):
+        self._lib, self.ptr = lib, ptr
+
+    def __del__(self):
+        try:
+            self._lib.otc_host_free_pinned(self.ptr)
+        except Exception:
+            pass
+
+
 def pinned_empty(nbytes: int) -> np.ndarray:
-    """A numpy view over hipHostMalloc'd (pinned) memory; freed with the array's
-    owner object."""
+    """A uint8 numpy array over pinned (hipHostMalloc) host memory, so the
+    engine copies it with DMA directly (no staging)."""
     lib = _native.require_gpu_lib()
     p = lib.otc_host_alloc_pinned(nbytes)
     if not p:
         raise MemoryError("hipHostMalloc failed")
     buf = (ctypes.c_uint8 * nbytes).from_address(p)
-    arr = np.frombuffer(buf, dtype=np.uint8)
-
-    class _Owner:
-        def __del__(self_inner):
-            lib.otc_host_free_pinned(p)
-
-    arr_owner = _Owner()
-    arr = arr.view()
-    arr.flags.writeable = True
-    _PINNED_OWNERS[id(arr)] = arr_owner
-    return arr
-
-
-_PINNED_OWNERS: dict = {}
+    buf._owner = _PinnedOwner(lib, p)  # lifetime: numpy view -> ctypes buffer -> owner
+    return np.frombuffer(buf, dtype=np.uint8)
