@@ -86,22 +86,43 @@ __device__ __forceinline__ void tbl4_lane_consts(uint32_t lane, uint32_t (&lk)[4
     for (int k = 0; k < 4; ++k) lk[k] = ((uint32_t)(k >> 1) << 16) | ((uint32_t)(k & 1) << 7) | ((lane & 31u) << 2);
 }
 
-template <int R0, int NR, int B>
+/* ISSUE_ALL: per round, issue every lookup of all B blocks before combining
+ * any of them.  hipcc otherwise consumes each ds_read right away (1-3 LDS ops
+ * in flight per wave); with at most 16 waves per CU (the 128 KiB table allows
+ * one workgroup) that starves the LDS pipe.  gfx9 lgkmcnt still caps a wave at
+ * 15 outstanding LDS ops. */
+template <int R0, int NR, int B, bool ISSUE_ALL = true>
 __device__ __forceinline__ void enc_rounds4_from(const uint32_t *tbl, const uint32_t (&lk)[4], const otc_aes_key &K,
                                                  uint32_t (&s)[B][4])
 {
 #pragma unroll
     for (int r = R0; r < NR; ++r) {
         uint32_t t[B][4];
+        if (ISSUE_ALL) {
+            uint32_t a[B][4][4];
 #pragma unroll
-        for (int b = 0; b < B; ++b) {
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lk[0], SEL_HI(0)));
-                uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lk[1], SEL_HI(1)));
-                uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lk[2], SEL_HI(2)));
-                uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lk[3], SEL_HI(3)));
-                t[b][j] = xor3(xor3(a0, a1, a2), a3, K.rk[4 * r + j]);
+                for (int b = 0; b < B; ++b)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        a[b][j][k] = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + k) & 3], lk[k], SEL_HI(k)));
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int b = 0; b < B; ++b)
+                    t[b][j] = xor3(xor3(a[b][j][0], a[b][j][1], a[b][j][2]), a[b][j][3], K.rk[4 * r + j]);
+        } else {
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lk[0], SEL_HI(0)));
+                    uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lk[1], SEL_HI(1)));
+                    uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lk[2], SEL_HI(2)));
+                    uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lk[3], SEL_HI(3)));
+                    t[b][j] = xor3(xor3(a0, a1, a2), a3, K.rk[4 * r + j]);
+                }
             }
         }
 #pragma unroll
@@ -110,17 +131,21 @@ __device__ __forceinline__ void enc_rounds4_from(const uint32_t *tbl, const uint
             for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
     }
     uint32_t t[B][4];
+    uint32_t a[B][4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                a[b][j][k] = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + k) & 3], lk[k], SEL_HI(k)));
 #pragma unroll
     for (int b = 0; b < B; ++b) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lk[0], SEL_HI(0)));
-            uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lk[1], SEL_HI(1)));
-            uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lk[2], SEL_HI(2)));
-            uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lk[3], SEL_HI(3)));
             /* S[x] sits in byte 1 of T0, byte 2 of T1, byte 3 of T2, byte 0 of T3 */
-            uint32_t lo = __builtin_amdgcn_perm(a1, a0, 0x0c0c0601u);
-            uint32_t hi = __builtin_amdgcn_perm(a3, a2, 0x04030c0cu);
+            uint32_t lo = __builtin_amdgcn_perm(a[b][j][1], a[b][j][0], 0x0c0c0601u);
+            uint32_t hi = __builtin_amdgcn_perm(a[b][j][3], a[b][j][2], 0x04030c0cu);
             t[b][j] = xor3(lo, hi, K.rk[4 * NR + j]);
         }
     }
@@ -413,7 +438,7 @@ struct CtrParams {
 
 __device__ __forceinline__ uint32_t te_u(uint32_t idx) { return g_tab.te0[idx & 0xFFu]; } /* uniform lookup */
 
-template <int NR, int B, int THREADS, bool TBL4>
+template <int NR, int B, int THREADS, bool TBL4, bool ISSUE_ALL = true>
 __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_aes_key K)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tbl[TBL4 ? 2 * 256 * 64 : 256 * 64];
@@ -482,7 +507,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_
         }
         /* rounds 3..NR */
         if (TBL4)
-            enc_rounds4_from<3, NR, B>(tbl, lk, K, s);
+            enc_rounds4_from<3, NR, B, ISSUE_ALL>(tbl, lk, K, s);
         else
             enc_rounds_from<3, NR, B>(tbl, lane4, K, s);
 
@@ -768,7 +793,7 @@ hipError_t tt_ecb_encrypt(const void *in, void *out, uint64_t nblocks, const otc
 
 int g_tt_wg_per_cu = 2; /* lowered to 1 while a co-resident bitsliced kernel runs (hybrid impl) */
 
-template <int NR, int T, int B, bool TBL4 = false>
+template <int NR, int T, int B, bool TBL4 = false, bool ISSUE_ALL = true>
 hipError_t launch_ctr_cached_tb(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo, hipStream_t st)
 {
     constexpr uint64_t PER = (uint64_t)T * B;
@@ -776,7 +801,7 @@ hipError_t launch_ctr_cached_tb(CtrParams P, const otc_aes_key &K, uint64_t ctr_
     P.cbase.lo = ctr_lo - P.shift;
     const uint64_t vt = P.nfull + (P.tail ? 1 : 0) + P.shift;
     int grid = grid_for(vt, PER, TBL4 ? 1 : g_tt_wg_per_cu);
-    hipLaunchKernelGGL((k_aes_ctr_tt_cached<NR, B, T, TBL4>), dim3(grid), dim3(T), 0, st, P, K);
+    hipLaunchKernelGGL((k_aes_ctr_tt_cached<NR, B, T, TBL4, ISSUE_ALL>), dim3(grid), dim3(T), 0, st, P, K);
     return hipGetLastError();
 }
 
@@ -787,6 +812,7 @@ hipError_t launch_ctr_cached(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo,
      * measurements); default = 4-table layout, 1024 threads x 4 blocks/lane */
     const TTVariant v = tt_variant();
     if (v.threads == 1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, true>(P, K, ctr_lo, st);
+    if (v.threads == 2 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, true, false>(P, K, ctr_lo, st);
     if (v.threads == -1024 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, false>(P, K, ctr_lo, st);
     if (v.threads == -1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, false>(P, K, ctr_lo, st);
     return launch_ctr_cached_tb<NR, 1024, 4, true>(P, K, ctr_lo, st);
