@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--gib", type=float, default=64.0, help="per-GPU shard size in GiB")
     ap.add_argument("--impl", default=os.environ.get("OTC_BENCH_IMPL", "auto"))
     ap.add_argument("--no-aes256", action="store_true")
+    ap.add_argument("--no-bitslice", action="store_true")
     args = ap.parse_args()
 
     from our_tree_amd import ops
@@ -80,19 +81,19 @@ def main():
             print(json.dumps({"error": "verification failed"}))
         sys.exit(1)
 
-    def step(k=key):
-        ops.ctr(buf, k, counter, out=buf, block_offset=my_block0, impl=args.impl)
+    def step(k=key, impl=args.impl):
+        ops.ctr(buf, k, counter, out=buf, block_offset=my_block0, impl=impl)
 
-    def timed(nsteps, k):
+    def timed(nsteps, k, impl=args.impl):
         for _ in range(args.warmup):
-            step(k)
+            step(k, impl)
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(nsteps):
-            step(k)
+            step(k, impl)
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
@@ -108,6 +109,12 @@ def main():
     cpb = (ms_per_step * 1e-3) * info["clock_hz"] * info["cus"] / nbytes
 
     extra = {}
+    if not args.no_bitslice and args.impl != "bitslice":
+        # BASELINE config 3 names the wave-bitsliced VALU kernel for this
+        # 64 GiB AES-128-CTR shard: time it too (same buffer, same protocol)
+        bs_steps = max(1, min(args.steps, 5))
+        el_bs = timed(bs_steps, key, impl="bitslice")
+        extra["bitsliced_ctr_gbps_whole_node"] = round(nbytes * world * bs_steps / el_bs / 1e9, 3)
     if not args.no_aes256:
         k256_steps = max(1, min(args.steps, 5))
         el256 = timed(k256_steps, key256)

@@ -52,7 +52,7 @@ enum : int { BS_CTR = 0, BS_ECB = 1 };
 
 __device__ __forceinline__ W lane_mask(uint32_t lane, int n) { return (W)(0u - ((lane >> n) & 1u)); }
 
-template <int NR, int MODE, bool CACHE>
+template <int NR, int MODE, bool CACHE, int PF>
 __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
 {
     const uint32_t lane = threadIdx.x & 63u;
@@ -140,6 +140,27 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
 
         pin_n(s, 128);
         sched_fence();
+
+        /* uniform task base (may point before the buffer for the first CTR
+         * task; those slots are masked) + 32-bit per-lane offsets */
+        const int64_t tstart = (int64_t)vbase - (int64_t)shift;
+        const uint8_t *ib = P.in + tstart * 16;
+        uint8_t *ob = P.out + tstart * 16;
+        uint32_t lo = lane * 16u;
+        /* ordered after the pin above (volatile asms keep their order), so
+         * the loads below cannot be hoisted into the round phase */
+        asm volatile("" : "+v"(lo));
+        auto slot_ok = [&](int k) {
+            const int64_t si = tstart + (int64_t)lane + 64 * k;
+            return full || (si >= 0 && (uint64_t)si < P.nblocks);
+        };
+        /* CTR plaintext is software-pipelined PF slots ahead: after the
+         * output transposes the first PF loads are issued, then each group of
+         * 4 slots issues the loads of the group PF/4 ahead (PF = 0: each group
+         * loads and waits for its own slots).  Issuing the first loads before
+         * the transposes instead pushes the kernel past 256 VGPRs. */
+        uint4 pt[32];
+        sched_fence();
         /* planes -> blocks (keystream / ciphertext without the last key) */
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
@@ -148,26 +169,28 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
             sched_fence();
         }
 
+        if (MODE == BS_CTR) {
+#pragma unroll
+            for (int k = 0; k < PF; ++k)
+                pt[k] = slot_ok(k) ? *(const uint4 *)(ib + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
+        }
         const uint32_t k0 = rk[4 * NR + 0], k1 = rk[4 * NR + 1], k2 = rk[4 * NR + 2],
                        k3 = rk[4 * NR + 3];
-        /* uniform task base (may point before the buffer for the first CTR
-         * task; those slots are masked) + 32-bit per-lane offsets */
-        const int64_t tstart = (int64_t)vbase - (int64_t)shift;
-        const uint8_t *ib = P.in + tstart * 16;
-        uint8_t *ob = P.out + tstart * 16;
-        const uint32_t lo = lane * 16u;
 #pragma unroll
         for (int k = 0; k < 32; ++k) {
-            /* bound the plaintext loads in flight (else all 32 x 16 B are
-             * hoisted and double the live registers) */
-            if ((k & 3) == 0) sched_fence();
-            const int64_t si = tstart + (int64_t)lane + 64 * k;
-            const bool ok = full || (si >= 0 && (uint64_t)si < P.nblocks);
+            if ((k & 3) == 0) {
+                sched_fence();
+                if (MODE == BS_CTR) {
+#pragma unroll
+                    for (int j = k + PF; j < k + PF + 4 && j < 32; ++j)
+                        pt[j] = slot_ok(j) ? *(const uint4 *)(ib + lo + 1024u * j) : make_uint4(0, 0, 0, 0);
+                }
+            }
             const uint32_t off = lo + 1024u * k;
-            if (ok) {
+            if (slot_ok(k)) {
                 uint4 o;
                 if (MODE == BS_CTR) {
-                    const uint4 x = *(const uint4 *)(ib + off);
+                    const uint4 x = pt[k];
                     o.x = x3(x.x, s[k], k0);
                     o.y = x3(x.y, s[32 + k], k1);
                     o.z = x3(x.z, s[64 + k], k2);
@@ -198,10 +221,20 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     if (wgs < 1) wgs = 1;
     if (wgs > 0xFFFFFFFFull) return hipErrorInvalidValue;
     static const bool cache = getenv("OTC_BS_CTR_CACHE") && atoi(getenv("OTC_BS_CTR_CACHE")) != 0;
-    if (MODE == BS_CTR && cache)
-        hipLaunchKernelGGL((k_aes_bs<NR, MODE, true>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
-    else
-        hipLaunchKernelGGL((k_aes_bs<NR, MODE, false>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
+    /* CTR plaintext prefetch distance: 8 slots for AES-128 (+1%, measured;
+     * OTC_BS_PF=0 turns it off).  AES-192/256 keep PF = 0: there the extra
+     * registers cost the second wave per SIMD (-45%). */
+    static const bool pf = !getenv("OTC_BS_PF") || atoi(getenv("OTC_BS_PF")) != 0;
+    if (MODE == BS_CTR && cache) {
+        hipLaunchKernelGGL((k_aes_bs<NR, MODE, true, 0>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
+    } else if constexpr (MODE == BS_CTR && NR == 10) {
+        if (pf)
+            hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 8>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
+        else
+            hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 0>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
+    } else {
+        hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 0>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
+    }
     return hipGetLastError();
 }
 

@@ -813,6 +813,7 @@ hipError_t launch_ctr_cached(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo,
     const TTVariant v = tt_variant();
     if (v.threads == 1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, true>(P, K, ctr_lo, st);
     if (v.threads == 2 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, true, false>(P, K, ctr_lo, st);
+    if (v.threads == 512 && v.b == 4) return launch_ctr_cached_tb<NR, 512, 4, true>(P, K, ctr_lo, st);
     if (v.threads == -1024 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, false>(P, K, ctr_lo, st);
     if (v.threads == -1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, false>(P, K, ctr_lo, st);
     return launch_ctr_cached_tb<NR, 1024, 4, true>(P, K, ctr_lo, st);
