@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cstdint>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -125,6 +126,26 @@ int check_key(const otc_aes_key *k, int dir)
     return OTC_OK;
 }
 
+/* Device buffers of the cipher ops: non-null, 16-byte aligned (every kernel
+ * moves 16 B per lane with global_load/store_dwordx4), and either the same
+ * buffer (in place, where the mode allows it) or disjoint -- a partial overlap
+ * would race between workgroups. */
+int check_bufs(const void *in, const void *out, size_t nbytes, bool inplace_ok, const char *what)
+{
+    if (nbytes == 0) return OTC_OK;
+    if (!in || !out) return set_err(OTC_ERR_ARG, std::string(what) + ": null buffer");
+    if (((uintptr_t)in | (uintptr_t)out) & 15u)
+        return set_err(OTC_ERR_ARG, std::string(what) + ": device buffers must be 16-byte aligned");
+    if (in == out) {
+        if (!inplace_ok) return set_err(OTC_ERR_ARG, std::string(what) + ": in-place operation is not supported");
+        return OTC_OK;
+    }
+    const uintptr_t a = (uintptr_t)in, b = (uintptr_t)out;
+    if (a < b + nbytes && b < a + nbytes)
+        return set_err(OTC_ERR_ARG, std::string(what) + ": input and output overlap partially");
+    return OTC_OK;
+}
+
 } // namespace
 
 /* ---- errors / keys ------------------------------------------------------ */
@@ -151,6 +172,7 @@ extern "C" int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_a
 {
     if (nbytes % 16) return set_err(OTC_ERR_ARG, "ECB length must be a multiple of 16");
     if (!k) return set_err(OTC_ERR_ARG, "null key");
+    if (int r = check_bufs(in, out, nbytes, true, "aes_ecb")) return r;
     if (nbytes == 0) return OTC_OK;
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
@@ -165,11 +187,11 @@ extern "C" int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_a
 }
 
 /* Hybrid CTR: the T-table kernel (LDS-bound, ~40% VALU) and the bitsliced
- * kernel (VALU-only) run CONCURRENTLY on two streams over disjoint ranges, so
- * each CU hosts one T-table workgroup (16 waves, 64 KiB LDS, 49 VGPRs) beside
- * bitsliced waves (1 per SIMD, 256 VGPRs): the bitsliced waves soak up the
- * VALU slack of the LDS-bound kernel.  OTC_HYBRID_TT = fraction of blocks
- * given to the T-table kernel. */
+ * kernel (VALU-only) run CONCURRENTLY on two streams over disjoint ranges.
+ * With OTC_TT_VARIANT=1024x2 (64 VGPRs x 4 waves) or 512x4 (112 x 2) each CU
+ * hosts one T-table workgroup beside one 256-VGPR bitsliced wave per SIMD.
+ * OTC_HYBRID_TT = fraction of blocks given to the T-table kernel.  Measured
+ * slower than the T-table alone (docs/PERF.md): kept as an option. */
 struct AuxStream {
     int dev = -1;
     hipStream_t s = nullptr;
@@ -227,6 +249,7 @@ static int ctr_common(const void *in, void *out, size_t nbytes, const otc_aes_ke
 {
     int r = check_key(k, OTC_DIR_ENCRYPT);
     if (r) return r;
+    if ((r = check_bufs(in, out, nbytes, true, "aes_ctr"))) return r;
     if (nbytes == 0) return OTC_OK;
     hipStream_t st = (hipStream_t)stream;
     const int im = pick_impl(impl, k->bits);
@@ -262,7 +285,8 @@ extern "C" int otc_aes_cbc_decrypt(const void *in, void *out, size_t nbytes, con
     int r = check_key(k, OTC_DIR_DECRYPT);
     if (r) return r;
     if (nbytes % 16) return set_err(OTC_ERR_ARG, "CBC length must be a multiple of 16");
-    if (in == out && nbytes > 16) return set_err(OTC_ERR_ARG, "in-place CBC decryption is not supported");
+    if (!iv) return set_err(OTC_ERR_ARG, "null iv");
+    if ((r = check_bufs(in, out, nbytes, nbytes <= 16, "aes_cbc_decrypt"))) return r;
     if (nbytes == 0) return OTC_OK;
     hipError_t e = otc_impl::tt_cbc_decrypt(in, out, nbytes / 16, *k, ctr_from_bytes(iv), (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "cbc_decrypt launch");
@@ -275,6 +299,9 @@ extern "C" int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t se
     int r = check_key(k, OTC_DIR_ENCRYPT);
     if (r) return r;
     if (seg_bytes % 16) return set_err(OTC_ERR_ARG, "segment length must be a multiple of 16");
+    if (!iv0) return set_err(OTC_ERR_ARG, "null iv");
+    if (nseg && seg_bytes > SIZE_MAX / nseg) return set_err(OTC_ERR_ARG, "size overflow");
+    if ((r = check_bufs(in, out, seg_bytes * nseg, true, "aes_cbc_encrypt_segments"))) return r;
     if (nseg == 0 || seg_bytes == 0) return OTC_OK;
     hipError_t e = otc_impl::tt_cbc_encrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
                                                 (hipStream_t)stream);
@@ -290,7 +317,9 @@ extern "C" int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t se
     if (seg_bytes % 16) return set_err(OTC_ERR_ARG, "segment length must be a multiple of 16");
     size_t sb = seg_bytes / 16;
     if (sb == 0) return set_err(OTC_ERR_ARG, "empty segments");
-    if (in == out) return set_err(OTC_ERR_ARG, "in-place CBC decryption is not supported");
+    if (!iv0) return set_err(OTC_ERR_ARG, "null iv");
+    if (nseg && seg_bytes > SIZE_MAX / nseg) return set_err(OTC_ERR_ARG, "size overflow");
+    if ((r = check_bufs(in, out, seg_bytes * nseg, false, "aes_cbc_decrypt_segments"))) return r;
     if (nseg == 0) return OTC_OK;
     hipError_t e = otc_impl::tt_cbc_decrypt_seg(in, out, sb, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "cbc_decrypt_segments launch");
@@ -303,7 +332,8 @@ extern "C" int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, 
     int r = check_key(k, OTC_DIR_ENCRYPT);
     if (r) return r;
     if (nbytes % 16) return set_err(OTC_ERR_ARG, "CFB128 device path needs a multiple of 16 bytes");
-    if (in == out && nbytes > 16) return set_err(OTC_ERR_ARG, "in-place CFB decryption is not supported");
+    if (!iv) return set_err(OTC_ERR_ARG, "null iv");
+    if ((r = check_bufs(in, out, nbytes, nbytes <= 16, "aes_cfb128_decrypt"))) return r;
     if (nbytes == 0) return OTC_OK;
     uint32_t ivw[4];
     memcpy(ivw, iv, 16);
@@ -314,6 +344,8 @@ extern "C" int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, 
 
 extern "C" int otc_xor(const void *a, const void *b, void *out, size_t nbytes, void *stream)
 {
+    if (int r = check_bufs(a, out, nbytes, true, "xor")) return r;
+    if (int r = check_bufs(b, out, nbytes, true, "xor")) return r;
     if (nbytes == 0) return OTC_OK;
     hipError_t e = otc_impl::k_xor(a, b, out, nbytes, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "xor launch");
@@ -325,6 +357,12 @@ extern "C" int otc_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, s
 {
     if (keylen < 1 || keylen > 256) return set_err(OTC_ERR_ARG, "RC4 key length must be 1..256");
     if (nstreams == 0 || len == 0) return OTC_OK;
+    if (!keys || !out) return set_err(OTC_ERR_ARG, "rc4_multi: null buffer");
+    if (len > SIZE_MAX / nstreams) return set_err(OTC_ERR_ARG, "size overflow");
+    if (in && in != out) {
+        const uintptr_t a = (uintptr_t)in, b = (uintptr_t)out, n = nstreams * len;
+        if (a < b + n && b < a + n) return set_err(OTC_ERR_ARG, "rc4_multi: input and output overlap partially");
+    }
     hipError_t e = otc_impl::k_rc4_multi(keys, keylen, nstreams, len, drop, in, out, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "rc4_multi launch");
     return OTC_OK;
@@ -333,6 +371,7 @@ extern "C" int otc_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, s
 extern "C" int otc_fill_random(void *p, size_t nbytes, uint64_t seed, void *stream)
 {
     if (nbytes == 0) return OTC_OK;
+    if (int r = check_bufs(p, p, nbytes, true, "fill_random")) return r;
     hipError_t e = otc_impl::k_fill_random(p, nbytes, seed, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "fill_random launch");
     return OTC_OK;
@@ -341,6 +380,8 @@ extern "C" int otc_fill_random(void *p, size_t nbytes, uint64_t seed, void *stre
 extern "C" int otc_checksum(const void *p, size_t nbytes, uint64_t *out_dev, void *stream)
 {
     if (nbytes % 8) return set_err(OTC_ERR_ARG, "checksum length must be a multiple of 8");
+    if (!out_dev || (nbytes && !p)) return set_err(OTC_ERR_ARG, "checksum: null buffer");
+    if (((uintptr_t)p | (uintptr_t)out_dev) & 7u) return set_err(OTC_ERR_ARG, "checksum: buffers must be 8-byte aligned");
     hipError_t e = otc_impl::k_checksum(p, nbytes, out_dev, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "checksum launch");
     return OTC_OK;
@@ -531,6 +572,29 @@ static bool is_pinned(const void *p)
 /* Launch the cipher on one device chunk. `blk0` = block offset of the chunk
  * inside the whole stream; `prev` = for CBC-dec, the 16-byte ciphertext block
  * preceding the chunk (the halo), as counter-style numeric IV. */
+/* Up-front validation of a host-streamed job (engine and multi-GPU), so a bad
+ * call fails before any allocation or copy is issued. */
+static int check_stream_args(int mode, const void *host_in, const void *host_out, size_t nbytes,
+                             const otc_aes_key *k, const uint8_t ivc[16])
+{
+    if (mode != OTC_MODE_ECB && mode != OTC_MODE_CTR && mode != OTC_MODE_CBC_DEC)
+        return set_err(OTC_ERR_ARG, "unsupported streaming mode");
+    if (mode != OTC_MODE_CTR && nbytes % 16) return set_err(OTC_ERR_ARG, "length must be a multiple of 16");
+    if (nbytes && (!host_in || !host_out)) return set_err(OTC_ERR_ARG, "null host buffer");
+    if (!k) return set_err(OTC_ERR_ARG, "null key");
+    if (mode == OTC_MODE_CTR || mode == OTC_MODE_CBC_DEC) {
+        if (!ivc) return set_err(OTC_ERR_ARG, "null iv/counter");
+        if (int r = check_key(k, mode == OTC_MODE_CTR ? OTC_DIR_ENCRYPT : OTC_DIR_DECRYPT)) return r;
+    } else if (int r = check_key(k, k->dir)) {
+        return r;
+    }
+    if (host_in != host_out && nbytes) {
+        const uintptr_t a = (uintptr_t)host_in, b = (uintptr_t)host_out;
+        if (a < b + nbytes && b < a + nbytes) return set_err(OTC_ERR_ARG, "input and output overlap partially");
+    }
+    return OTC_OK;
+}
+
 static int run_chunk(int mode, const void *din, void *dout, size_t n, const otc_aes_key *k, const uint8_t ivc[16],
                      uint64_t blk0, const uint8_t *halo, int impl, hipStream_t st)
 {
@@ -547,7 +611,7 @@ extern "C" int otc_engine_run(otc_engine *e, int mode, const void *host_in, void
                               otc_stream_stats *stats)
 {
     if (!e) return set_err(OTC_ERR_ARG, "null engine");
-    if (mode != OTC_MODE_CTR && nbytes % 16) return set_err(OTC_ERR_ARG, "length must be a multiple of 16");
+    if (int r = check_stream_args(mode, host_in, host_out, nbytes, k, ivc)) return r;
     if (mode == OTC_MODE_CBC_DEC && block_offset) return set_err(OTC_ERR_ARG, "CBC: pass the halo as iv instead");
     HIPCHK(hipSetDevice(e->device));
     auto t0 = std::chrono::steady_clock::now();
@@ -628,9 +692,9 @@ extern "C" int otc_multi_run(int ngpus, int strategy, int mode, const void *host
                              const otc_aes_key *k, const uint8_t ivc[16], int impl, size_t chunk_bytes,
                              otc_multi_stats *stats)
 {
+    if (int r = check_stream_args(mode, host_in, host_out, nbytes, k, ivc)) return r;
     int ndev = otc_device_count();
     if (ngpus < 1 || ngpus > ndev) return set_err(OTC_ERR_ARG, "ngpus out of range");
-    if (nbytes % 16 && mode != OTC_MODE_CTR) return set_err(OTC_ERR_ARG, "length must be a multiple of 16");
     const size_t nblk = (nbytes + 15) / 16;
     /* planner: contiguous block-aligned shards, remainder spread over the
      * first shards (nothing dropped, unlike reference test.c:50) */

@@ -141,7 +141,8 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
         }
         if (live) {
             uint4 o = make_uint4(w[0], w[1], w[2], w[3]);
-            if (((base + n) & 15) == 0) {
+            /* 16-byte path only where both pointers are 16-byte aligned */
+            if ((((uintptr_t)(out + base + n) | (in ? (uintptr_t)(in + base + n) : 0)) & 15u) == 0) {
                 if (in) {
                     const uint4 x = *reinterpret_cast<const uint4 *>(in + base + n);
                     o.x ^= x.x; o.y ^= x.y; o.z ^= x.z; o.w ^= x.w;

@@ -54,6 +54,32 @@ def _out_like(x: torch.Tensor, out):
     return out
 
 
+def _bytes(t: torch.Tensor) -> torch.Tensor:
+    """Flat uint8 view of a contiguous tensor."""
+    return t.reshape(-1).view(torch.uint8)
+
+
+def _run(x: torch.Tensor, out: torch.Tensor, call):
+    """call(in_ptr, out_ptr) -> rc.  The kernels move 16 bytes per lane, so the
+    native API requires 16-byte aligned buffers; a misaligned tensor (e.g. a
+    byte slice ``t[3:]``) is staged through an aligned temporary (torch's
+    allocator aligns every fresh allocation) and copied back."""
+    xp, op = x.data_ptr(), out.data_ptr()
+    if not (xp % 16 or op % 16) or _nbytes(x) == 0:
+        return call(xp, op)
+    xi = _bytes(x).clone() if xp % 16 else _bytes(x)
+    if op == xp:
+        xo = xi  # in place stays in place (the native API rejects modes that forbid it)
+    elif op % 16:
+        xo = torch.empty_like(xi)
+    else:
+        xo = _bytes(out)
+    rc = call(xi.data_ptr(), xo.data_ptr())
+    if rc == 0 and xo.data_ptr() != op:
+        _bytes(out).copy_(xo)
+    return rc
+
+
 def _b16(v, name) -> ctypes.Array:
     v = bytes(v)
     if len(v) != 16:
@@ -72,8 +98,8 @@ def ctr(x: torch.Tensor, key: bytes, counter: bytes, out: torch.Tensor | None = 
     out = _out_like(x, out)
     k = expand_key(key)
     with torch.cuda.device(x.device):
-        rc = _lib().otc_aes_ctr(x.data_ptr(), out.data_ptr(), _nbytes(x), ctypes.byref(k), _b16(counter, "counter"),
-                                int(block_offset), _impl(impl), _stream(x))
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_ctr(ip, op, _nbytes(x), ctypes.byref(k), _b16(counter, "counter"),
+            int(block_offset), _impl(impl), _stream(x)))
     _native.check(rc, "otc_aes_ctr")
     return out
 
@@ -88,8 +114,8 @@ def ctr_rfc3686(x: torch.Tensor, key: bytes, nonce: bytes, ivec: bytes, out=None
     n = (ctypes.c_uint8 * 4).from_buffer_copy(bytes(nonce))
     iv = (ctypes.c_uint8 * 8).from_buffer_copy(bytes(ivec))
     with torch.cuda.device(x.device):
-        rc = _lib().otc_aes_ctr_rfc3686(x.data_ptr(), out.data_ptr(), _nbytes(x), ctypes.byref(k), n, iv,
-                                        int(block_offset), _impl(impl), _stream(x))
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_ctr_rfc3686(ip, op, _nbytes(x), ctypes.byref(k), n, iv,
+            int(block_offset), _impl(impl), _stream(x)))
     _native.check(rc, "otc_aes_ctr_rfc3686")
     return out
 
@@ -99,7 +125,7 @@ def ecb_encrypt(x: torch.Tensor, key: bytes, out=None, impl="auto") -> torch.Ten
     out = _out_like(x, out)
     k = expand_key(key)
     with torch.cuda.device(x.device):
-        rc = _lib().otc_aes_ecb(x.data_ptr(), out.data_ptr(), _nbytes(x), ctypes.byref(k), _impl(impl), _stream(x))
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_ecb(ip, op, _nbytes(x), ctypes.byref(k), _impl(impl), _stream(x)))
     _native.check(rc, "otc_aes_ecb(encrypt)")
     return out
 
@@ -109,7 +135,7 @@ def ecb_decrypt(x: torch.Tensor, key: bytes, out=None) -> torch.Tensor:
     out = _out_like(x, out)
     k = expand_key(key, decrypt=True)
     with torch.cuda.device(x.device):
-        rc = _lib().otc_aes_ecb(x.data_ptr(), out.data_ptr(), _nbytes(x), ctypes.byref(k), 0, _stream(x))
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_ecb(ip, op, _nbytes(x), ctypes.byref(k), 0, _stream(x)))
     _native.check(rc, "otc_aes_ecb(decrypt)")
     return out
 
@@ -120,8 +146,8 @@ def cbc_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None) -> torch.Tenso
     out = _out_like(x, out)
     k = expand_key(key, decrypt=True)
     with torch.cuda.device(x.device):
-        rc = _lib().otc_aes_cbc_decrypt(x.data_ptr(), out.data_ptr(), _nbytes(x), ctypes.byref(k), _b16(iv, "iv"),
-                                        _stream(x))
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_cbc_decrypt(ip, op, _nbytes(x), ctypes.byref(k), _b16(iv, "iv"),
+            _stream(x)))
     _native.check(rc, "otc_aes_cbc_decrypt")
     return out
 
@@ -136,8 +162,8 @@ def cbc_encrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes:
         raise ValueError("byte size must be a multiple of segment_bytes")
     k = expand_key(key)
     with torch.cuda.device(x.device):
-        rc = _lib().otc_aes_cbc_encrypt_segments(x.data_ptr(), out.data_ptr(), segment_bytes, n // segment_bytes,
-                                                 ctypes.byref(k), _b16(iv0, "iv0"), _stream(x))
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_cbc_encrypt_segments(ip, op, segment_bytes, n // segment_bytes,
+            ctypes.byref(k), _b16(iv0, "iv0"), _stream(x)))
     _native.check(rc, "otc_aes_cbc_encrypt_segments")
     return out
 
@@ -150,8 +176,8 @@ def cbc_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes:
         raise ValueError("byte size must be a multiple of segment_bytes")
     k = expand_key(key, decrypt=True)
     with torch.cuda.device(x.device):
-        rc = _lib().otc_aes_cbc_decrypt_segments(x.data_ptr(), out.data_ptr(), segment_bytes, n // segment_bytes,
-                                                 ctypes.byref(k), _b16(iv0, "iv0"), _stream(x))
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_cbc_decrypt_segments(ip, op, segment_bytes, n // segment_bytes,
+            ctypes.byref(k), _b16(iv0, "iv0"), _stream(x)))
     _native.check(rc, "otc_aes_cbc_decrypt_segments")
     return out
 
@@ -161,7 +187,7 @@ def cfb128_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None) -> torch.Te
     out = _out_like(x, out)
     k = expand_key(key)
     with torch.cuda.device(x.device):
-        rc = _lib().otc_aes_cfb128_decrypt(x.data_ptr(), out.data_ptr(), _nbytes(x), ctypes.byref(k), _b16(iv, "iv"),
-                                           _stream(x))
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_cfb128_decrypt(ip, op, _nbytes(x), ctypes.byref(k), _b16(iv, "iv"),
+            _stream(x)))
     _native.check(rc, "otc_aes_cfb128_decrypt")
     return out

@@ -7,7 +7,7 @@ import ctypes
 import torch
 
 from .. import _native
-from .aes_ops import _check_dev, _nbytes, _stream
+from .aes_ops import _bytes, _check_dev, _nbytes, _run, _stream
 
 
 def xor(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -17,8 +17,11 @@ def xor(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> to
     if _nbytes(a) != _nbytes(b):
         raise ValueError("a and b must have the same byte size")
     out = torch.empty_like(a) if out is None else out
+    if b.data_ptr() % 16:
+        b = _bytes(b).clone()  # 16-byte alignment (a and out are staged by _run)
     with torch.cuda.device(a.device):
-        rc = _native.require_gpu_lib().otc_xor(a.data_ptr(), b.data_ptr(), out.data_ptr(), _nbytes(a), _stream(a))
+        rc = _run(a, out, lambda ip, op: _native.require_gpu_lib().otc_xor(
+            ip, b.data_ptr(), op, _nbytes(a), _stream(a)))
     _native.check(rc, "otc_xor")
     return out
 
@@ -50,7 +53,8 @@ def fill_random_(t: torch.Tensor, seed: int = 0) -> torch.Tensor:
     """Fill ``t`` in place with deterministic pseudo-random bytes (splitmix64)."""
     _check_dev(t, "t")
     with torch.cuda.device(t.device):
-        rc = _native.require_gpu_lib().otc_fill_random(t.data_ptr(), _nbytes(t), seed & (2**64 - 1), _stream(t))
+        rc = _run(t, t, lambda ip, op: _native.require_gpu_lib().otc_fill_random(
+            op, _nbytes(t), seed & (2**64 - 1), _stream(t)))
     _native.check(rc, "otc_fill_random")
     return t
 
@@ -59,6 +63,8 @@ def checksum(t: torch.Tensor) -> int:
     """Position-dependent 64-bit XOR fold of a device buffer (byte size % 8 == 0)."""
     _check_dev(t, "t")
     acc = torch.zeros(1, dtype=torch.int64, device=t.device)
+    if t.data_ptr() % 8:
+        t = _bytes(t).clone()  # the fold reads 8-byte words
     with torch.cuda.device(t.device):
         rc = _native.require_gpu_lib().otc_checksum(t.data_ptr(), _nbytes(t), acc.data_ptr(), _stream(t))
     _native.check(rc, "otc_checksum")

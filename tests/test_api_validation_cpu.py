@@ -1,0 +1,117 @@
+"""Fault injection against the native device API (csrc/hip/engine.cpp, C API
+csrc/include/otc.h) without a GPU: every bad argument -- misaligned or null
+pointers, partial overlaps, bad lengths, wrong key schedules, size overflow --
+must be rejected with OTC_ERR_ARG and a message *before* any HIP call, so the
+fake pointers below are never dereferenced.  (The reference checks nothing:
+AES.cu:217-254 ignores every CUDA return code; SURVEY.md section 5 "Failure
+detection".)"""
+import ctypes
+
+import pytest
+
+from our_tree_amd import _native
+
+ERR_ARG = -1
+ENC, DEC = 1, 0
+A = 0x7F0000000000  # fake, 16-byte aligned device addresses (never touched)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not _native.gpu_lib_available():
+        pytest.skip("libotc.so not built")
+    return _native.require_gpu_lib()
+
+
+def key(lib, bits=128, d=ENC):
+    k = _native.OtcAesKey()
+    assert lib.otc_aes_key_init(ctypes.byref(k), _native.as_u8p(bytes(range(bits // 8))), bits, d) == 0
+    return k
+
+
+def err(lib) -> str:
+    return lib.otc_last_error().decode()
+
+
+def c16():
+    return (ctypes.c_uint8 * 16)()
+
+
+def test_key_init_rejects_bad_sizes(lib):
+    k = _native.OtcAesKey()
+    assert lib.otc_aes_key_init(ctypes.byref(k), _native.as_u8p(bytes(20)), 160, ENC) == ERR_ARG
+    assert "128/192/256" in err(lib)
+
+
+@pytest.mark.parametrize("inp,out,what", [
+    (A + 1, A + 4096, "aligned"),
+    (A, A + 4096 + 8, "aligned"),
+    (None, A, "null"),
+    (A, None, "null"),
+    (A, A + 16, "overlap"),
+    (A + 32, A, "overlap"),
+])
+def test_ctr_rejects_bad_buffers(lib, inp, out, what):
+    k = key(lib)
+    rc = lib.otc_aes_ctr(inp, out, 1024, ctypes.byref(k), c16(), 0, 0, None)
+    assert rc == ERR_ARG and what in err(lib)
+
+
+def test_zero_length_is_a_noop(lib):
+    k = key(lib)
+    assert lib.otc_aes_ctr(None, None, 0, ctypes.byref(k), c16(), 0, 0, None) == 0
+    assert lib.otc_aes_ecb(A + 3, A + 5, 0, ctypes.byref(k), 0, None) == 0
+
+
+def test_ecb_length_and_alignment(lib):
+    k = key(lib)
+    assert lib.otc_aes_ecb(A, A + 4096, 17, ctypes.byref(k), 0, None) == ERR_ARG
+    assert "multiple of 16" in err(lib)
+    assert lib.otc_aes_ecb(A + 8, A + 4096, 32, ctypes.byref(k), 0, None) == ERR_ARG
+
+
+def test_wrong_schedule_direction(lib):
+    kd = key(lib, 256, DEC)
+    assert lib.otc_aes_ctr(A, A + 4096, 64, ctypes.byref(kd), c16(), 0, 0, None) == ERR_ARG
+    assert "encryption schedule" in err(lib)
+    ke = key(lib, 192, ENC)
+    assert lib.otc_aes_cbc_decrypt(A, A + 4096, 64, ctypes.byref(ke), c16(), None) == ERR_ARG
+    assert "decryption schedule" in err(lib)
+
+
+def test_cbc_cfb_in_place_rules(lib):
+    kd, ke = key(lib, 128, DEC), key(lib, 128, ENC)
+    assert lib.otc_aes_cbc_decrypt(A, A, 64, ctypes.byref(kd), c16(), None) == ERR_ARG
+    assert "in-place" in err(lib)
+    assert lib.otc_aes_cfb128_decrypt(A, A, 64, ctypes.byref(ke), c16(), None) == ERR_ARG
+    assert lib.otc_aes_cbc_decrypt_segments(A, A, 64, 4, ctypes.byref(kd), c16(), None) == ERR_ARG
+    assert lib.otc_aes_cbc_decrypt(A, A + 4096, 64, ctypes.byref(kd), None, None) == ERR_ARG
+    assert "null iv" in err(lib)
+
+
+def test_segment_size_overflow(lib):
+    k = key(lib)
+    big = 1 << 62
+    assert lib.otc_aes_cbc_encrypt_segments(A, A + 4096, big, 16, ctypes.byref(k), c16(), None) == ERR_ARG
+    assert "overflow" in err(lib)
+    assert lib.otc_aes_cbc_encrypt_segments(A, A + 4096, 20, 2, ctypes.byref(k), c16(), None) == ERR_ARG
+
+
+def test_stream_ops_validation(lib):
+    assert lib.otc_xor(A + 4, A + 4096, A + 8192, 64, None) == ERR_ARG
+    assert lib.otc_xor(A, A + 4096, A + 4096 + 16, 64, None) == ERR_ARG  # b overlaps out
+    assert lib.otc_checksum(A + 4, 64, A + 4096, None) == ERR_ARG
+    assert lib.otc_checksum(A, 63, A + 4096, None) == ERR_ARG
+    assert lib.otc_rc4_multi(A, 0, 4, 16, 0, None, A + 4096, None) == ERR_ARG
+    assert lib.otc_rc4_multi(A, 257, 4, 16, 0, None, A + 4096, None) == ERR_ARG
+    assert lib.otc_rc4_multi(A, 16, 4, 64, 0, A, A + 16, None) == ERR_ARG
+    assert "overlap" in err(lib)
+    assert lib.otc_fill_random(A + 2, 64, 1, None) == ERR_ARG
+
+
+def test_engine_and_multi_reject_bad_arguments(lib):
+    assert lib.otc_engine_run(None, 1, None, None, 16, None, None, 0, 0, None) == ERR_ARG
+    st = _native.MultiStats() if hasattr(_native, "MultiStats") else None
+    rc = lib.otc_multi_run(0, 0, 1, None, None, 16, None, None, 0, 0,
+                           ctypes.byref(st) if st is not None else None)
+    assert rc == ERR_ARG

@@ -208,3 +208,61 @@ def test_errors_are_loud(gpu):
     y = rnd(32, gpu)
     with pytest.raises(RuntimeError):
         ops.cbc_decrypt(y, os.urandom(16), os.urandom(16), out=y)  # in-place unsupported
+
+
+@pytest.mark.parametrize("off_in,off_out", [(1, 0), (0, 3), (5, 5), (8, 8)])
+def test_misaligned_tensors_are_staged(gpu, off_in, off_out):
+    """Byte slices at any offset work (the native API needs 16-byte alignment;
+    ops stage misaligned tensors through aligned temporaries)."""
+    key, ctr0 = os.urandom(16), os.urandom(16)
+    n = 4096 * 16 + 7
+    base_in, base_out = rnd(n + 64, gpu, 21), torch.zeros(n + 64, dtype=torch.uint8, device=gpu)
+    x = base_in[off_in:off_in + n]
+    out = base_out[off_out:off_out + n]
+    ops.ctr(x, key, ctr0, out=out)
+    assert host(out) == cpu_ref.ctr(key, ctr0, host(x))
+    assert host(base_out[:off_out]) == bytes(off_out)  # nothing written outside the slice
+    assert host(base_out[off_out + n:]) == bytes(64 - off_out)
+    # in place on a misaligned slice
+    y = base_in[off_in:off_in + n]
+    ref = cpu_ref.ctr(key, ctr0, host(y))
+    ops.ctr(y, key, ctr0, out=y)
+    assert host(y) == ref
+    # ECB / CBC-decrypt / XOR / fill / checksum on misaligned slices
+    m = 16 * 1000
+    e = rnd(m + 16, gpu, 22)[off_in:off_in + m]
+    c = ops.ecb_encrypt(e, key)
+    assert host(c) == cpu_ref.ecb(key, host(e))
+    iv = os.urandom(16)
+    dst = torch.empty(m + 16, dtype=torch.uint8, device=gpu)[off_out:off_out + m]
+    ops.cbc_decrypt(e, key, iv, out=dst)
+    assert host(dst) == cpu_ref.cbc(key, iv, host(e), decrypt=True)
+    a, b = rnd(m + 9, gpu, 23)[off_in:off_in + m], rnd(m + 9, gpu, 24)[off_out:off_out + m]
+    assert torch.equal(ops.xor(a, b), a ^ b)
+    f = torch.empty(m + 9, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(f[off_in:off_in + m], 7)
+    g = torch.empty(m, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(g, 7)
+    assert torch.equal(f[off_in:off_in + m], g)
+    assert ops.checksum(f[off_in:off_in + m]) == ops.checksum(g)
+
+
+def test_partial_overlap_is_rejected(gpu):
+    buf = rnd(1 << 16, gpu, 25)
+    with pytest.raises(RuntimeError, match="overlap"):
+        ops.ctr(buf[:4096], os.urandom(16), os.urandom(16), out=buf[16:4112])
+
+
+@pytest.mark.parametrize("impl", IMPLS)
+def test_deterministic_rerun(gpu, impl):
+    """Run twice, compare (race detection): no kernel has
+    shared mutable state, so repeated runs are bit-identical."""
+    key, ctr0 = os.urandom(32), os.urandom(16)
+    x = rnd(64 << 20, gpu, 26)
+    y1 = ops.ctr(x, key, ctr0, impl=impl)
+    y2 = ops.ctr(x, key, ctr0, impl=impl)
+    assert torch.equal(y1, y2)
+    e1 = ops.ecb_encrypt(x, key, impl=impl)
+    e2 = ops.ecb_encrypt(x, key, impl=impl)
+    assert torch.equal(e1, e2)
+    assert torch.equal(ops.ecb_decrypt(e1, key), x)
