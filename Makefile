@@ -5,6 +5,8 @@
 #                      bin/test bin/aes_test bin/aes_ecb_e bin/aes_ecb_d bin/otbench
 #   make cpu        -> CPU-only pieces (no hipcc needed)
 #   make SAN=1 cpu  -> CPU oracle with ASan/UBSan (host only)
+#   make SAN=thread cpu -> CPU oracle with ThreadSanitizer (host only)
+#   make san-check  -> build csrc/cli/san_driver.c with TSan and ASan+UBSan, run both
 #
 # Reference build: Makefile:1-56 (gcc -O0), aes-modes/Makefile (clang -O0,
 # broken on current compilers), aes-gpu/Source/Makefile.asc (nvcc, no -arch).
@@ -23,6 +25,11 @@ ifeq ($(SAN),1)
 CFLAGS   += -fsanitize=address,undefined -fno-omit-frame-pointer
 CXXFLAGS += -fsanitize=address,undefined -fno-omit-frame-pointer
 SANLD    := -fsanitize=address,undefined
+endif
+ifeq ($(SAN),thread)
+CFLAGS   += -fsanitize=thread
+CXXFLAGS += -fsanitize=thread
+SANLD    := -fsanitize=thread
 endif
 
 LIBDIR := our_tree_amd/lib
@@ -66,7 +73,7 @@ $(OBJ)/hip/engine.o: csrc/hip/engine.cpp csrc/hip/otc_device.h csrc/include/otc.
 
 $(LIBDIR)/libotc.so: $(HIP_OBJ) $(CPU_OBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lpthread -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lrocprofiler-sdk-roctx -lpthread -Wl,-rpath,$(ROCM)/lib
 
 $(LIBDIR)/libotc_cpu.so: $(CPU_OBJ)
 	@mkdir -p $(LIBDIR)
@@ -103,3 +110,13 @@ bin/otbench: csrc/cli/otbench.cpp $(LIBDIR)/libotc.so
 
 clean:
 	rm -rf build $(LIBDIR)/*.so $(BINS) bin/test_cpu bin/aes_test_cpu
+
+# Host sanitizers over the threaded CPU paths (also tests/test_sanitizers_cpu.py)
+SAN_SRC := csrc/cpu/aes.c csrc/cpu/arc4.c csrc/cli/san_driver.c
+san-check:
+	@mkdir -p build/san
+	$(CC) -O1 -g -std=gnu99 -Icsrc/include -fsanitize=thread $(SAN_SRC) -o build/san/tsan -lpthread
+	$(CC) -O1 -g -std=gnu99 -Icsrc/include -fsanitize=address,undefined -fno-sanitize-recover=undefined $(SAN_SRC) -o build/san/asan -lpthread
+	TSAN_OPTIONS=halt_on_error=1 ./build/san/tsan
+	./build/san/asan
+.PHONY: san-check

@@ -30,7 +30,7 @@ static uint32_t g_td0[256];
 static uint32_t g_rcon[10];
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 
-static inline uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+static inline uint32_t rotl32(uint32_t x, int n) { return (x << (n & 31)) | (x >> ((32 - n) & 31)); }
 static inline uint8_t xt(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0x00)); }
 
 static uint8_t gf_mul(uint8_t a, uint8_t b)

@@ -16,6 +16,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <atomic>
@@ -126,6 +127,16 @@ int check_key(const otc_aes_key *k, int dir)
     return OTC_OK;
 }
 
+/* roctx range for rocprofv3 --marker-trace (a no-op unless a tool is attached):
+ * every public entry point is one named range, so traces show the API call
+ * around its kernels and copies. */
+struct Range {
+    explicit Range(const char *name) { roctxRangePushA(name); }
+    ~Range() { roctxRangePop(); }
+    Range(const Range &) = delete;
+    Range &operator=(const Range &) = delete;
+};
+
 /* Device buffers of the cipher ops: non-null, 16-byte aligned (every kernel
  * moves 16 B per lane with global_load/store_dwordx4), and either the same
  * buffer (in place, where the mode allows it) or disjoint -- a partial overlap
@@ -170,6 +181,7 @@ extern "C" int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, in
 extern "C" int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_aes_key *k, int impl,
                            void *stream)
 {
+    Range rg("otc_aes_ecb");
     if (nbytes % 16) return set_err(OTC_ERR_ARG, "ECB length must be a multiple of 16");
     if (!k) return set_err(OTC_ERR_ARG, "null key");
     if (int r = check_bufs(in, out, nbytes, true, "aes_ecb")) return r;
@@ -263,6 +275,7 @@ static int ctr_common(const void *in, void *out, size_t nbytes, const otc_aes_ke
 extern "C" int otc_aes_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key *k, const uint8_t ctr0[16],
                            uint64_t block_offset, int impl, void *stream)
 {
+    Range rg("otc_aes_ctr");
     if (!ctr0) return set_err(OTC_ERR_ARG, "null counter");
     return ctr_common(in, out, nbytes, k, ctr_add(ctr_from_bytes(ctr0), block_offset, false), false, impl, stream);
 }
@@ -271,6 +284,7 @@ extern "C" int otc_aes_ctr_rfc3686(const void *in, void *out, size_t nbytes, con
                                    const uint8_t nonce[4], const uint8_t ivec[8], uint64_t block_offset, int impl,
                                    void *stream)
 {
+    Range rg("otc_aes_ctr_rfc3686");
     if (!nonce || !ivec) return set_err(OTC_ERR_ARG, "null nonce/ivec");
     uint8_t cb[16];
     memcpy(cb, nonce, 4);
@@ -282,6 +296,7 @@ extern "C" int otc_aes_ctr_rfc3686(const void *in, void *out, size_t nbytes, con
 extern "C" int otc_aes_cbc_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
                                    const uint8_t iv[16], void *stream)
 {
+    Range rg("otc_aes_cbc_decrypt");
     int r = check_key(k, OTC_DIR_DECRYPT);
     if (r) return r;
     if (nbytes % 16) return set_err(OTC_ERR_ARG, "CBC length must be a multiple of 16");
@@ -296,6 +311,7 @@ extern "C" int otc_aes_cbc_decrypt(const void *in, void *out, size_t nbytes, con
 extern "C" int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                             const otc_aes_key *k, const uint8_t iv0[16], void *stream)
 {
+    Range rg("otc_aes_cbc_encrypt_segments");
     int r = check_key(k, OTC_DIR_ENCRYPT);
     if (r) return r;
     if (seg_bytes % 16) return set_err(OTC_ERR_ARG, "segment length must be a multiple of 16");
@@ -312,6 +328,7 @@ extern "C" int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t se
 extern "C" int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                             const otc_aes_key *k, const uint8_t iv0[16], void *stream)
 {
+    Range rg("otc_aes_cbc_decrypt_segments");
     int r = check_key(k, OTC_DIR_DECRYPT);
     if (r) return r;
     if (seg_bytes % 16) return set_err(OTC_ERR_ARG, "segment length must be a multiple of 16");
@@ -329,6 +346,7 @@ extern "C" int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t se
 extern "C" int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
                                       const uint8_t iv[16], void *stream)
 {
+    Range rg("otc_aes_cfb128_decrypt");
     int r = check_key(k, OTC_DIR_ENCRYPT);
     if (r) return r;
     if (nbytes % 16) return set_err(OTC_ERR_ARG, "CFB128 device path needs a multiple of 16 bytes");
@@ -344,6 +362,7 @@ extern "C" int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, 
 
 extern "C" int otc_xor(const void *a, const void *b, void *out, size_t nbytes, void *stream)
 {
+    Range rg("otc_xor");
     if (int r = check_bufs(a, out, nbytes, true, "xor")) return r;
     if (int r = check_bufs(b, out, nbytes, true, "xor")) return r;
     if (nbytes == 0) return OTC_OK;
@@ -355,6 +374,7 @@ extern "C" int otc_xor(const void *a, const void *b, void *out, size_t nbytes, v
 extern "C" int otc_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t len, size_t drop,
                              const void *in, void *out, void *stream)
 {
+    Range rg("otc_rc4_multi");
     if (keylen < 1 || keylen > 256) return set_err(OTC_ERR_ARG, "RC4 key length must be 1..256");
     if (nstreams == 0 || len == 0) return OTC_OK;
     if (!keys || !out) return set_err(OTC_ERR_ARG, "rc4_multi: null buffer");
@@ -370,6 +390,7 @@ extern "C" int otc_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, s
 
 extern "C" int otc_fill_random(void *p, size_t nbytes, uint64_t seed, void *stream)
 {
+    Range rg("otc_fill_random");
     if (nbytes == 0) return OTC_OK;
     if (int r = check_bufs(p, p, nbytes, true, "fill_random")) return r;
     hipError_t e = otc_impl::k_fill_random(p, nbytes, seed, (hipStream_t)stream);
@@ -379,6 +400,7 @@ extern "C" int otc_fill_random(void *p, size_t nbytes, uint64_t seed, void *stre
 
 extern "C" int otc_checksum(const void *p, size_t nbytes, uint64_t *out_dev, void *stream)
 {
+    Range rg("otc_checksum");
     if (nbytes % 8) return set_err(OTC_ERR_ARG, "checksum length must be a multiple of 8");
     if (!out_dev || (nbytes && !p)) return set_err(OTC_ERR_ARG, "checksum: null buffer");
     if (((uintptr_t)p | (uintptr_t)out_dev) & 7u) return set_err(OTC_ERR_ARG, "checksum: buffers must be 8-byte aligned");
@@ -610,6 +632,7 @@ extern "C" int otc_engine_run(otc_engine *e, int mode, const void *host_in, void
                               const otc_aes_key *k, const uint8_t ivc[16], uint64_t block_offset, int impl,
                               otc_stream_stats *stats)
 {
+    Range rg("otc_engine_run");
     if (!e) return set_err(OTC_ERR_ARG, "null engine");
     if (int r = check_stream_args(mode, host_in, host_out, nbytes, k, ivc)) return r;
     if (mode == OTC_MODE_CBC_DEC && block_offset) return set_err(OTC_ERR_ARG, "CBC: pass the halo as iv instead");
@@ -692,6 +715,7 @@ extern "C" int otc_multi_run(int ngpus, int strategy, int mode, const void *host
                              const otc_aes_key *k, const uint8_t ivc[16], int impl, size_t chunk_bytes,
                              otc_multi_stats *stats)
 {
+    Range rg("otc_multi_run");
     if (int r = check_stream_args(mode, host_in, host_out, nbytes, k, ivc)) return r;
     int ndev = otc_device_count();
     if (ngpus < 1 || ngpus > ndev) return set_err(OTC_ERR_ARG, "ngpus out of range");
@@ -814,6 +838,7 @@ extern "C" int otc_multi_run(int ngpus, int strategy, int mode, const void *host
 extern "C" int otc_multi_ctr_resident(int ngpus, void *const *dev_bufs, size_t shard_bytes, const otc_aes_key *k,
                                       const uint8_t ctr0[16], int impl, double *elapsed_ms)
 {
+    Range rg("otc_multi_ctr_resident");
     if (ngpus < 1 || ngpus > otc_device_count()) return set_err(OTC_ERR_ARG, "ngpus out of range");
     if (shard_bytes % 16) return set_err(OTC_ERR_ARG, "shard must be a multiple of 16");
     std::vector<hipStream_t> st(ngpus);
