@@ -711,6 +711,178 @@ extern "C" int otc_engine_run(otc_engine *e, int mode, const void *host_in, void
 }
 
 /* ---- L4 multi-GPU (single process) -------------------------------------- */
+/* ---- RCCL root scatter / gather (otc_multi_run strategy 1) -----------------
+ * Root GPU 0 ingests the host stream, ncclScatter deals equal S-byte pieces to
+ * every GPU over xGMI, each GPU runs the cipher, ncclGather collects the
+ * results at the root, which drains them to the host.  Two root buffer sets
+ * are used in ping-pong: H2D of round r+1 (copy stream) and D2H of round r-1
+ * (copy stream) overlap the scatter/compute/gather of round r, ordered by
+ * events.  ncclScatter needs equal counts, so the last round is zero padded.
+ *
+ * Failure detection: waits poll hipStreamQuery and ncclCommGetAsyncError with a
+ * watchdog (OTC_RCCL_TIMEOUT_S, default 600 s); on an async error or timeout
+ * every communicator is aborted (ncclCommAbort) instead of destroyed, so a
+ * hung peer cannot hang the caller.  All resources are owned by RcclJob and
+ * released on every exit path. */
+struct RcclJob {
+    int n = 0;
+    std::vector<ncclComm_t> comms;
+    std::vector<hipStream_t> st;          /* per GPU: scatter, cipher, gather */
+    std::vector<void *> dsh, dsh_out;     /* per GPU S-byte piece (in / out) */
+    hipStream_t h2d = nullptr, d2h = nullptr;  /* root copy streams */
+    void *root_in[2] = {nullptr, nullptr}, *root_out[2] = {nullptr, nullptr};
+    hipEvent_t ev_in[2] = {}, ev_scattered[2] = {}, ev_gathered[2] = {}, ev_drained[2] = {};
+    bool failed = false;
+
+    ~RcclJob()
+    {
+        for (int g = 0; g < n; ++g) {
+            (void)hipSetDevice(g);
+            if (!failed && st[g]) (void)hipStreamSynchronize(st[g]);
+        }
+        (void)hipSetDevice(0);
+        if (!failed) {
+            if (h2d) (void)hipStreamSynchronize(h2d);
+            if (d2h) (void)hipStreamSynchronize(d2h);
+        }
+        for (int g = 0; g < n; ++g) {
+            if (comms[g]) {
+                if (failed) ncclCommAbort(comms[g]);
+                else ncclCommDestroy(comms[g]);
+            }
+        }
+        for (int g = 0; g < n; ++g) {
+            (void)hipSetDevice(g);
+            if (dsh[g]) (void)hipFree(dsh[g]);
+            if (dsh_out[g]) (void)hipFree(dsh_out[g]);
+            if (st[g]) (void)hipStreamDestroy(st[g]);
+        }
+        (void)hipSetDevice(0);
+        for (int i = 0; i < 2; ++i) {
+            if (root_in[i]) (void)hipFree(root_in[i]);
+            if (root_out[i]) (void)hipFree(root_out[i]);
+            for (hipEvent_t ev : {ev_in[i], ev_scattered[i], ev_gathered[i], ev_drained[i]})
+                if (ev) (void)hipEventDestroy(ev);
+        }
+        if (h2d) (void)hipStreamDestroy(h2d);
+        if (d2h) (void)hipStreamDestroy(d2h);
+    }
+
+    /* wait for `s` while watching every communicator */
+    int wait(hipStream_t s, double timeout_s)
+    {
+        auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess) return OTC_OK;
+            if (q != hipErrorNotReady) {
+                failed = true;
+                return hip_fail(q, "hipStreamQuery (RCCL job)");
+            }
+            for (int g = 0; g < n; ++g) {
+                ncclResult_t ae = ncclSuccess;
+                if (ncclCommGetAsyncError(comms[g], &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+                    failed = true;
+                    return set_err(OTC_ERR_RCCL, std::string("RCCL async error on GPU ") + std::to_string(g) + ": " +
+                                                     ncclGetErrorString(ae));
+                }
+            }
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+                failed = true;
+                return set_err(OTC_ERR_RCCL, "RCCL collective timed out (OTC_RCCL_TIMEOUT_S)");
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+};
+
+static int rccl_scatter_gather(int ngpus, int mode, const uint8_t *hin, uint8_t *hout, size_t nbytes,
+                               const otc_aes_key *k, const uint8_t ivc[16], int impl, size_t chunk_bytes)
+{
+    const char *to = getenv("OTC_RCCL_TIMEOUT_S");
+    const double timeout_s = to ? atof(to) : 600.0;
+    RcclJob J;
+    J.n = ngpus;
+    J.comms.assign(ngpus, nullptr);
+    J.st.assign(ngpus, nullptr);
+    J.dsh.assign(ngpus, nullptr);
+    J.dsh_out.assign(ngpus, nullptr);
+    std::vector<int> devs(ngpus);
+    for (int g = 0; g < ngpus; ++g) devs[g] = g;
+    RCCLCHK(ncclCommInitAll(J.comms.data(), ngpus, devs.data()));
+    size_t S = chunk_bytes ? chunk_bytes : (size_t)64 << 20; /* per-GPU bytes per round */
+    S = (S + 15) & ~(size_t)15;
+    const size_t round = S * (size_t)ngpus;
+    for (int g = 0; g < ngpus; ++g) {
+        HIPCHK(hipSetDevice(g));
+        HIPCHK(hipStreamCreateWithFlags(&J.st[g], hipStreamNonBlocking));
+        HIPCHK(hipMalloc(&J.dsh[g], S));
+        HIPCHK(hipMalloc(&J.dsh_out[g], S));
+    }
+    HIPCHK(hipSetDevice(0));
+    HIPCHK(hipStreamCreateWithFlags(&J.h2d, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&J.d2h, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+        HIPCHK(hipMalloc(&J.root_in[i], round));
+        HIPCHK(hipMalloc(&J.root_out[i], round));
+        for (hipEvent_t *ev : {&J.ev_in[i], &J.ev_scattered[i], &J.ev_gathered[i], &J.ev_drained[i]})
+            HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    }
+    const size_t nrounds = (nbytes + round - 1) / round;
+    for (size_t r = 0; r < nrounds; ++r) {
+        const int b = (int)(r & 1);
+        const size_t off = r * round, n = std::min(round, nbytes - off);
+        HIPCHK(hipSetDevice(0));
+        /* root_in[b] is free once round r-2's scatter has read it */
+        if (r >= 2) HIPCHK(hipStreamWaitEvent(J.h2d, J.ev_scattered[b], 0));
+        if (n < round) HIPCHK(hipMemsetAsync(J.root_in[b], 0, round, J.h2d));
+        HIPCHK(hipMemcpyAsync(J.root_in[b], hin + off, n, hipMemcpyHostToDevice, J.h2d));
+        HIPCHK(hipEventRecord(J.ev_in[b], J.h2d));
+        HIPCHK(hipStreamWaitEvent(J.st[0], J.ev_in[b], 0));
+        RCCLCHK(ncclGroupStart());
+        for (int g = 0; g < ngpus; ++g)
+            RCCLCHK(ncclScatter(J.root_in[b], J.dsh[g], S, ncclUint8, 0, J.comms[g], J.st[g]));
+        RCCLCHK(ncclGroupEnd());
+        HIPCHK(hipSetDevice(0));
+        HIPCHK(hipEventRecord(J.ev_scattered[b], J.st[0]));
+        for (int g = 0; g < ngpus; ++g) {
+            const size_t goff = off + (size_t)g * S;
+            if (goff >= nbytes) continue;
+            HIPCHK(hipSetDevice(g));
+            const size_t gn = std::min(S, nbytes - goff);
+            uint8_t halo[16];
+            const uint8_t *hp = nullptr;
+            if (mode == OTC_MODE_CBC_DEC && goff > 0) {
+                memcpy(halo, hin + goff - 16, 16);
+                hp = halo;
+            }
+            if (int rr = run_chunk(mode, J.dsh[g], J.dsh_out[g], gn, k, ivc, goff / 16, hp, impl, J.st[g])) {
+                J.failed = true;
+                return rr;
+            }
+        }
+        /* root_out[b] is free once round r-2's D2H has drained it */
+        HIPCHK(hipSetDevice(0));
+        if (r >= 2) HIPCHK(hipStreamWaitEvent(J.st[0], J.ev_drained[b], 0));
+        RCCLCHK(ncclGroupStart());
+        for (int g = 0; g < ngpus; ++g)
+            RCCLCHK(ncclGather(J.dsh_out[g], J.root_out[b], S, ncclUint8, 0, J.comms[g], J.st[g]));
+        RCCLCHK(ncclGroupEnd());
+        HIPCHK(hipSetDevice(0));
+        HIPCHK(hipEventRecord(J.ev_gathered[b], J.st[0]));
+        HIPCHK(hipStreamWaitEvent(J.d2h, J.ev_gathered[b], 0));
+        HIPCHK(hipMemcpyAsync(hout + off, J.root_out[b], n, hipMemcpyDeviceToHost, J.d2h));
+        HIPCHK(hipEventRecord(J.ev_drained[b], J.d2h));
+        /* every buffer reuse is ordered by the events above, so the host only
+         * enqueues; it blocks in the copies when the host buffers are pageable
+         * (pin them -- otc_host_register -- for H2D/D2H overlap) */
+    }
+    HIPCHK(hipSetDevice(0));
+    if (int w = J.wait(J.st[0], timeout_s)) return w;
+    if (int w = J.wait(J.d2h, timeout_s)) return w;
+    return OTC_OK;
+}
+
 extern "C" int otc_multi_run(int ngpus, int strategy, int mode, const void *host_in, void *host_out, size_t nbytes,
                              const otc_aes_key *k, const uint8_t ivc[16], int impl, size_t chunk_bytes,
                              otc_multi_stats *stats)
@@ -753,77 +925,8 @@ extern "C" int otc_multi_run(int ngpus, int strategy, int mode, const void *host
         for (int g = 0; g < ngpus; ++g)
             if (res[g]) rc = res[g];
     } else {
-        /* RCCL root scatter/gather, chunked so the root never holds more than
-         * 2 x ngpus x per-GPU chunk.  ncclScatter needs equal counts: the
-         * stream is processed in rounds of ngpus*S bytes; the final partial
-         * round is padded. */
-        if (mode == OTC_MODE_CBC_DEC) {
-            /* halo handling needs the previous block per shard; done host side */
-        }
-        std::vector<ncclComm_t> comms(ngpus);
-        std::vector<int> devs(ngpus);
-        for (int g = 0; g < ngpus; ++g) devs[g] = g;
-        RCCLCHK(ncclCommInitAll(comms.data(), ngpus, devs.data()));
-        size_t S = chunk_bytes ? chunk_bytes : (size_t)64 << 20; /* per-GPU bytes per round */
-        S = (S + 15) & ~(size_t)15;
-        const size_t round = S * (size_t)ngpus;
-        std::vector<hipStream_t> st(ngpus);
-        std::vector<void *> dsh(ngpus), dsh_out(ngpus);
-        void *root_in = nullptr, *root_out = nullptr;
-        for (int g = 0; g < ngpus; ++g) {
-            HIPCHK(hipSetDevice(g));
-            HIPCHK(hipStreamCreateWithFlags(&st[g], hipStreamNonBlocking));
-            HIPCHK(hipMalloc(&dsh[g], S));
-            HIPCHK(hipMalloc(&dsh_out[g], S));
-            if (g == 0) {
-                HIPCHK(hipMalloc(&root_in, round));
-                HIPCHK(hipMalloc(&root_out, round));
-            }
-        }
-        const uint8_t *hin = (const uint8_t *)host_in;
-        uint8_t *hout = (uint8_t *)host_out;
-        for (size_t off = 0; off < nbytes && rc == OTC_OK; off += round) {
-            const size_t n = std::min(round, nbytes - off);
-            HIPCHK(hipSetDevice(0));
-            if (n < round) HIPCHK(hipMemsetAsync(root_in, 0, round, st[0]));
-            HIPCHK(hipMemcpyAsync(root_in, hin + off, n, hipMemcpyHostToDevice, st[0]));
-            RCCLCHK(ncclGroupStart());
-            for (int g = 0; g < ngpus; ++g)
-                RCCLCHK(ncclScatter(root_in, dsh[g], S, ncclUint8, 0, comms[g], st[g]));
-            RCCLCHK(ncclGroupEnd());
-            for (int g = 0; g < ngpus; ++g) {
-                HIPCHK(hipSetDevice(g));
-                const size_t goff = off + (size_t)g * S;
-                if (goff >= nbytes) continue;
-                const size_t gn = std::min(S, nbytes - goff);
-                uint8_t halo[16];
-                const uint8_t *hp = nullptr;
-                if (mode == OTC_MODE_CBC_DEC && goff > 0) {
-                    memcpy(halo, hin + goff - 16, 16);
-                    hp = halo;
-                }
-                int r = run_chunk(mode, dsh[g], dsh_out[g], gn, k, ivc, goff / 16, hp, impl, st[g]);
-                if (r) { rc = r; break; }
-            }
-            RCCLCHK(ncclGroupStart());
-            for (int g = 0; g < ngpus; ++g)
-                RCCLCHK(ncclGather(dsh_out[g], root_out, S, ncclUint8, 0, comms[g], st[g]));
-            RCCLCHK(ncclGroupEnd());
-            HIPCHK(hipSetDevice(0));
-            HIPCHK(hipMemcpyAsync(hout + off, root_out, n, hipMemcpyDeviceToHost, st[0]));
-            HIPCHK(hipStreamSynchronize(st[0]));
-        }
-        for (int g = 0; g < ngpus; ++g) {
-            (void)hipSetDevice(g);
-            (void)hipStreamSynchronize(st[g]);
-            (void)hipFree(dsh[g]);
-            (void)hipFree(dsh_out[g]);
-            (void)hipStreamDestroy(st[g]);
-            ncclCommDestroy(comms[g]);
-        }
-        (void)hipSetDevice(0);
-        (void)hipFree(root_in);
-        (void)hipFree(root_out);
+        rc = rccl_scatter_gather(ngpus, mode, (const uint8_t *)host_in, (uint8_t *)host_out, nbytes, k, ivc, impl,
+                                 chunk_bytes);
     }
     auto t1 = std::chrono::steady_clock::now();
     if (stats) {

@@ -83,3 +83,26 @@ def test_models_api_on_gpu(gpu):
     m = RC4MultiStream(keys)
     z = torch.randint(0, 256, (128, 100), dtype=torch.uint8, device=gpu)
     assert torch.equal(m.crypt(m.crypt(z)), z)
+
+
+@pytest.mark.parametrize("mode", ["ctr", "cbc-dec"])
+def test_resumable_file_job_on_gpu(gpu, tmp_path, mode):
+    """Interrupted + resumed file job through the pinned GPU pipeline equals
+    the oracle (our_tree_amd/parallel/filejob.py)."""
+    from our_tree_amd.parallel import filejob
+
+    n = (3 << 20) + (16 if mode == "cbc-dec" else 5)
+    data = os.urandom(n)
+    src, dst = tmp_path / "in", tmp_path / "out"
+    src.write_bytes(data)
+    key, iv = os.urandom(16), os.urandom(16)
+    be = filejob.gpu_backend(chunk_bytes=1 << 20)
+    try:
+        r = filejob.crypt_file(str(src), str(dst), key, iv, mode=mode, chunk_bytes=1 << 20, backend=be, max_chunks=1)
+        assert not r["done"]
+        r = filejob.crypt_file(str(src), str(dst), key, iv, mode=mode, chunk_bytes=1 << 20, backend=be)
+        assert r["done"] and r["resumed_from"] == 1
+    finally:
+        be.close()
+    ref = cpu_ref.ctr(key, iv, data) if mode == "ctr" else cpu_ref.cbc(key, iv, data, decrypt=True)
+    assert dst.read_bytes() == ref
