@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--impl", default=os.environ.get("OTC_BENCH_IMPL", "auto"))
     ap.add_argument("--no-aes256", action="store_true")
     ap.add_argument("--no-bitslice", action="store_true")
+    ap.add_argument("--no-clock", action="store_true")
     args = ap.parse_args()
 
     from our_tree_amd import ops
@@ -108,6 +109,20 @@ def main():
     info = dinfo.info(local)
     cpb = (ms_per_step * 1e-3) * info["clock_hz"] * info["cus"] / nbytes
 
+    # Clock the chip holds under this load (untimed extra steps with the
+    # one-wave probe beside them): cycles/byte/CU at the nominal clock
+    # overstates the cycle count when the chip lowers its clock.
+    clk_ghz = None
+    if not args.no_clock:
+        n_clk = max(3, int(0.3 / max(ms_per_step * 1e-3, 1e-6)) + 1)
+        window = 0.6 * n_clk * ms_per_step * 1e-3
+        probe = ops.clock_probe(0.2 * n_clk * ms_per_step * 1e-3, window, device=dev)
+        for _ in range(n_clk):
+            step()
+        torch.cuda.synchronize()
+        clk_ghz = ops.clock_ghz(probe)
+    cpb_eff = (ms_per_step * 1e-3) * clk_ghz * 1e9 * info["cus"] / nbytes if clk_ghz else None
+
     extra = {}
     if not args.no_bitslice and args.impl != "bitslice":
         # BASELINE config 3 names the wave-bitsliced VALU kernel for this
@@ -145,6 +160,8 @@ def main():
                 "impl": args.impl,
             },
             "cycles_per_byte_per_cu": round(cpb, 4),
+            "cycles_per_byte_per_cu_at_held_clock": round(cpb_eff, 4) if cpb_eff else None,
+            "held_clock_ghz": round(clk_ghz, 3) if clk_ghz else None,
             "per_gpu_gbps": round(value / world, 3),
             "baseline": {"value_gbps": BASELINE_GBPS, "what": "AES-NI CTR-256 1000MiB 8thr (BASELINE.md)",
                          "gpu_headline_gbps": BASELINE_GPU_GBPS},

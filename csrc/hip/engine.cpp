@@ -50,6 +50,7 @@ void tt_set_wg_per_cu(int);
 hipError_t k_xor(const void *, const void *, void *, size_t, hipStream_t);
 hipError_t k_fill_random(void *, size_t, uint64_t, hipStream_t);
 hipError_t k_checksum(const void *, size_t, uint64_t *, hipStream_t);
+hipError_t k_clock(uint64_t *, uint64_t, uint64_t, hipStream_t);
 hipError_t k_rc4_multi(const uint8_t *, int, size_t, size_t, size_t, const void *, void *, hipStream_t);
 } // namespace otc_impl
 
@@ -406,6 +407,18 @@ extern "C" int otc_checksum(const void *p, size_t nbytes, uint64_t *out_dev, voi
     if (((uintptr_t)p | (uintptr_t)out_dev) & 7u) return set_err(OTC_ERR_ARG, "checksum: buffers must be 8-byte aligned");
     hipError_t e = otc_impl::k_checksum(p, nbytes, out_dev, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "checksum launch");
+    return OTC_OK;
+}
+
+extern "C" int otc_clock_probe(uint64_t *out_dev, double delay_s, double window_s, void *stream)
+{
+    if (!out_dev || ((uintptr_t)out_dev & 7u)) return set_err(OTC_ERR_ARG, "clock_probe: bad output buffer");
+    if (!(delay_s >= 0.0) || !(window_s > 0.0) || delay_s + window_s > 60.0)
+        return set_err(OTC_ERR_ARG, "clock_probe: delay/window out of range (total <= 60 s)");
+    const uint64_t hz = 100000000ull; /* s_memrealtime */
+    hipError_t e = otc_impl::k_clock(out_dev, (uint64_t)(delay_s * hz), (uint64_t)(window_s * hz) + 1,
+                                     (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "clock_probe launch");
     return OTC_OK;
 }
 

@@ -185,9 +185,44 @@ int grid_stream(uint64_t items, int per_cu)
     return (int)(need < cap ? need : cap);
 }
 
+/* Clock probe: one wave stamps s_memtime (shader clock) and s_memrealtime
+ * (constant 100 MHz) around a window of `ticks` real-time ticks that starts
+ * `delay` ticks after launch, sleeping in between so it takes no issue slots
+ * from co-resident waves.  Launched on a side stream beside a workload, it
+ * reads the clock the chip holds under that load (MI355X_MICROARCH: the chip
+ * lowers its clock under load; cycles/byte at the nominal 2.4 GHz overstate
+ * the cycle count).  out[0] = shader cycles, out[1] = real-time ticks. */
+__global__ __launch_bounds__(64) void k_clock_probe(unsigned long long *out, uint64_t delay, uint64_t ticks)
+{
+    uint64_t r = __builtin_amdgcn_s_memrealtime();
+    const uint64_t start = r + delay;
+    while (r < start) {
+        __builtin_amdgcn_s_sleep(32);
+        r = __builtin_amdgcn_s_memrealtime();
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+    do {
+        __builtin_amdgcn_s_sleep(32);
+        r = __builtin_amdgcn_s_memrealtime();
+    } while (r - r0 < ticks);
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        out[0] = t1 - t0;
+        out[1] = r1 - r0;
+    }
+}
+
 } // namespace
 
 namespace otc_impl {
+
+hipError_t k_clock(uint64_t *out, uint64_t delay_ticks, uint64_t ticks, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_clock_probe, dim3(1), dim3(64), 0, st, (unsigned long long *)out, delay_ticks, ticks);
+    return hipGetLastError();
+}
 
 hipError_t k_xor(const void *a, const void *b, void *out, size_t n, hipStream_t st)
 {

@@ -122,6 +122,12 @@ int otc_fill_random(void *p, size_t nbytes, uint64_t seed, void *stream);
  * *out_dev (device pointer to one uint64). */
 int otc_checksum(const void *p, size_t nbytes, uint64_t *out_dev, void *stream);
 
+/* Clock probe: a one-wave kernel on `stream` that sleeps `delay_s`, then
+ * measures the shader clock over `window_s` seconds of real time; run it on a
+ * side stream beside a workload.  out_dev[0] = shader cycles, out_dev[1] =
+ * 100 MHz ticks, so GHz = 0.1 * out[0] / out[1]. */
+int otc_clock_probe(uint64_t *out_dev, double delay_s, double window_s, void *stream);
+
 /* ---- device memory / sync helpers (so C harnesses need no HIP headers) --- */
 void *otc_dev_malloc(size_t nbytes);
 void otc_dev_free(void *p);

@@ -145,6 +145,7 @@ def _declare_gpu(lib):
         "otc_rc4_multi": (c_int, [c_vp, c_int, c_sz, c_sz, c_sz, c_vp, c_vp, c_vp]),
         "otc_fill_random": (c_int, [c_vp, c_sz, c_u64, c_vp]),
         "otc_checksum": (c_int, [c_vp, c_sz, c_vp, c_vp]),
+        "otc_clock_probe": (c_int, [c_vp, ctypes.c_double, ctypes.c_double, c_vp]),
         "otc_device_count": (c_int, []),
         "otc_device_cus": (c_int, [c_int]),
         "otc_device_clock_khz": (c_int, [c_int]),

@@ -2,9 +2,10 @@
 from .aes_ops import (IMPLS, cbc_decrypt, cbc_decrypt_segments, cbc_encrypt_segments, cfb128_decrypt, ctr,
                       ctr_rfc3686, ecb_decrypt, ecb_encrypt)
 from .keys import expand_key
-from .stream_ops import checksum, fill_random_, rc4_multi, xor
+from .stream_ops import checksum, clock_ghz, clock_probe, fill_random_, rc4_multi, xor
 
 __all__ = [
     "IMPLS", "ctr", "ctr_rfc3686", "ecb_encrypt", "ecb_decrypt", "cbc_decrypt", "cbc_encrypt_segments",
     "cbc_decrypt_segments", "cfb128_decrypt", "expand_key", "xor", "rc4_multi", "fill_random_", "checksum",
+    "clock_probe", "clock_ghz",
 ]

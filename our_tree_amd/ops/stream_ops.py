@@ -69,3 +69,23 @@ def checksum(t: torch.Tensor) -> int:
         rc = _native.require_gpu_lib().otc_checksum(t.data_ptr(), _nbytes(t), acc.data_ptr(), _stream(t))
     _native.check(rc, "otc_checksum")
     return int(acc.item()) & (2**64 - 1)
+
+
+def clock_probe(delay_s: float, window_s: float, device=None, stream=None) -> torch.Tensor:
+    """Launch the one-wave clock probe (``otc_clock_probe``) on ``stream``
+    (default: a new side stream) and return its 2-element result tensor; read
+    it with :func:`clock_ghz` after the workload has been synchronized."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    out = torch.zeros(2, dtype=torch.int64, device=dev)
+    s = stream if stream is not None else torch.cuda.Stream(device=dev)
+    with torch.cuda.device(dev):
+        rc = _native.require_gpu_lib().otc_clock_probe(out.data_ptr(), float(delay_s), float(window_s),
+                                                       ctypes.c_void_p(s.cuda_stream))
+    _native.check(rc, "otc_clock_probe")
+    out._probe_stream = s  # keep the side stream alive until the result is read
+    return out
+
+
+def clock_ghz(probe: torch.Tensor) -> float:
+    cyc, ticks = (int(v) for v in probe.cpu().tolist())
+    return 0.1 * cyc / ticks if ticks > 0 else float("nan")

@@ -266,3 +266,17 @@ def test_deterministic_rerun(gpu, impl):
     e2 = ops.ecb_encrypt(x, key, impl=impl)
     assert torch.equal(e1, e2)
     assert torch.equal(ops.ecb_decrypt(e1, key), x)
+
+
+def test_clock_probe_beside_a_workload(gpu):
+    """The one-wave probe co-resides with a full-chip kernel and reads a sane
+    shader clock (gfx950 peak 2.4 GHz)."""
+    x = torch.empty(1 << 30, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(x, 3)
+    probe = ops.clock_probe(0.01, 0.05, device=gpu)
+    key, ctr0 = os.urandom(16), os.urandom(16)
+    for _ in range(120):  # ~1 ms each
+        ops.ctr(x, key, ctr0, out=x)
+    torch.cuda.synchronize()
+    ghz = ops.clock_ghz(probe)
+    assert 0.3 < ghz < 2.6, ghz
