@@ -656,6 +656,103 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg(CbcSegParams P, otc
     }
 }
 
+/* Same job, grouped memory access: each lane loads and stores the next G
+ * blocks of its segment back to back (one burst per cache line) instead of
+ * one block per block-time.  Lanes are a segment apart (4 KiB for disk
+ * sectors), so every wave access touches 64 lines; spread over G block-times,
+ * the ~2048 live segments per CU evict those lines from L2 between uses and
+ * each 16-byte block re-fetches a whole line.  Group g+1 is prefetched while
+ * group g is encrypted; ciphertext overwrites the plaintext registers and is
+ * stored as a burst at the end of the group. */
+template <int NR, int B, int THREADS, int G>
+__global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg_g(CbcSegParams P, otc_aes_key K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
+    fill_tbl4<THREADS>(tbl, g_tab.te0);
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    uint32_t lk[4];
+    tbl4_lane_consts(lane, lk);
+    constexpr uint64_t PER = (uint64_t)THREADS * B;
+    const uint64_t sb = P.seg_blocks;
+    const uint64_t ng = sb / G;
+
+    for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nseg; base += (uint64_t)gridDim.x * PER) {
+        uint64_t first[B]; /* block index of the segment's first block */
+        bool live[B];
+        uint32_t c[B][4];
+        uint4 cur[B][G], nxt[B][G];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const uint64_t seg = base + (uint64_t)wave * 64u * B + 64u * b + lane;
+            live[b] = seg < P.nseg;
+            first[b] = seg * sb;
+            Ctr128 ivv;
+            ivv.lo = P.iv0.lo + seg;
+            ivv.hi = P.iv0.hi + (ivv.lo < P.iv0.lo ? 1 : 0);
+            ctr_words(ivv, 0, false, c[b][0], c[b][1], c[b][2], c[b][3]);
+#pragma unroll
+            for (int t = 0; t < G; ++t)
+                cur[b][t] = (live[b] && ng) ? ld16(P.in, first[b] + t) : make_uint4(0, 0, 0, 0);
+        }
+        for (uint64_t g = 0; g < ng; ++g) {
+            const bool more = g + 1 < ng;
+#pragma unroll
+            for (int b = 0; b < B; ++b)
+#pragma unroll
+                for (int t = 0; t < G; ++t)
+                    nxt[b][t] = (live[b] && more) ? ld16(P.in, first[b] + (g + 1) * G + t) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < G; ++t) {
+                uint32_t s[B][4];
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+                    s[b][0] = cur[b][t].x ^ c[b][0] ^ K.rk[0];
+                    s[b][1] = cur[b][t].y ^ c[b][1] ^ K.rk[1];
+                    s[b][2] = cur[b][t].z ^ c[b][2] ^ K.rk[2];
+                    s[b][3] = cur[b][t].w ^ c[b][3] ^ K.rk[3];
+                }
+                enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) c[b][q] = s[b][q];
+                    cur[b][t] = make_uint4(s[b][0], s[b][1], s[b][2], s[b][3]);
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+#pragma unroll
+                for (int t = 0; t < G; ++t) {
+                    if (live[b]) st16(P.out, first[b] + g * G + t, cur[b][t]);
+                    cur[b][t] = nxt[b][t];
+                }
+            }
+        }
+        /* remaining sb % G blocks, one at a time */
+        for (uint64_t j = ng * G; j < sb; ++j) {
+            uint32_t s[B][4];
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const uint4 p = live[b] ? ld16(P.in, first[b] + j) : make_uint4(0, 0, 0, 0);
+                s[b][0] = p.x ^ c[b][0] ^ K.rk[0];
+                s[b][1] = p.y ^ c[b][1] ^ K.rk[1];
+                s[b][2] = p.z ^ c[b][2] ^ K.rk[2];
+                s[b][3] = p.w ^ c[b][3] ^ K.rk[3];
+            }
+            enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) c[b][q] = s[b][q];
+                if (live[b]) st16(P.out, first[b] + j, make_uint4(s[b][0], s[b][1], s[b][2], s[b][3]));
+            }
+        }
+    }
+}
+
 /* CBC-decrypt over segments of ANY length: the plain CBC kernel XORs every
  * block with its predecessor; this fix-up swaps that predecessor for IV_s at
  * each segment start s >= 1 (touches nseg blocks only). */
@@ -773,7 +870,16 @@ template <int NR>
 hipError_t launch_seg_nr(const CbcSegParams &P, const otc_aes_key &K, hipStream_t st)
 {
     int grid = grid_for(P.nseg, (uint64_t)SEG_THREADS * SEG_B, 1);
-    hipLaunchKernelGGL((k_aes_cbc_enc_seg<NR, SEG_B, SEG_THREADS>), dim3(grid), dim3(SEG_THREADS), 0, st, P, K);
+    /* OTC_CBC_GROUP: blocks per load/store burst (1 = the per-block kernel) */
+    static const int grp = getenv("OTC_CBC_GROUP") ? atoi(getenv("OTC_CBC_GROUP")) : 4;
+    if (grp == 4 && P.seg_blocks >= 4)
+        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, SEG_B, SEG_THREADS, 4>), dim3(grid), dim3(SEG_THREADS), 0, st, P,
+                           K);
+    else if (grp == 8 && P.seg_blocks >= 8) /* B = 1: two 8-block buffers per segment fit without spills */
+        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, 1, SEG_THREADS, 8>),
+                           dim3(grid_for(P.nseg, (uint64_t)SEG_THREADS, 1)), dim3(SEG_THREADS), 0, st, P, K);
+    else
+        hipLaunchKernelGGL((k_aes_cbc_enc_seg<NR, SEG_B, SEG_THREADS>), dim3(grid), dim3(SEG_THREADS), 0, st, P, K);
     return hipGetLastError();
 }
 
