@@ -5,7 +5,7 @@
  *
  *   otbench --mode ctr|ecb|ecb-dec|cbc-dec|cbc-enc-seg|cfb-dec|xor|rc4
  *           [--bits 128] [--bytes 1G] [--iters 20] [--warmup 3]
- *           [--impl auto|ttable|bitslice] [--inplace] [--verify]
+ *           [--impl auto|ttable|bitslice] [--inplace] [--verify] [--clock]
  *           [--e2e --chunk 256M]            host-resident, pinned pipeline
  *           [--gpus N --strategy direct|rccl] single-process multi-GPU (e2e)
  *           [--seg 4096]                    CBC segment size
@@ -48,7 +48,7 @@ struct Cfg {
     size_t bytes = 1ull << 30;
     int iters = 20, warmup = 3;
     int impl = OTC_IMPL_AUTO;
-    bool inplace = false, verify = false, e2e = false;
+    bool inplace = false, verify = false, e2e = false, clock = false;
     size_t chunk = 256ull << 20;
     int gpus = 1, strategy = 0;
     size_t seg = 4096;
@@ -131,6 +131,7 @@ int main(int argc, char **argv)
             c.impl = v == "ttable" ? OTC_IMPL_TTABLE : v == "bitslice" ? OTC_IMPL_BITSLICE : v == "hybrid" ? OTC_IMPL_HYBRID : OTC_IMPL_AUTO;
         } else if (a == "--inplace") c.inplace = true;
         else if (a == "--verify") c.verify = true;
+        else if (a == "--clock") c.clock = true;
         else if (a == "--e2e") c.e2e = true;
         else if (a == "--chunk") c.chunk = parse_size(nx());
         else if (a == "--gpus") c.gpus = atoi(nx());
@@ -234,12 +235,21 @@ int main(int argc, char **argv)
     }
     const double gbps = c.bytes / (ms * 1e6);
     const double cpb = (ms * 1e-3) * clk_hz * cus / (double)c.bytes;
+    double held = 0.0;
+    if (c.clock && otc_measure_clock(run_op, &a, &held)) {
+        fprintf(stderr, "clock: %s\n", otc_last_error());
+        return 1;
+    }
+    char clk[160] = "";
+    if (c.clock)
+        snprintf(clk, sizeof clk, "\"held_clock_ghz\": %.3f, \"cycles_per_byte_per_cu_held\": %.3f, ", held,
+                 (ms * 1e-3) * held * 1e9 * cus / (double)c.bytes);
     printf("{\"mode\": \"%s\", \"bits\": %d, \"bytes\": %zu, \"impl\": \"%s\", \"inplace\": %s, \"iters\": %d, "
-           "\"ms\": %.4f, \"gbps\": %.2f, \"cycles_per_byte_per_cu\": %.3f, \"cus\": %d, \"clock_mhz\": %.0f, "
+           "\"ms\": %.4f, \"gbps\": %.2f, \"cycles_per_byte_per_cu\": %.3f, \"cus\": %d, \"clock_mhz\": %.0f, %s"
            "\"verified\": %s}\n",
            c.mode.c_str(), c.bits, c.bytes,
            c.impl == OTC_IMPL_TTABLE ? "ttable" : c.impl == OTC_IMPL_BITSLICE ? "bitslice" : c.impl == OTC_IMPL_HYBRID ? "hybrid" : "auto",
-           c.inplace ? "true" : "false", c.iters, ms, gbps, cpb, cus, clk_hz / 1e6,
+           c.inplace ? "true" : "false", c.iters, ms, gbps, cpb, cus, clk_hz / 1e6, clk,
            c.verify ? (ok ? "true" : "false") : "null");
     otc_dev_free(a.in);
     if (!c.inplace) otc_dev_free(a.out);

@@ -871,7 +871,7 @@ hipError_t launch_seg_nr(const CbcSegParams &P, const otc_aes_key &K, hipStream_
 {
     int grid = grid_for(P.nseg, (uint64_t)SEG_THREADS * SEG_B, 1);
     /* OTC_CBC_GROUP: blocks per load/store burst (1 = the per-block kernel) */
-    static const int grp = getenv("OTC_CBC_GROUP") ? atoi(getenv("OTC_CBC_GROUP")) : 4;
+    static const int grp = getenv("OTC_CBC_GROUP") ? atoi(getenv("OTC_CBC_GROUP")) : 8;
     if (grp == 4 && P.seg_blocks >= 4)
         hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, SEG_B, SEG_THREADS, 4>), dim3(grid), dim3(SEG_THREADS), 0, st, P,
                            K);

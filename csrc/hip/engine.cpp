@@ -479,24 +479,62 @@ extern "C" int otc_memset(void *p, int v, size_t nbytes)
     HIPCHK(hipMemset(p, v, nbytes));
     return OTC_OK;
 }
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    ~EventPair()
+    {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+    }
+};
+
 extern "C" int otc_time_op(otc_op_fn op, void *arg, int iters, double *ms_per_iter)
 {
-    hipEvent_t a, b;
-    HIPCHK(hipEventCreate(&a));
-    HIPCHK(hipEventCreate(&b));
+    if (!op) return set_err(OTC_ERR_ARG, "null op");
+    EventPair ev;
+    HIPCHK(hipEventCreate(&ev.a));
+    HIPCHK(hipEventCreate(&ev.b));
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipEventRecord(a, nullptr));
+    HIPCHK(hipEventRecord(ev.a, nullptr));
     for (int i = 0; i < iters; ++i) {
         int r = op(arg);
         if (r) return r;
     }
-    HIPCHK(hipEventRecord(b, nullptr));
-    HIPCHK(hipEventSynchronize(b));
+    HIPCHK(hipEventRecord(ev.b, nullptr));
+    HIPCHK(hipEventSynchronize(ev.b));
     float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, a, b));
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
+    HIPCHK(hipEventElapsedTime(&ms, ev.a, ev.b));
     if (ms_per_iter) *ms_per_iter = iters > 0 ? ms / iters : 0.0;
+    return OTC_OK;
+}
+
+/* Held clock under `op`: the clock probe on its own non-blocking stream,
+ * beside >= 0.3 s of back-to-back ops on the default stream. */
+extern "C" int otc_measure_clock(otc_op_fn op, void *arg, double *ghz)
+{
+    if (!op || !ghz) return set_err(OTC_ERR_ARG, "null argument");
+    double ms = 0.0;
+    if (int r = otc_time_op(op, arg, 1, &ms)) return r;
+    const int n = std::max(3, (int)(300.0 / std::max(ms, 1e-3)) + 1);
+    struct Res {
+        hipStream_t s = nullptr;
+        uint64_t *d = nullptr;
+        ~Res()
+        {
+            if (d) (void)hipFree(d);
+            if (s) (void)hipStreamDestroy(s);
+        }
+    } R;
+    HIPCHK(hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&R.d, 2 * sizeof(uint64_t)));
+    HIPCHK(hipMemset(R.d, 0, 2 * sizeof(uint64_t)));
+    if (int r = otc_clock_probe(R.d, 0.2 * n * ms * 1e-3, 0.6 * n * ms * 1e-3, R.s)) return r;
+    for (int i = 0; i < n; ++i)
+        if (int r = op(arg)) return r;
+    HIPCHK(hipDeviceSynchronize());
+    uint64_t h[2] = {0, 0};
+    HIPCHK(hipMemcpy(h, R.d, sizeof h, hipMemcpyDeviceToHost));
+    *ghz = h[1] ? 0.1 * (double)h[0] / (double)h[1] : 0.0;
     return OTC_OK;
 }
 

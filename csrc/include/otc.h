@@ -140,6 +140,8 @@ int otc_memset(void *p, int v, size_t nbytes);
  * bracketed by hipEvents (kernel-only timing). */
 typedef int (*otc_op_fn)(void *arg);
 int otc_time_op(otc_op_fn op, void *arg, int iters, double *ms_per_iter);
+/* Clock (GHz) the chip holds while running `op` back to back (>= 0.3 s). */
+int otc_measure_clock(otc_op_fn op, void *arg, double *ghz);
 
 /* ---- device info ------------------------------------------------------- */
 int otc_device_count(void);
