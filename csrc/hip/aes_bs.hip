@@ -52,9 +52,15 @@ enum : int { BS_CTR = 0, BS_ECB = 1 };
 
 __device__ __forceinline__ W lane_mask(uint32_t lane, int n) { return (W)(0u - ((lane >> n) & 1u)); }
 
-template <int NR, int MODE, bool CACHE, int PF>
+template <int NR, int MODE, bool CACHE, int PF, int LS>
 __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
 {
+    /* CTR: the plaintext of slots 0..LS-1 is copied into LDS by the DMA path
+     * (global_load_lds_dwordx4, no VGPRs) when the task starts and lands
+     * while the ~60 us of rounds run; layout [wave][slot][lane] x 16 B is
+     * exactly the lane-linear image glds writes, and each lane reads its own
+     * 16 B back with a conflict-free ds_read_b128. */
+    __shared__ uint4 stage[LS > 0 ? 4 * LS * 64 : 1];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * 4u + wave;
@@ -74,6 +80,18 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
         const bool full = vbase >= shift && vbase + 2048u - shift <= P.nblocks; /* uniform */
         W s[128];
 
+        if (MODE == BS_CTR && LS > 0) {
+            const int64_t t0 = (int64_t)vbase - (int64_t)shift;
+            const uint8_t *ib0 = P.in + t0 * 16 + lane * 16u;
+#pragma unroll
+            for (int k = 0; k < LS; ++k) {
+                const int64_t si = t0 + (int64_t)lane + 64 * k;
+                if (full || (si >= 0 && (uint64_t)si < P.nblocks))
+                    __builtin_amdgcn_global_load_lds((const void *)(ib0 + 1024u * k),
+                                                     (__attribute__((address_space(3))) void *)&stage[(wave * LS + k) * 64],
+                                                     16, 0, 0);
+            }
+        }
         if (MODE == BS_CTR) {
             /* C = cbase + vbase (128-bit, or 64-bit wrap) */
             uint64_t clo = P.cbase.lo + vbase;
@@ -171,7 +189,7 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
 
         if (MODE == BS_CTR) {
 #pragma unroll
-            for (int k = 0; k < PF; ++k)
+            for (int k = LS; k < LS + PF && k < 32; ++k)
                 pt[k] = slot_ok(k) ? *(const uint4 *)(ib + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
         }
         const uint32_t k0 = rk[4 * NR + 0], k1 = rk[4 * NR + 1], k2 = rk[4 * NR + 2],
@@ -182,7 +200,7 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
                 sched_fence();
                 if (MODE == BS_CTR) {
 #pragma unroll
-                    for (int j = k + PF; j < k + PF + 4 && j < 32; ++j)
+                    for (int j = (k + PF > LS + PF ? k + PF : LS + PF); j < k + PF + 4 && j < 32; ++j)
                         pt[j] = slot_ok(j) ? *(const uint4 *)(ib + lo + 1024u * j) : make_uint4(0, 0, 0, 0);
                 }
             }
@@ -190,7 +208,7 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
             if (slot_ok(k)) {
                 uint4 o;
                 if (MODE == BS_CTR) {
-                    const uint4 x = pt[k];
+                    const uint4 x = k < LS ? stage[(wave * LS + k) * 64 + lane] : pt[k];
                     o.x = x3(x.x, s[k], k0);
                     o.y = x3(x.y, s[32 + k], k1);
                     o.z = x3(x.z, s[64 + k], k2);
@@ -221,19 +239,28 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     if (wgs < 1) wgs = 1;
     if (wgs > 0xFFFFFFFFull) return hipErrorInvalidValue;
     static const bool cache = getenv("OTC_BS_CTR_CACHE") && atoi(getenv("OTC_BS_CTR_CACHE")) != 0;
-    /* CTR plaintext prefetch distance: 8 slots for AES-128 (+1%, measured;
-     * OTC_BS_PF=0 turns it off).  AES-192/256 keep PF = 0: there the extra
-     * registers cost the second wave per SIMD (-45%). */
+    /* CTR plaintext: LS = 20 slots (20 KiB per wave, 160 KiB for the two
+     * 4-wave workgroups a CU holds) prefetched into LDS at task start
+     * (OTC_BS_LDS=0 turns it off); the rest pipelined PF = 8 slots ahead in
+     * registers for AES-128 (OTC_BS_PF=0 turns it off; AES-192/256 keep PF = 0:
+     * there the extra registers cost the second wave per SIMD). */
     static const bool pf = !getenv("OTC_BS_PF") || atoi(getenv("OTC_BS_PF")) != 0;
+    static const bool lds = !getenv("OTC_BS_LDS") || atoi(getenv("OTC_BS_LDS")) != 0;
+    const dim3 g((unsigned)wgs), b(256);
     if (MODE == BS_CTR && cache) {
-        hipLaunchKernelGGL((k_aes_bs<NR, MODE, true, 0>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
-    } else if constexpr (MODE == BS_CTR && NR == 10) {
-        if (pf)
-            hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 8>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
+        hipLaunchKernelGGL((k_aes_bs<NR, MODE, true, 0, 0>), g, b, 0, st, P, K);
+    } else if constexpr (MODE == BS_CTR) {
+        constexpr int PFN = NR == 10 ? 8 : 0;
+        if (lds && pf)
+            hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, PFN, 20>), g, b, 0, st, P, K);
+        else if (lds)
+            hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 0, 20>), g, b, 0, st, P, K);
+        else if (pf)
+            hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, PFN, 0>), g, b, 0, st, P, K);
         else
-            hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 0>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
+            hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 0, 0>), g, b, 0, st, P, K);
     } else {
-        hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 0>), dim3((unsigned)wgs), dim3(256), 0, st, P, K);
+        hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 0, 0>), g, b, 0, st, P, K);
     }
     return hipGetLastError();
 }
