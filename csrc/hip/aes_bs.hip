@@ -83,13 +83,16 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
         if (MODE == BS_CTR && LS > 0) {
             const int64_t t0 = (int64_t)vbase - (int64_t)shift;
             const uint8_t *ib0 = P.in + t0 * 16 + lane * 16u;
+            /* branch-free (a per-slot branch splits the kernel's one basic
+             * block and costs ~70 VGPRs): lanes outside the buffer load block 0
+             * instead, and their slots are never stored */
 #pragma unroll
             for (int k = 0; k < LS; ++k) {
                 const int64_t si = t0 + (int64_t)lane + 64 * k;
-                if (full || (si >= 0 && (uint64_t)si < P.nblocks))
-                    __builtin_amdgcn_global_load_lds((const void *)(ib0 + 1024u * k),
-                                                     (__attribute__((address_space(3))) void *)&stage[(wave * LS + k) * 64],
-                                                     16, 0, 0);
+                const bool ok = full || (si >= 0 && (uint64_t)si < P.nblocks);
+                __builtin_amdgcn_global_load_lds((const void *)(ok ? ib0 + 1024u * k : P.in),
+                                                 (__attribute__((address_space(3))) void *)&stage[(wave * LS + k) * 64],
+                                                 16, 0, 0);
             }
         }
         if (MODE == BS_CTR) {
@@ -208,7 +211,9 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
             if (slot_ok(k)) {
                 uint4 o;
                 if (MODE == BS_CTR) {
-                    const uint4 x = k < LS ? stage[(wave * LS + k) * 64 + lane] : pt[k];
+                    /* lane index from the laundered offset: keeps the LDS
+                     * reads below the round phase (else hoisted, +70 VGPRs) */
+                    const uint4 x = k < LS ? stage[(wave * LS + k) * 64 + (lo >> 4)] : pt[k];
                     o.x = x3(x.x, s[k], k0);
                     o.y = x3(x.y, s[32 + k], k1);
                     o.z = x3(x.z, s[64 + k], k2);
@@ -239,24 +244,24 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     if (wgs < 1) wgs = 1;
     if (wgs > 0xFFFFFFFFull) return hipErrorInvalidValue;
     static const bool cache = getenv("OTC_BS_CTR_CACHE") && atoi(getenv("OTC_BS_CTR_CACHE")) != 0;
-    /* CTR plaintext: LS = 20 slots (20 KiB per wave, 160 KiB for the two
-     * 4-wave workgroups a CU holds) prefetched into LDS at task start
-     * (OTC_BS_LDS=0 turns it off); the rest pipelined PF = 8 slots ahead in
-     * registers for AES-128 (OTC_BS_PF=0 turns it off; AES-192/256 keep PF = 0:
-     * there the extra registers cost the second wave per SIMD). */
+    /* AES-128 CTR plaintext: LS = 20 slots (20 KiB per wave, 160 KiB for the
+     * two 4-wave workgroups a CU holds) prefetched into LDS at task start
+     * (+5%, OTC_BS_LDS=0 turns it off), the rest pipelined PF = 8 slots ahead
+     * in registers (+1%, OTC_BS_PF=0).  AES-192/256 use neither: with 48/60
+     * round-key SGPRs either one pushes them past 256 VGPRs and costs the
+     * second wave per SIMD (-45%). */
     static const bool pf = !getenv("OTC_BS_PF") || atoi(getenv("OTC_BS_PF")) != 0;
     static const bool lds = !getenv("OTC_BS_LDS") || atoi(getenv("OTC_BS_LDS")) != 0;
     const dim3 g((unsigned)wgs), b(256);
     if (MODE == BS_CTR && cache) {
         hipLaunchKernelGGL((k_aes_bs<NR, MODE, true, 0, 0>), g, b, 0, st, P, K);
-    } else if constexpr (MODE == BS_CTR) {
-        constexpr int PFN = NR == 10 ? 8 : 0;
+    } else if constexpr (MODE == BS_CTR && NR == 10) {
         if (lds && pf)
-            hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, PFN, 20>), g, b, 0, st, P, K);
+            hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 8, 20>), g, b, 0, st, P, K);
         else if (lds)
             hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 0, 20>), g, b, 0, st, P, K);
         else if (pf)
-            hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, PFN, 0>), g, b, 0, st, P, K);
+            hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 8, 0>), g, b, 0, st, P, K);
         else
             hipLaunchKernelGGL((k_aes_bs<NR, MODE, false, 0, 0>), g, b, 0, st, P, K);
     } else {
