@@ -52,15 +52,14 @@ enum : int { BS_CTR = 0, BS_ECB = 1 };
 
 __device__ __forceinline__ W lane_mask(uint32_t lane, int n) { return (W)(0u - ((lane >> n) & 1u)); }
 
+/* CTR: the plaintext of slots 0..LS-1 is copied into LDS by the DMA path
+ * (global_load_lds_dwordx4, no VGPRs) when the task starts and lands while the
+ * ~60 us of rounds run; layout [wave][slot][lane] x 16 B is exactly the
+ * lane-linear image glds writes, and each lane reads its own 16 B back with a
+ * conflict-free ds_read_b128. */
 template <int NR, int MODE, bool CACHE, int PF, int LS>
-__global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
+__device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key &K, uint4 *stage)
 {
-    /* CTR: the plaintext of slots 0..LS-1 is copied into LDS by the DMA path
-     * (global_load_lds_dwordx4, no VGPRs) when the task starts and lands
-     * while the ~60 us of rounds run; layout [wave][slot][lane] x 16 B is
-     * exactly the lane-linear image glds writes, and each lane reads its own
-     * 16 B back with a conflict-free ds_read_b128. */
-    __shared__ uint4 stage[LS > 0 ? 4 * LS * 64 : 1];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t gwave = (uint64_t)blockIdx.x * 4u + wave;
@@ -227,6 +226,24 @@ __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
     }
 }
 
+template <int NR, int MODE, bool CACHE, int PF, int LS>
+__global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
+{
+    __shared__ uint4 stage[LS > 0 ? 4 * LS * 64 : 1];
+    aes_bs_task<NR, MODE, CACHE, PF, LS>(P, K, stage);
+}
+
+/* Same task at 3 waves per SIMD (<= 168 VGPRs, ~32 values spilled to
+ * scratch): the default (OTC_BS_W3=0 selects k_aes_bs).  LS > 0 (12 slots, 3
+ * workgroups x 48 KiB) measured slower: more spills than latency saved. */
+template <int NR, int MODE, int LS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_aes_bs_w3(BsParams P,
+                                                                                             otc_aes_key K)
+{
+    __shared__ uint4 stage[LS > 0 ? 4 * LS * 64 : 1];
+    aes_bs_task<NR, MODE, false, 0, LS>(P, K, stage);
+}
+
 int g_cus = 0;
 
 template <int NR, int MODE>
@@ -251,9 +268,16 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
      * round-key SGPRs either one pushes them past 256 VGPRs and costs the
      * second wave per SIMD (-45%). */
     static const bool pf = !getenv("OTC_BS_PF") || atoi(getenv("OTC_BS_PF")) != 0;
-    static const bool lds = !getenv("OTC_BS_LDS") || atoi(getenv("OTC_BS_LDS")) != 0;
     const dim3 g((unsigned)wgs), b(256);
-    if (MODE == BS_CTR && cache) {
+    /* Default: 3 waves per SIMD (<= 168 VGPRs with ~32 values in scratch):
+     * +9..15% over the 2-wave builds below in every mode and key size, whose
+     * register-hungry plaintext prefetches (PF, LDS) it makes unnecessary
+     * (measured: docs/PERF.md).  OTC_BS_W3=0 selects the 2-wave builds. */
+    static const bool w3 = !getenv("OTC_BS_W3") || atoi(getenv("OTC_BS_W3")) != 0;
+    static const bool lds = !getenv("OTC_BS_LDS") || atoi(getenv("OTC_BS_LDS")) != 0;
+    if (w3 && !(MODE == BS_CTR && cache)) {
+        hipLaunchKernelGGL((k_aes_bs_w3<NR, MODE, 0>), g, b, 0, st, P, K);
+    } else if (MODE == BS_CTR && cache) {
         hipLaunchKernelGGL((k_aes_bs<NR, MODE, true, 0, 0>), g, b, 0, st, P, K);
     } else if constexpr (MODE == BS_CTR && NR == 10) {
         if (lds && pf)
