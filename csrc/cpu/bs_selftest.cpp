@@ -53,6 +53,23 @@ extern "C" int otc_bitslice_selftest(int verbose)
                 ++fails;
             }
     }
+    /* transpose32 (perm / bit-select stages) vs the bit-by-bit reference */
+    for (int t = 0; t < 64; ++t) {
+        W a[32], b[32];
+        uint64_t z = 0x9E3779B97F4A7C15ull * (uint64_t)(t + 1);
+        for (int i = 0; i < 32; ++i) {
+            z ^= z << 13; z ^= z >> 7; z ^= z << 17;
+            a[i] = b[i] = (W)(z >> 11);
+        }
+        transpose32(a);
+        transpose32_ref(b);
+        for (int i = 0; i < 32; ++i)
+            if (a[i] != b[i]) {
+                if (verbose) printf("  transpose32 mismatch (trial %d, word %d)\n", t, i);
+                ++fails;
+                break;
+            }
+    }
     /* full cipher */
     srand(7);
     for (int bits = 128; bits <= 256; bits += 64) {

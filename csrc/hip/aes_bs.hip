@@ -261,20 +261,19 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     if (wgs < 1) wgs = 1;
     if (wgs > 0xFFFFFFFFull) return hipErrorInvalidValue;
     static const bool cache = getenv("OTC_BS_CTR_CACHE") && atoi(getenv("OTC_BS_CTR_CACHE")) != 0;
-    /* AES-128 CTR plaintext: LS = 20 slots (20 KiB per wave, 160 KiB for the
-     * two 4-wave workgroups a CU holds) prefetched into LDS at task start
-     * (+5%, OTC_BS_LDS=0 turns it off), the rest pipelined PF = 8 slots ahead
-     * in registers (+1%, OTC_BS_PF=0).  AES-192/256 use neither: with 48/60
-     * round-key SGPRs either one pushes them past 256 VGPRs and costs the
-     * second wave per SIMD (-45%). */
-    static const bool pf = !getenv("OTC_BS_PF") || atoi(getenv("OTC_BS_PF")) != 0;
+    /* 2-wave builds (OTC_BS_W3=0), AES-128 CTR options: LS = 20 plaintext
+     * slots prefetched into LDS at task start (OTC_BS_LDS=1, measured +5% on
+     * the 2-wave build) and PF = 8 slots pipelined in registers (OTC_BS_PF=1,
+     * +1%).  Off by default: the 3-wave build beats both, and with the current
+     * transpose they push the 2-wave build past 256 VGPRs. */
+    static const bool pf = getenv("OTC_BS_PF") && atoi(getenv("OTC_BS_PF")) != 0;
     const dim3 g((unsigned)wgs), b(256);
     /* Default: 3 waves per SIMD (<= 168 VGPRs with ~32 values in scratch):
      * +9..15% over the 2-wave builds below in every mode and key size, whose
      * register-hungry plaintext prefetches (PF, LDS) it makes unnecessary
      * (measured: docs/PERF.md).  OTC_BS_W3=0 selects the 2-wave builds. */
     static const bool w3 = !getenv("OTC_BS_W3") || atoi(getenv("OTC_BS_W3")) != 0;
-    static const bool lds = !getenv("OTC_BS_LDS") || atoi(getenv("OTC_BS_LDS")) != 0;
+    static const bool lds = getenv("OTC_BS_LDS") && atoi(getenv("OTC_BS_LDS")) != 0;
     if (w3 && !(MODE == BS_CTR && cache)) {
         hipLaunchKernelGGL((k_aes_bs_w3<NR, MODE, 0>), g, b, 0, st, P, K);
     } else if (MODE == BS_CTR && cache) {

@@ -379,19 +379,71 @@ OTC_HD void round_last(W *s, const W *k)
  * and back.  Plane 8*b+i, bit k  <->  block k, byte b, bit i, i.e. word
  * w = b/4, bit 8*(b%4)+i of blk[k][w].  Each word-column w is an independent
  * 32x32 bit-matrix transpose. */
+/* v_perm_b32 (byte select from {hi, lo}; selector bytes 0-3 = lo, 4-7 = hi),
+ * emulated on the host. */
+OTC_HD W perm_b(W hi, W lo, uint32_t sel)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_perm(hi, lo, sel);
+#else
+    W r = 0;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t s = (sel >> (8 * i)) & 0xFFu;
+        const W byte = s < 4 ? (lo >> (8 * s)) & 0xFFu : (hi >> (8 * (s - 4))) & 0xFFu;
+        r |= byte << (8 * i);
+    }
+    return r;
+#endif
+}
+
+/* bit select: m ? x : y  (v_bfi_b32 / v_bitop3_b32) */
+OTC_HD W bsel(W m, W x, W y) { return (x & m) | (y & ~m); }
+
+/* one bit-level block-swap stage of transpose32 (J = 4, 2, 1; a template so
+ * the stage is fully unrolled -- a rolled loop puts m[] in scratch) */
+template <int J>
+OTC_HD void transpose_bits(W *m, W mk)
+{
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        if (k & J) continue;
+        const W a = m[k], b = m[k | J];
+        m[k] = bsel(mk << J, b << J, a);
+        m[k | J] = bsel(mk, a >> J, b);
+    }
+}
+
 OTC_HD void transpose32(W *m)
 {
-    /* in-place 32x32 transpose: m[r] bit c  ->  m[c] bit r */
-    W mask = 0x0000FFFFu;
+    /* in-place 32x32 transpose: m[r] bit c  ->  m[c] bit r.  Classic 5-stage
+     * block swap; the 16- and 8-bit stages only move bytes, so each output
+     * word is one v_perm_b32 (2 ops per pair instead of 5); the 4/2/1-bit
+     * stages are a shift and a bit select per word (4 ops per pair). */
 #pragma unroll
-    for (int j = 16; j != 0; j >>= 1, mask ^= (mask << j)) {
-#pragma unroll
-        for (int k = 0; k < 32; k = ((k | j) + 1) & ~j) {
-            W t = ((m[k] >> j) ^ m[k | j]) & mask;
-            m[k] ^= t << j;
-            m[k | j] ^= t;
-        }
+    for (int k = 0; k < 16; ++k) {
+        const W a = m[k], b = m[k | 16];
+        m[k] = perm_b(b, a, 0x05040100u);      /* [b1 b0 a1 a0] */
+        m[k | 16] = perm_b(b, a, 0x07060302u); /* [b3 b2 a3 a2] */
     }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        if (k & 8) continue;
+        const W a = m[k], b = m[k | 8];
+        m[k] = perm_b(b, a, 0x06020400u);     /* [b2 a2 b0 a0] */
+        m[k | 8] = perm_b(b, a, 0x07030501u); /* [b3 a3 b1 a1] */
+    }
+    transpose_bits<4>(m, 0x0F0F0F0Fu);
+    transpose_bits<2>(m, 0x33333333u);
+    transpose_bits<1>(m, 0x55555555u);
+}
+
+/* Reference transpose (host tests). */
+inline void transpose32_ref(W *m)
+{
+    W t[32] = {0};
+    for (int r = 0; r < 32; ++r)
+        for (int c = 0; c < 32; ++c) t[c] |= ((m[r] >> c) & 1u) << r;
+    for (int i = 0; i < 32; ++i) m[i] = t[i];
 }
 
 } /* namespace otc_bs */
