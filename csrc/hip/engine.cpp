@@ -777,6 +777,7 @@ extern "C" int otc_engine_run(otc_engine *e, int mode, const void *host_in, void
  * released on every exit path. */
 struct RcclJob {
     int n = 0;
+    size_t S = 0;                         /* per-GPU bytes per round */
     std::vector<ncclComm_t> comms;
     std::vector<hipStream_t> st;          /* per GPU: scatter, cipher, gather */
     std::vector<void *> dsh, dsh_out;     /* per GPU S-byte piece (in / out) */
@@ -847,13 +848,10 @@ struct RcclJob {
     }
 };
 
-static int rccl_scatter_gather(int ngpus, int mode, const uint8_t *hin, uint8_t *hout, size_t nbytes,
-                               const otc_aes_key *k, const uint8_t ivc[16], int impl, size_t chunk_bytes)
+static int rccl_job_init(RcclJob &J, int ngpus, size_t S)
 {
-    const char *to = getenv("OTC_RCCL_TIMEOUT_S");
-    const double timeout_s = to ? atof(to) : 600.0;
-    RcclJob J;
     J.n = ngpus;
+    J.S = S;
     J.comms.assign(ngpus, nullptr);
     J.st.assign(ngpus, nullptr);
     J.dsh.assign(ngpus, nullptr);
@@ -861,8 +859,6 @@ static int rccl_scatter_gather(int ngpus, int mode, const uint8_t *hin, uint8_t 
     std::vector<int> devs(ngpus);
     for (int g = 0; g < ngpus; ++g) devs[g] = g;
     RCCLCHK(ncclCommInitAll(J.comms.data(), ngpus, devs.data()));
-    size_t S = chunk_bytes ? chunk_bytes : (size_t)64 << 20; /* per-GPU bytes per round */
-    S = (S + 15) & ~(size_t)15;
     const size_t round = S * (size_t)ngpus;
     for (int g = 0; g < ngpus; ++g) {
         HIPCHK(hipSetDevice(g));
@@ -879,6 +875,54 @@ static int rccl_scatter_gather(int ngpus, int mode, const uint8_t *hin, uint8_t 
         for (hipEvent_t *ev : {&J.ev_in[i], &J.ev_scattered[i], &J.ev_gathered[i], &J.ev_drained[i]})
             HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
     }
+    return OTC_OK;
+}
+
+/* The communicators, streams and buffers of the last job are cached across
+ * calls (ncclCommInitAll + allocation cost ~0.4 s, more than streaming 8 GiB);
+ * a different GPU count or round size rebuilds them, a failure aborts them,
+ * otc_multi_release() frees them.  Never torn down by a static destructor:
+ * at process exit the HIP runtime may already be gone. */
+std::mutex g_rccl_mu;
+RcclJob *g_rccl = nullptr;
+
+static int rccl_job_run(RcclJob &J, int mode, const uint8_t *hin, uint8_t *hout, size_t nbytes,
+                        const otc_aes_key *k, const uint8_t ivc[16], int impl, double timeout_s);
+
+static int rccl_scatter_gather(int ngpus, int mode, const uint8_t *hin, uint8_t *hout, size_t nbytes,
+                               const otc_aes_key *k, const uint8_t ivc[16], int impl, size_t chunk_bytes)
+{
+    const char *to = getenv("OTC_RCCL_TIMEOUT_S");
+    const double timeout_s = to ? atof(to) : 600.0;
+    size_t S = chunk_bytes ? chunk_bytes : (size_t)64 << 20; /* per-GPU bytes per round */
+    S = (S + 15) & ~(size_t)15;
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    if (g_rccl && (g_rccl->n != ngpus || g_rccl->S != S)) {
+        delete g_rccl;
+        g_rccl = nullptr;
+    }
+    if (!g_rccl) {
+        RcclJob *J = new RcclJob;
+        if (int r = rccl_job_init(*J, ngpus, S)) {
+            delete J;
+            return r;
+        }
+        g_rccl = J;
+    }
+    int rc = rccl_job_run(*g_rccl, mode, hin, hout, nbytes, k, ivc, impl, timeout_s);
+    if (rc) { /* unknown state: abort the communicators, rebuild next time */
+        g_rccl->failed = true;
+        delete g_rccl;
+        g_rccl = nullptr;
+    }
+    return rc;
+}
+
+static int rccl_job_run(RcclJob &J, int mode, const uint8_t *hin, uint8_t *hout, size_t nbytes,
+                        const otc_aes_key *k, const uint8_t ivc[16], int impl, double timeout_s)
+{
+    const int ngpus = J.n;
+    const size_t S = J.S, round = S * (size_t)ngpus;
     const size_t nrounds = (nbytes + round - 1) / round;
     for (size_t r = 0; r < nrounds; ++r) {
         const int b = (int)(r & 1);
@@ -932,6 +976,13 @@ static int rccl_scatter_gather(int ngpus, int mode, const uint8_t *hin, uint8_t 
     if (int w = J.wait(J.st[0], timeout_s)) return w;
     if (int w = J.wait(J.d2h, timeout_s)) return w;
     return OTC_OK;
+}
+
+extern "C" void otc_multi_release(void)
+{
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    delete g_rccl;
+    g_rccl = nullptr;
 }
 
 extern "C" int otc_multi_run(int ngpus, int strategy, int mode, const void *host_in, void *host_out, size_t nbytes,

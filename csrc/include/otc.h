@@ -205,6 +205,10 @@ int otc_multi_run(int ngpus, int strategy, int mode, const void *host_in, void *
                   size_t nbytes, const otc_aes_key *k, const uint8_t iv_or_ctr[16], int impl,
                   size_t chunk_bytes, otc_multi_stats *stats);
 
+/* Free the RCCL communicators / buffers that strategy 1 caches between calls
+ * (rebuilt on demand). */
+void otc_multi_release(void);
+
 /* Device-resident multi-GPU CTR: buffers dev_bufs[g] (already on GPU g) hold
  * shard g of `shard_bytes`; all GPUs encrypt in place concurrently with the
  * right counter offsets.  Returns elapsed ms (wall, all GPUs). */
