@@ -32,6 +32,7 @@
 
 #include "aes.h"
 #include "otc.h"
+#include "otc_aesni.h"
 #include "otc_device.h"
 
 using otc_dev::Ctr128;
@@ -420,6 +421,44 @@ extern "C" int otc_clock_probe(uint64_t *out_dev, double delay_s, double window_
                                      (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "clock_probe launch");
     return OTC_OK;
+}
+
+/* ---- AES-NI-shaped bulk API (otc_aesni.h) ------------------------------- */
+static int key_from_sched(otc_aes_key *k, const unsigned char *sched, int nr, int dir)
+{
+    if (!sched) return set_err(OTC_ERR_ARG, "null key schedule");
+    if (nr != 10 && nr != 12 && nr != 14) return set_err(OTC_ERR_ARG, "number_of_rounds must be 10, 12 or 14");
+    memset(k, 0, sizeof *k);
+    memcpy(k->rk, sched, 16u * (unsigned)(nr + 1)); /* FIPS byte order = LE words on the host */
+    k->nr = nr;
+    k->dir = dir;
+    k->bits = 32 * (nr - 6);
+    return OTC_OK;
+}
+
+extern "C" int otc_AES_ECB_encrypt(const unsigned char *in, unsigned char *out, unsigned long length,
+                                   const unsigned char *key, int number_of_rounds, void *stream)
+{
+    otc_aes_key k;
+    if (int r = key_from_sched(&k, key, number_of_rounds, OTC_DIR_ENCRYPT)) return r;
+    return otc_aes_ecb(in, out, length, &k, OTC_IMPL_AUTO, stream);
+}
+
+extern "C" int otc_AES_ECB_decrypt(const unsigned char *in, unsigned char *out, unsigned long length,
+                                   const unsigned char *key, int number_of_rounds, void *stream)
+{
+    otc_aes_key k;
+    if (int r = key_from_sched(&k, key, number_of_rounds, OTC_DIR_DECRYPT)) return r;
+    return otc_aes_ecb(in, out, length, &k, OTC_IMPL_AUTO, stream);
+}
+
+extern "C" int otc_AES_CTR_encrypt(const unsigned char *in, unsigned char *out, const unsigned char ivec[8],
+                                   const unsigned char nonce[4], unsigned long length, const unsigned char *key,
+                                   int number_of_rounds, void *stream)
+{
+    otc_aes_key k;
+    if (int r = key_from_sched(&k, key, number_of_rounds, OTC_DIR_ENCRYPT)) return r;
+    return otc_aes_ctr_rfc3686(in, out, length, &k, nonce, ivec, 0, OTC_IMPL_AUTO, stream);
 }
 
 /* ---- device info -------------------------------------------------------- */

@@ -146,6 +146,10 @@ def _declare_gpu(lib):
         "otc_fill_random": (c_int, [c_vp, c_sz, c_u64, c_vp]),
         "otc_checksum": (c_int, [c_vp, c_sz, c_vp, c_vp]),
         "otc_clock_probe": (c_int, [c_vp, ctypes.c_double, ctypes.c_double, c_vp]),
+        "otc_AES_ECB_encrypt": (c_int, [c_vp, c_vp, ctypes.c_ulong, c_u8p, c_int, c_vp]),
+        "otc_AES_ECB_decrypt": (c_int, [c_vp, c_vp, ctypes.c_ulong, c_u8p, c_int, c_vp]),
+        "otc_AES_CTR_encrypt": (c_int, [c_vp, c_vp, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int, c_vp]),
+        "otc_multi_release": (None, []),
         "otc_device_count": (c_int, []),
         "otc_device_cus": (c_int, [c_int]),
         "otc_device_clock_khz": (c_int, [c_int]),

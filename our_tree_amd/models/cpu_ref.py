@@ -140,6 +140,21 @@ def aesni_ctr(key: bytes, nonce: bytes, ivec: bytes, data: bytes, block_offset: 
     return bytes(out)[: len(data)]
 
 
+def aesni_schedule(key: bytes, decrypt: bool = False):
+    """(schedule bytes, Nr) as AES_*_Key_Expansion / AES_Key_Expansion_Dec
+    produce them (16*(Nr+1) bytes)."""
+    lib = _native.cpu_lib()
+    nr = {16: 10, 24: 12, 32: 14}[len(key)]
+    sched = (ctypes.c_uint8 * 240)()
+    {10: lib.AES_128_Key_Expansion, 12: lib.AES_192_Key_Expansion, 14: lib.AES_256_Key_Expansion}[nr](
+        _native.as_u8p(bytes(key)), sched)
+    if decrypt:
+        dsched = (ctypes.c_uint8 * 240)()
+        lib.AES_Key_Expansion_Dec(sched, dsched, nr)
+        sched = dsched
+    return bytes(sched)[: 16 * (nr + 1)], nr
+
+
 def aesni_ecb(key: bytes, data: bytes, decrypt: bool = False) -> bytes:
     lib = _native.cpu_lib()
     nr = {16: 10, 24: 12, 32: 14}[len(key)]

@@ -115,3 +115,27 @@ def test_engine_and_multi_reject_bad_arguments(lib):
     rc = lib.otc_multi_run(0, 0, 1, None, None, 16, None, None, 0, 0,
                            ctypes.byref(st) if st is not None else None)
     assert rc == ERR_ARG
+
+
+@pytest.mark.parametrize("bits", [128, 192, 256])
+@pytest.mark.parametrize("dec", [False, True])
+def test_aesni_schedule_bytes_equal_kernel_schedule(lib, bits, dec):
+    """otc_aesni.h passes AES-NI schedules straight to the kernels: the
+    AES_*_Key_Expansion / AES_Key_Expansion_Dec bytes must equal the PolarSSL
+    word schedule (otc_aes_key.rk) byte for byte."""
+    from our_tree_amd.models import cpu_ref
+    if not cpu_ref.aesni_supported():
+        pytest.skip("no AES-NI on this CPU")
+    kb = bytes((7 * i + 3) & 0xFF for i in range(bits // 8))
+    sched, nr = cpu_ref.aesni_schedule(kb, decrypt=dec)
+    k = _native.OtcAesKey()
+    assert lib.otc_aes_key_init(ctypes.byref(k), _native.as_u8p(kb), bits, DEC if dec else ENC) == 0
+    assert k.nr == nr
+    assert bytes(k)[: 16 * (nr + 1)] == sched
+
+
+def test_aesni_shaped_api_rejects_bad_rounds(lib):
+    sched = (ctypes.c_uint8 * 240)()
+    assert lib.otc_AES_ECB_encrypt(A, A + 4096, 64, sched, 11, None) == ERR_ARG
+    assert "number_of_rounds" in err(lib)
+    assert lib.otc_AES_CTR_encrypt(A + 1, A + 4096, c16(), c16(), 64, sched, 10, None) == ERR_ARG

@@ -280,3 +280,30 @@ def test_clock_probe_beside_a_workload(gpu):
     torch.cuda.synchronize()
     ghz = ops.clock_ghz(probe)
     assert 0.3 < ghz < 2.6, ghz
+
+
+@pytest.mark.parametrize("bits", KEYBITS)
+def test_aesni_shaped_device_api(gpu, bits):
+    """otc_AES_{ECB_encrypt,ECB_decrypt,CTR_encrypt} (otc_aesni.h) with AES-NI
+    schedules == the AES-NI CPU baseline (reference aesni.h shapes)."""
+    import ctypes
+    from our_tree_amd import _native
+    if not cpu_ref.aesni_supported():
+        pytest.skip("no AES-NI on this CPU")
+    lib = _native.require_gpu_lib()
+    key = os.urandom(bits // 8)
+    nonce, ivec = os.urandom(4), os.urandom(8)
+    n = 16 * 3001
+    x = rnd(n + 5, gpu, 30)[:n]
+    y = torch.empty_like(x)
+    st = ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
+    es, nr = cpu_ref.aesni_schedule(key)
+    ds, _ = cpu_ref.aesni_schedule(key, decrypt=True)
+    u8 = _native.as_u8p
+    assert lib.otc_AES_CTR_encrypt(x.data_ptr(), y.data_ptr(), u8(ivec), u8(nonce), n, u8(es), nr, st) == 0
+    assert host(y) == cpu_ref.aesni_ctr(key, nonce, ivec, host(x))
+    assert lib.otc_AES_ECB_encrypt(x.data_ptr(), y.data_ptr(), n, u8(es), nr, st) == 0
+    assert host(y) == cpu_ref.aesni_ecb(key, host(x))
+    z = torch.empty_like(x)
+    assert lib.otc_AES_ECB_decrypt(y.data_ptr(), z.data_ptr(), n, u8(ds), nr, st) == 0
+    assert torch.equal(z, x)
