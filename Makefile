@@ -2,7 +2,7 @@
 #
 #   make            -> our_tree_amd/lib/libotc.so (HIP kernels + runtime + CPU oracle)
 #                      our_tree_amd/lib/libotc_cpu.so (CPU oracle only, no ROCm deps)
-#                      bin/test bin/aes_test bin/aes_ecb_e bin/aes_ecb_d bin/otbench
+#                      bin/test bin/aes_test bin/aes_ecb_e bin/aes_ecb_d bin/otbench bin/bc_test
 #   make cpu        -> CPU-only pieces (no hipcc needed)
 #   make SAN=1 cpu  -> CPU oracle with ASan/UBSan (host only)
 #   make SAN=thread cpu -> CPU oracle with ThreadSanitizer (host only)
@@ -40,7 +40,7 @@ CPU_OBJ := $(patsubst csrc/cpu/%.c,$(OBJ)/cpu/%.o,$(CPU_SRC)) $(OBJ)/cpu/bs_self
 HIP_SRC := csrc/hip/aes_tt.hip csrc/hip/aes_bs.hip csrc/hip/stream_ops.hip
 HIP_OBJ := $(patsubst csrc/hip/%.hip,$(OBJ)/hip/%.o,$(HIP_SRC)) $(OBJ)/hip/engine.o
 
-BINS := bin/test bin/aes_test bin/aes_ecb_e bin/aes_ecb_d bin/otbench
+BINS := bin/test bin/aes_test bin/aes_ecb_e bin/aes_ecb_d bin/otbench bin/bc_test
 
 .PHONY: all cpu clean
 all: $(LIBDIR)/libotc.so $(LIBDIR)/libotc_cpu.so $(BINS) bin/test_cpu bin/aes_test_cpu
@@ -107,6 +107,10 @@ bin/aes_ecb_d: csrc/cli/aes_ecb_d.c $(LIBDIR)/libotc.so
 bin/otbench: csrc/cli/otbench.cpp $(LIBDIR)/libotc.so
 	@mkdir -p bin
 	$(CXX) -O2 -std=c++17 $(INC) $< -o $@ -L$(LIBDIR) -lotc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
+
+bin/bc_test: csrc/cli/bc_test.cpp csrc/include/otc_cipher.hpp $(LIBDIR)/libotc.so
+	@mkdir -p bin
+	$(CXX) -O2 -std=c++17 -Wall $(INC) $< -o $@ -L$(LIBDIR) -lotc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 
 clean:
 	rm -rf build $(LIBDIR)/*.so $(BINS) bin/test_cpu bin/aes_test_cpu

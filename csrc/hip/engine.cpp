@@ -681,6 +681,19 @@ static bool is_pinned(const void *p)
     return a.type == hipMemoryTypeHost;
 }
 
+extern "C" int otc_ptr_kind(const void *p)
+{
+    if (!p) return OTC_PTR_HOST;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return OTC_PTR_HOST;
+    }
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) return OTC_PTR_DEVICE;
+    if (a.type == hipMemoryTypeHost) return OTC_PTR_PINNED;
+    return OTC_PTR_HOST;
+}
+
 /* Launch the cipher on one device chunk. `blk0` = block offset of the chunk
  * inside the whole stream; `prev` = for CBC-dec, the 16-byte ciphertext block
  * preceding the chunk (the halo), as counter-style numeric IV. */

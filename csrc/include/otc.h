@@ -178,6 +178,13 @@ int otc_engine_run(otc_engine *e, int mode, const void *host_in, void *host_out,
                    const otc_aes_key *k, const uint8_t iv_or_ctr[16], uint64_t block_offset,
                    int impl, otc_stream_stats *stats);
 
+/* Where a pointer lives: pageable host memory, pinned host memory, or device
+ * memory (decides between the kernels and the host pipeline). */
+#define OTC_PTR_HOST 0
+#define OTC_PTR_PINNED 1
+#define OTC_PTR_DEVICE 2
+int otc_ptr_kind(const void *p);
+
 /* Pin / unpin an existing host range (hipHostRegister) so the engine copies
  * it without staging. */
 int otc_host_register(void *p, size_t nbytes);

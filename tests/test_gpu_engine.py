@@ -106,3 +106,15 @@ def test_resumable_file_job_on_gpu(gpu, tmp_path, mode):
         be.close()
     ref = cpu_ref.ctr(key, iv, data) if mode == "ctr" else cpu_ref.cbc(key, iv, data, decrypt=True)
     assert dst.read_bytes() == ref
+
+
+def test_cpp_blockcipher_interface(gpu):
+    """csrc/include/otc_cipher.hpp (otc::BlockCipher / otc::AesGpu) through
+    bin/bc_test: FIPS-197 vectors on device and host buffers, CTR/CBC host
+    path == device path, error paths."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bin", "bc_test")
+    if not os.path.exists(exe):
+        pytest.fail("bin/bc_test not built (make)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "bc_test: OK" in r.stdout, r.stdout + r.stderr
