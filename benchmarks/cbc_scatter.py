@@ -8,7 +8,13 @@ link is not the bottleneck), scatters equal pieces (RCCL scatter = one-hop
 fan-out over the root's 7 xGMI links), every rank CBC-encrypts its piece as
 independent 4 KiB sectors (IV_s = iv0 + global sector index -- the parallel
 CBC semantic), and the ciphertext is gathered back to
-the root.  Default total: 32 GiB per GPU (256 GiB at 8 GPUs).
+the root.  Default total: 32 GiB per GPU (256 GiB at 8 GPUs), streamed in
+rounds of --chunk-mib per rank, so nothing close to 256 GiB is ever resident.
+
+The rounds run through parallel.dist.ScatterGatherPipeline: the gather of
+round r (root ingress) is issued asynchronously on its own communicator and
+overlaps the scatter of round r+1 (root egress) -- xGMI links are full
+duplex.  --no-overlap serialises both on one communicator (A/B).
 
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 benchmarks/cbc_scatter.py
     python benchmarks/cbc_scatter.py --gib-per-gpu 4        # 1 GPU
@@ -20,7 +26,6 @@ import sys
 import time
 
 import torch
-import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -36,6 +41,7 @@ def main():
     ap.add_argument("--chunk-mib", type=int, default=1024, help="per-rank bytes per scatter round")
     ap.add_argument("--sector", type=int, default=4096)
     ap.add_argument("--bits", type=int, default=256)
+    ap.add_argument("--no-overlap", action="store_true", help="serial scatter -> encrypt -> gather rounds")
     args = ap.parse_args()
 
     rank, world, local = pdist.init_from_env()
@@ -43,56 +49,52 @@ def main():
     chunk = args.chunk_mib << 20
     total = int(args.gib_per_gpu * (1 << 30)) * world
     total -= total % (chunk * world)
+    rounds = total // (chunk * world)
     key = bytes(range(args.bits // 8))
     iv0 = bytes(range(0xA0, 0xB0))
     seg = args.sector
+    pipe = pdist.ScatterGatherPipeline(chunk, root=0, device=dev, overlap=not args.no_overlap)
 
-    src = torch.empty(chunk * world, dtype=torch.uint8, device=dev) if rank == 0 else None
-    recv = torch.empty(chunk, dtype=torch.uint8, device=dev)
-    ct = torch.empty(chunk, dtype=torch.uint8, device=dev)
-    gathered = torch.empty(chunk * world, dtype=torch.uint8, device=dev) if rank == 0 else None
-    rounds = total // (chunk * world)
+    def produce(send, r):
+        ops.fill_random_(send, seed=r)
 
-    def one_round(r, check=False):
-        if rank == 0:
-            ops.fill_random_(src, seed=r)
-        if world > 1:
-            dist.scatter(recv, list(src.chunk(world)) if rank == 0 else None, src=0)
-        else:
-            recv.copy_(src)
+    def work(piece, out, r):
         gofs = (r * world + rank) * chunk
-        ivr = sh.ctr_add(iv0, gofs // seg)
-        ops.cbc_encrypt_segments(recv, key, ivr, seg, out=ct)
-        if world > 1:
-            dist.gather(ct, list(gathered.chunk(world)) if rank == 0 else None, dst=0)
-        else:
-            gathered.copy_(ct)
-        if check and rank == 0:
-            torch.cuda.synchronize()
-            n = 4 * seg
-            pt = src[:n].cpu().numpy().tobytes()
-            exp = cpu_ref.cbc_segments(key, sh.ctr_add(iv0, (r * world) * chunk // seg), pt, seg)
-            return gathered[:n].cpu().numpy().tobytes() == exp
-        return True
+        ops.cbc_encrypt_segments(piece, key, sh.ctr_add(iv0, gofs // seg), seg, out=out)
 
-    ok = one_round(0, check=True)  # warmup + verification (outside timing)
+    verdict = {}
+
+    def verify(gathered, r):
+        """first sectors of rank 0's and the last rank's pieces vs the oracle
+        (warmup round only, outside the timed region)"""
+        torch.cuda.synchronize()
+        n = 4 * seg
+        ok = True
+        for g in (0, world - 1):
+            a = g * chunk
+            pt = pipe.send[r % len(pipe.send)][a:a + n].cpu().numpy().tobytes()
+            exp = cpu_ref.cbc_segments(key, sh.ctr_add(iv0, (r * world + g) * chunk // seg), pt, seg)
+            ok = ok and gathered[a:a + n].cpu().numpy().tobytes() == exp
+        verdict["ok"] = ok
+
+    pipe.run(1, produce, work, verify)  # warmup + verification
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        torch.distributed.barrier()
     t0 = time.perf_counter()
-    for r in range(rounds):
-        one_round(r)
+    pipe.run(rounds, produce, work)
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        torch.distributed.barrier()
     el = pdist.allreduce_max(time.perf_counter() - t0)
     if rank == 0:
-        print(json.dumps({"metric": f"GB/s AES-{args.bits}-CBC (sector-parallel) root scatter/gather", "n_gpus": world,
-                          "total_bytes": total, "rounds": rounds, "chunk_per_rank": chunk, "seconds": round(el, 3),
-                          "value": round(total / el / 1e9, 3), "unit": "GB/s", "verified_sample": bool(ok),
+        print(json.dumps({"metric": f"GB/s AES-{args.bits}-CBC (sector-parallel) root scatter/gather",
+                          "n_gpus": world, "total_bytes": total, "rounds": rounds, "chunk_per_rank": chunk,
+                          "overlap": pipe.overlap, "seconds": round(el, 3), "value": round(total / el / 1e9, 3),
+                          "unit": "GB/s", "verified_sample": bool(verdict.get("ok")),
                           "data": "synthetic random (root GPU fill)"}), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

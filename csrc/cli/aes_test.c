@@ -26,6 +26,8 @@
 #include "otc.h"
 #endif
 
+#define MAX_GPUS 16
+
 static size_t MSG_LEN;
 static unsigned char *msg, *out;
 static aes_context actx;
@@ -94,6 +96,53 @@ static int parse_list(const char *s, long long *o, int max)
 static const char *LABEL[] = {"Plain ECB", "Plain CTR", "AESNI ECB", "AESNI CTR", "HIP ECB", "HIP CTR", "HIP CBC"};
 static const char *SUITE[] = {"plain-ecb", "plain-ctr", "aesni-ecb", "aesni-ctr", "hip-ecb", "hip-ctr", "hip-cbc"};
 
+#ifdef OTC_WITH_GPU
+/* Sample check of a HIP row (outside the timed region): the first 64 bytes of
+ * every GPU's shard against the CPU oracle, with the shard's counter offset
+ * (CTR) or halo IV (CBC decryption). */
+static int verify_shards(int kind, const unsigned char *key, int bits, int nt, void **dout, const size_t *goff,
+                         const size_t *glen)
+{
+    aes_context c;
+    if (kind == 6)
+        aes_setkey_dec(&c, key, (unsigned)bits);
+    else
+        aes_setkey_enc(&c, key, (unsigned)bits);
+    unsigned char ctr0[16] = {0};
+    memcpy(ctr0, nonce, 4);
+    memcpy(ctr0 + 4, ivec, 8);
+    ctr0[15] = 1;
+    for (int g = 0; g < nt; ++g) {
+        unsigned char got[64], exp[64];
+        size_t n = glen[g] < 64 ? glen[g] : 64;
+        if (kind != 5) n &= ~(size_t)15;
+        if (!n) continue;
+        otc_set_device(g);
+        if (otc_memcpy(got, dout[g], n, OTC_D2H)) return 1;
+        const unsigned char *m = msg + goff[g];
+        if (kind == 4) {
+            for (size_t i = 0; i < n; i += 16) aes_crypt_ecb(&c, AES_ENCRYPT, m + i, exp + i);
+        } else if (kind == 5) {
+            unsigned char nc[16], sb[16];
+            memcpy(nc, ctr0, 16);
+            aes_ctr128_add(nc, goff[g] / 16);
+            int o = 0;
+            aes_crypt_ctr(&c, (int)n, &o, nc, sb, m, exp);
+        } else {
+            unsigned char iv[16];
+            memcpy(iv, goff[g] ? m - 16 : ctr0, 16);
+            aes_crypt_cbc(&c, AES_DECRYPT, n, iv, m, exp);
+        }
+        if (memcmp(got, exp, n)) {
+            fprintf(stderr, "%s: output of GPU %d does not match the CPU oracle\n", LABEL[kind], g);
+            return 1;
+        }
+    }
+    otc_set_device(0);
+    return 0;
+}
+#endif
+
 int main(int argc, char **argv)
 {
     long long sizes[16] = {1048576, 10485760, 104857600, 1048576000};
@@ -136,18 +185,29 @@ int main(int argc, char **argv)
                 MSG_LEN = (size_t)sizes[si];
                 int nt = (int)threads[ti];
 #ifdef OTC_WITH_GPU
-                if (kind >= 4 && nt > otc_device_count()) continue;
+                if (kind >= 4 && (nt < 1 || nt > otc_device_count() || nt > MAX_GPUS)) continue;
 #endif
                 printf("%s, %zu, %d, ", LABEL[kind], MSG_LEN, nt);
                 msg = malloc(MSG_LEN);
                 out = malloc(MSG_LEN);
                 for (size_t i = 0; i < MSG_LEN; ++i) msg[i] = (unsigned char)(rand() % 255);
 #ifdef OTC_WITH_GPU
-                void *dmsg = NULL, *dout = NULL;
+                /* HIP rows: column 3 = GPUs; shard g (same planner as the CPU
+                 * threads) is resident on GPU g */
+                void *dmsg[MAX_GPUS] = {0}, *dout[MAX_GPUS] = {0};
+                size_t goff[MAX_GPUS], glen[MAX_GPUS];
                 if (kind >= 4) {
-                    dmsg = otc_dev_malloc(MSG_LEN);
-                    dout = otc_dev_malloc(MSG_LEN);
-                    otc_memcpy(dmsg, msg, MSG_LEN, OTC_H2D);
+                    for (int g = 0; g < nt; ++g) {
+                        shard(g, nt, &goff[g], &glen[g]);
+                        otc_set_device(g);
+                        dmsg[g] = otc_dev_malloc(glen[g]);
+                        dout[g] = otc_dev_malloc(glen[g]);
+                        if (!dmsg[g] || !dout[g]) {
+                            fprintf(stderr, "device alloc failed: %s\n", otc_last_error());
+                            return 1;
+                        }
+                        otc_memcpy(dmsg[g], msg + goff[g], glen[g], OTC_H2D);
+                    }
                 }
 #endif
                 for (int it = 0; it < iters; ++it) {
@@ -176,18 +236,24 @@ int main(int argc, char **argv)
                         memcpy(nc, nonce, 4);
                         memcpy(nc + 4, ivec, 8);
                         nc[15] = 1;
-                        int r;
-                        if (kind == 4) {
-                            otc_aes_key_init(&k, key, bits, OTC_DIR_ENCRYPT);
-                            r = otc_aes_ecb(dmsg, dout, MSG_LEN & ~(size_t)15, &k, OTC_IMPL_AUTO, NULL);
-                        } else if (kind == 5) {
-                            otc_aes_key_init(&k, key, bits, OTC_DIR_ENCRYPT);
-                            r = otc_aes_ctr(dmsg, dout, MSG_LEN, &k, nc, 0, OTC_IMPL_AUTO, NULL);
-                        } else {
-                            otc_aes_key_init(&k, key, bits, OTC_DIR_DECRYPT);
-                            r = otc_aes_cbc_decrypt(dmsg, dout, MSG_LEN & ~(size_t)15, &k, nc, NULL);
+                        otc_aes_key_init(&k, key, bits, kind == 6 ? OTC_DIR_DECRYPT : OTC_DIR_ENCRYPT);
+                        int r = 0;
+                        /* launch every shard, then wait for all GPUs */
+                        for (int g = 0; g < nt && !r; ++g) {
+                            otc_set_device(g);
+                            if (kind == 4) {
+                                r = otc_aes_ecb(dmsg[g], dout[g], glen[g] & ~(size_t)15, &k, OTC_IMPL_AUTO, NULL);
+                            } else if (kind == 5) { /* counter offset of the shard */
+                                r = otc_aes_ctr(dmsg[g], dout[g], glen[g], &k, nc, goff[g] / 16, OTC_IMPL_AUTO, NULL);
+                            } else { /* CBC-dec halo: the ciphertext block before the shard */
+                                const unsigned char *iv = goff[g] ? msg + goff[g] - 16 : nc;
+                                r = otc_aes_cbc_decrypt(dmsg[g], dout[g], glen[g] & ~(size_t)15, &k, iv, NULL);
+                            }
                         }
-                        if (!r) r = otc_device_sync();
+                        for (int g = 0; g < nt && !r; ++g) {
+                            otc_set_device(g);
+                            r = otc_device_sync();
+                        }
                         if (r) {
                             fprintf(stderr, "GPU error: %s\n", otc_last_error());
                             return 1;
@@ -195,10 +261,18 @@ int main(int argc, char **argv)
                     }
 #endif
                     printf("%lld, ", now_us() - t0);
+#ifdef OTC_WITH_GPU
+                    if (kind >= 4 && it == iters - 1 && verify_shards(kind, key, bits, nt, dout, goff, glen)) return 1;
+#endif
                 }
 #ifdef OTC_WITH_GPU
-                otc_dev_free(dmsg);
-                otc_dev_free(dout);
+                if (kind >= 4) {
+                    for (int g = 0; g < nt; ++g) {
+                        otc_dev_free(dmsg[g]);
+                        otc_dev_free(dout[g]);
+                    }
+                    otc_set_device(0);
+                }
 #endif
                 free(msg);
                 free(out);

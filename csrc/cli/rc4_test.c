@@ -9,8 +9,11 @@
  * followed by arc4_self_test(2).  Fixes vs the reference: remainder bytes are
  * not dropped (test.c:50), buffers are freed (test.c:67,79).
  *
- * Extensions:  --device gpu   XOR combiner runs on the GPU (column 3 then
- *                             means GPUs instead of CPU threads; data resident)
+ * Extensions:  --device gpu   XOR combiner runs on the GPUs: column 3 then
+ *                             counts GPUs instead of CPU threads (the buffers
+ *                             are sharded over that many devices, data
+ *                             resident; rows asking for more GPUs than the
+ *                             node has are skipped)
  *              --sizes a,b,.. --threads a,b,.. --iters N --noselftest
  */
 #include <pthread.h>
@@ -25,6 +28,7 @@
 #endif
 
 #define KEY_LENGTH_BYTES 16
+#define MAX_GPUS 16
 
 static long long us_between(struct timeval a, struct timeval b)
 {
@@ -64,10 +68,16 @@ int main(int argc, char **argv)
     }
 #endif
     srand(1337);
+#ifdef OTC_WITH_GPU
+    const int ndev = gpu ? otc_device_count() : 0;
+#endif
     for (int si = 0; si < nsizes; ++si) {
         for (int ti = 0; ti < nthreads; ++ti) {
             size_t len = (size_t)sizes[si];
             int nt = (int)threads[ti];
+#ifdef OTC_WITH_GPU
+            if (gpu && (nt < 1 || nt > ndev || nt > MAX_GPUS)) continue; /* column 3 = GPUs actually used */
+#endif
             printf("RC4, %zu, %d, ", len, nt);
             unsigned char *msg = malloc(len), *out = malloc(len), *ks = malloc(len);
             if (!msg || !out || !ks) {
@@ -86,25 +96,46 @@ int main(int argc, char **argv)
             gettimeofday(&t1, NULL);
             printf("%lld, \n", us_between(t0, t1));
 #ifdef OTC_WITH_GPU
-            void *dm = NULL, *dk = NULL, *dout = NULL;
+            /* GPU mode: the message and keystream are sharded over nt GPUs
+             * (16-byte aligned contiguous shards, resident); each GPU runs the
+             * combiner on its shard, all launched before any is waited for */
+            void *dm[MAX_GPUS] = {0}, *dk[MAX_GPUS] = {0}, *dout[MAX_GPUS] = {0};
+            size_t goff[MAX_GPUS + 1] = {0};
             if (gpu) {
-                dm = otc_dev_malloc(len);
-                dk = otc_dev_malloc(len);
-                dout = otc_dev_malloc(len);
-                if (!dm || !dk || !dout) {
-                    fprintf(stderr, "device alloc failed: %s\n", otc_last_error());
-                    return 1;
+                for (int g = 0; g < nt; ++g) goff[g] = (len / 16 * (size_t)g / (size_t)nt) * 16;
+                goff[nt] = len;
+                for (int g = 0; g < nt; ++g) {
+                    const size_t n = goff[g + 1] - goff[g];
+                    otc_set_device(g);
+                    dm[g] = otc_dev_malloc(n);
+                    dk[g] = otc_dev_malloc(n);
+                    dout[g] = otc_dev_malloc(n);
+                    if (!dm[g] || !dk[g] || !dout[g]) {
+                        fprintf(stderr, "device alloc failed: %s\n", otc_last_error());
+                        return 1;
+                    }
+                    otc_memcpy(dm[g], msg + goff[g], n, OTC_H2D);
+                    otc_memcpy(dk[g], ks + goff[g], n, OTC_H2D);
                 }
-                otc_memcpy(dm, msg, len, OTC_H2D);
-                otc_memcpy(dk, ks, len, OTC_H2D);
             }
 #endif
             for (int it = 0; it < iters; ++it) {
                 gettimeofday(&t0, NULL);
 #ifdef OTC_WITH_GPU
                 if (gpu) {
-                    otc_xor(dm, dk, dout, len, NULL);
-                    otc_device_sync();
+                    int rc = 0;
+                    for (int g = 0; g < nt && !rc; ++g) {
+                        otc_set_device(g);
+                        rc = otc_xor(dm[g], dk[g], dout[g], goff[g + 1] - goff[g], NULL);
+                    }
+                    for (int g = 0; g < nt && !rc; ++g) {
+                        otc_set_device(g);
+                        rc = otc_device_sync();
+                    }
+                    if (rc) {
+                        fprintf(stderr, "GPU error: %s\n", otc_last_error());
+                        return 1;
+                    }
                 } else
 #endif
                     arc4_crypt_mt(len, msg, ks, out, nt);
@@ -113,10 +144,14 @@ int main(int argc, char **argv)
             }
 #ifdef OTC_WITH_GPU
             if (gpu) {
-                otc_memcpy(out, dout, len, OTC_D2H);
-                otc_dev_free(dm);
-                otc_dev_free(dk);
-                otc_dev_free(dout);
+                for (int g = 0; g < nt; ++g) {
+                    otc_set_device(g);
+                    otc_memcpy(out + goff[g], dout[g], goff[g + 1] - goff[g], OTC_D2H);
+                    otc_dev_free(dm[g]);
+                    otc_dev_free(dk[g]);
+                    otc_dev_free(dout[g]);
+                }
+                otc_set_device(0);
             }
 #endif
             /* verify (outside the timed region) */

@@ -101,64 +101,149 @@ def cbc_decrypt_sharded(local_ct: torch.Tensor, key: bytes, iv: bytes) -> torch.
     return torch.frombuffer(bytearray(res), dtype=torch.uint8).view_as(local_ct)
 
 
-def scatter_apply_gather(full: torch.Tensor | None, nbytes: int, fn, root: int = 0,
-                         chunk_per_rank: int = 256 << 20, device=None) -> torch.Tensor | None:
-    """Root-resident stream -> equal-count chunked scatter -> ``fn(piece,
-    global_byte_offset)`` on every rank -> gather back to the root.
+_DUPLEX_GROUPS: dict = {}
 
-    Only 2 x chunk_per_rank of scratch is needed per rank and
-    world x chunk_per_rank on the root, so streams larger than one GPU's
-    HBM can be processed in rounds.  Returns the processed stream on the root
-    (None elsewhere)."""
+
+def duplex_groups():
+    """Two extra communicators over all ranks -- one carries scatters, the
+    other gathers.  Each communicator has its own RCCL stream, so a gather
+    (root ingress) and the next round's scatter (root egress) run at the same
+    time: xGMI links are full duplex, and one communicator would serialise the
+    two directions.  Collective on first use (every rank calls it in the same
+    order); cached afterwards."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return None, None
+    key = (dist.get_backend(), dist.get_world_size())
+    if key not in _DUPLEX_GROUPS:
+        _DUPLEX_GROUPS[key] = (dist.new_group(), dist.new_group())
+    return _DUPLEX_GROUPS[key]
+
+
+class ScatterGatherPipeline:
+    """Double-buffered root scatter -> per-rank work -> root gather.
+
+    Round r: the root fills a ``world x chunk`` staging buffer (``produce``),
+    scatters it (one ``chunk`` per rank), every rank runs ``fn(piece, out, r)``
+    writing ``out``, and ``out`` is gathered back to the root, which hands it to
+    ``consume``.  With ``overlap`` the gather of round r is asynchronous on its
+    own communicator and overlaps the scatter + work of round r+1 (two buffer
+    slots; a slot is reused only after the gather that read it has finished).
+
+    Memory: 4 x chunk per rank, plus 4 x world x chunk on the root -- chunked
+    rounds, so a stream larger than one GPU's 288 GB streams through the root.
+    """
+
+    def __init__(self, chunk_per_rank: int, root: int = 0, device=None, overlap: bool = True):
+        self.rank, self.world = _world()
+        self.root = root
+        if device is None:
+            device = (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
+                      else torch.device("cpu"))
+        self.device = torch.device(device)
+        self.chunk = max(sh.BLOCK, chunk_per_rank - chunk_per_rank % sh.BLOCK)
+        self.overlap = overlap and self.world > 1
+        self.g_sc, self.g_ga = duplex_groups() if self.overlap else (None, None)
+        nslot = 2 if self.overlap else 1
+
+        def mk(n):
+            return torch.empty(n, dtype=torch.uint8, device=self.device)
+
+        self.recv = [mk(self.chunk) for _ in range(nslot)]
+        self.out = [mk(self.chunk) for _ in range(nslot)]
+        is_root = self.rank == root
+        self.send = [mk(self.chunk * self.world) for _ in range(nslot)] if is_root else None
+        self.gath = [mk(self.chunk * self.world) for _ in range(nslot)] if is_root else None
+
+    def _drain(self, pend, consume):
+        work, slot, r = pend
+        if work is not None:
+            work.wait()
+        if self.rank == self.root and consume is not None:
+            consume(self.gath[slot], r)
+
+    def run(self, nrounds: int, produce, fn, consume=None):
+        """produce(send, r): root fills round r's staging buffer;
+        fn(piece, out, r): every rank writes its result for round r to out;
+        consume(gathered, r): root receives round r's gathered results."""
+        is_root = self.rank == self.root
+        nslot = len(self.recv)
+        pending = [None] * nslot
+        for r in range(nrounds):
+            s = r % nslot
+            if pending[s] is not None:  # the gather of round r - nslot still reads out[s]
+                self._drain(pending[s], consume)
+                pending[s] = None
+            if is_root:
+                produce(self.send[s], r)
+            if self.world > 1:
+                dist.scatter(self.recv[s], list(self.send[s].chunk(self.world)) if is_root else None,
+                             src=self.root, group=self.g_sc)
+            else:
+                self.recv[s].copy_(self.send[s])
+            fn(self.recv[s], self.out[s], r)
+            if self.world > 1:
+                work = dist.gather(self.out[s], list(self.gath[s].chunk(self.world)) if is_root else None,
+                                   dst=self.root, group=self.g_ga, async_op=self.overlap)
+            else:
+                self.gath[s].copy_(self.out[s])
+                work = None
+            pending[s] = (work if self.overlap else None, s, r)
+            if not self.overlap:
+                self._drain(pending[s], consume)
+                pending[s] = None
+        for k in range(nrounds, nrounds + nslot):  # drain in round order
+            s = k % nslot
+            if pending[s] is not None:
+                self._drain(pending[s], consume)
+                pending[s] = None
+
+
+def scatter_apply_gather(full: torch.Tensor | None, nbytes: int, fn, root: int = 0,
+                         chunk_per_rank: int = 256 << 20, device=None, overlap: bool = True) -> torch.Tensor | None:
+    """Root-resident stream -> equal-count chunked scatter -> ``fn(piece,
+    global_byte_offset)`` on every rank -> gather back to the root, through
+    ``ScatterGatherPipeline`` (the gather of round r overlaps the scatter of
+    round r+1).  Streams larger than one GPU's HBM are processed in rounds.
+    Returns the processed stream on the root (None elsewhere)."""
     rank, world = _world()
-    if device is None:
-        device = full.device if full is not None else (
-            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
-    chunk_per_rank = max(sh.BLOCK, chunk_per_rank - chunk_per_rank % sh.BLOCK)
-    round_bytes = chunk_per_rank * world
-    out = torch.empty(nbytes, dtype=torch.uint8, device=device) if rank == root else None
-    recv = torch.empty(chunk_per_rank, dtype=torch.uint8, device=device)
+    if device is None and full is not None:
+        device = full.device
+    pipe = ScatterGatherPipeline(chunk_per_rank, root=root, device=device, overlap=overlap)
+    chunk = pipe.chunk
+    round_bytes = chunk * world
+    nrounds = -(-nbytes // round_bytes)
+    out = torch.empty(nbytes, dtype=torch.uint8, device=pipe.device) if rank == root else None
     flat = full.reshape(-1).view(torch.uint8) if full is not None else None
-    for off in range(0, nbytes, round_bytes):
+
+    def produce(send, r):
+        off = r * round_bytes
         n = min(round_bytes, nbytes - off)
-        if rank == root:
-            pieces = []
-            for r in range(world):
-                p = torch.zeros(chunk_per_rank, dtype=torch.uint8, device=device)
-                a, b = off + r * chunk_per_rank, min(off + (r + 1) * chunk_per_rank, off + n)
-                if b > a:
-                    p[: b - a].copy_(flat[a:b])
-                pieces.append(p)
-        else:
-            pieces = None
-        if world > 1:
-            dist.scatter(recv, pieces if rank == root else None, src=root)
-        else:
-            recv.copy_(pieces[0])
-        gofs = off + rank * chunk_per_rank
-        valid = max(0, min(chunk_per_rank, nbytes - gofs))
+        send[:n].copy_(flat[off:off + n])
+        if n < round_bytes:
+            send[n:].zero_()
+
+    def work(piece, dst, r):
+        gofs = r * round_bytes + rank * chunk
+        valid = max(0, min(chunk, nbytes - gofs))
         if valid:
-            recv[:valid] = fn(recv[:valid].contiguous(), gofs)
-        gathered = [torch.empty_like(recv) for _ in range(world)] if rank == root else None
-        if world > 1:
-            dist.gather(recv, gathered, dst=root)
-        else:
-            gathered = [recv.clone()]
-        if rank == root:
-            for r in range(world):
-                a, b = off + r * chunk_per_rank, min(off + (r + 1) * chunk_per_rank, off + n)
-                if b > a:
-                    out[a:b].copy_(gathered[r][: b - a])
+            dst[:valid].copy_(fn(piece[:valid], gofs))
+
+    def consume(gathered, r):
+        off = r * round_bytes
+        n = min(round_bytes, nbytes - off)
+        out[off:off + n].copy_(gathered[:n])
+
+    pipe.run(nrounds, produce, work, consume)
     return out
 
 
 def scatter_ctr(full: torch.Tensor | None, nbytes: int, key: bytes, counter: bytes, root: int = 0,
-                chunk_per_rank: int = 256 << 20, impl="auto"):
+                chunk_per_rank: int = 256 << 20, impl="auto", overlap: bool = True):
     """CTR over a root-resident stream via RCCL scatter/gather."""
     def fn(piece, gofs):
         return _ctr_local(piece, key, counter, gofs // sh.BLOCK, impl)
 
-    return scatter_apply_gather(full, nbytes, fn, root=root, chunk_per_rank=chunk_per_rank)
+    return scatter_apply_gather(full, nbytes, fn, root=root, chunk_per_rank=chunk_per_rank, overlap=overlap)
 
 
 def allreduce_max(value: float, device=None) -> float:
