@@ -774,6 +774,89 @@ __global__ __launch_bounds__(256) void k_cbc_seg_fixup(const uint8_t *in, uint8_
 }
 
 /* ---------------------------------------------------------------------------
+ * Batched CTR (otc_aes_ctr_batch): many independent messages, each with its
+ * own buffers, key and counter, in ONE launch.  Work unit: a wave tile of
+ * 64 x B blocks of one message; tile t belongs to message tile_msg[t] at local
+ * tile t - tile_first[m] (host planner).  The descriptor and the message's
+ * round keys are wave-uniform: loaded once per tile and moved to SGPRs with
+ * readfirstlane, so the rounds are the same code as the single-message kernel
+ * (round keys as SGPR operands of the v_bitop3s).  The LDS 4-table image is
+ * key independent, so one persistent workgroup per CU serves every message.
+ * No counter caching here: tiles start at arbitrary counters.
+ * ------------------------------------------------------------------------- */
+struct BatchParams {
+    const otc_ctr_msg *msgs;
+    const otc_aes_key *keys;
+    const uint32_t *tile_msg;
+    const uint64_t *tile_first;
+    uint64_t ntiles;
+};
+
+__device__ __forceinline__ uint32_t ufl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t ufl64(uint64_t v)
+{
+    return ((uint64_t)ufl((uint32_t)(v >> 32)) << 32) | ufl((uint32_t)v);
+}
+
+template <int NR, int B, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_aes_ctr_batch_tt(BatchParams P)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
+    fill_tbl4<THREADS>(tbl, g_tab.te0);
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = ufl(threadIdx.x >> 6);
+    uint32_t lk[4];
+    tbl4_lane_consts(lane, lk);
+    constexpr uint32_t WAVES = THREADS / 64;
+    constexpr uint64_t TILE = 64u * B;
+
+    for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < P.ntiles; t += (uint64_t)gridDim.x * WAVES) {
+        const uint32_t m = ufl(P.tile_msg[t]);
+        const otc_ctr_msg *D = P.msgs + m;
+        const uint8_t *in = (const uint8_t *)ufl64(D->in);
+        uint8_t *out = (uint8_t *)ufl64(D->out);
+        const uint64_t nbytes = ufl64(D->nbytes);
+        const Ctr128 c = {ufl64(D->ctr_hi), ufl64(D->ctr_lo)};
+        const otc_aes_key *Kg = P.keys + ufl(D->key);
+        otc_aes_key K;
+#pragma unroll
+        for (int q = 0; q < 4 * (NR + 1); ++q) K.rk[q] = ufl(Kg->rk[q]);
+        const uint64_t nfull = nbytes >> 4;
+        const uint32_t tail = (uint32_t)(nbytes & 15u);
+        const uint64_t i0 = (t - ufl64(P.tile_first[m])) * TILE + lane;
+
+        uint32_t s[B][4];
+        uint4 x[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const uint64_t i = i0 + 64u * b;
+            ctr_words(c, i, false, s[b][0], s[b][1], s[b][2], s[b][3]);
+            x[b] = i < nfull ? ld16(in, i) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[b][j] ^= K.rk[j];
+        }
+        enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const uint64_t i = i0 + 64u * b;
+            if (i < nfull) {
+                st16(out, i, make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
+            } else if (i == nfull && tail) {
+                const uint32_t ks[4] = {s[b][0], s[b][1], s[b][2], s[b][3]};
+                for (uint32_t n = 0; n < tail; ++n)
+                    out[16 * i + n] = in[16 * i + n] ^ (uint8_t)(ks[n >> 2] >> (8 * (n & 3)));
+            }
+        }
+    }
+}
+
+constexpr int BATCH_THREADS = 1024;
+constexpr int BATCH_B = 4;
+static_assert(64 * BATCH_B == OTC_BATCH_TILE_BLOCKS, "tile size must match otc.h");
+
+/* ---------------------------------------------------------------------------
  * Host-side launch helpers
  * ------------------------------------------------------------------------- */
 int g_num_cus = 0;
@@ -883,10 +966,31 @@ hipError_t launch_seg_nr(const CbcSegParams &P, const otc_aes_key &K, hipStream_
     return hipGetLastError();
 }
 
+template <int NR>
+hipError_t launch_ctr_batch_nr(const BatchParams &P, hipStream_t st)
+{
+    /* one workgroup per CU (128 KiB LDS), 16 tiles per workgroup step */
+    const int grid = grid_for(P.ntiles, BATCH_THREADS / 64, 1);
+    hipLaunchKernelGGL((k_aes_ctr_batch_tt<NR, BATCH_B, BATCH_THREADS>), dim3(grid), dim3(BATCH_THREADS), 0, st, P);
+    return hipGetLastError();
+}
+
 } // namespace
 
 /* ---- internal entry points used by engine.cpp ---------------------------- */
 namespace otc_impl {
+
+hipError_t tt_ctr_batch(const otc_ctr_msg *msgs, const otc_aes_key *keys, const uint32_t *tile_msg,
+                        const uint64_t *tile_first, uint64_t ntiles, int nr, hipStream_t st)
+{
+    BatchParams P{msgs, keys, tile_msg, tile_first, ntiles};
+    switch (nr) {
+    case 10: return launch_ctr_batch_nr<10>(P, st);
+    case 12: return launch_ctr_batch_nr<12>(P, st);
+    case 14: return launch_ctr_batch_nr<14>(P, st);
+    default: return hipErrorInvalidValue;
+    }
+}
 
 hipError_t tt_ecb_encrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, hipStream_t st)
 {

@@ -47,6 +47,8 @@ hipError_t tt_cbc_decrypt_seg(const void *, void *, uint64_t, uint64_t, const ot
 hipError_t tt_cbc_encrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
 hipError_t bs_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
+hipError_t tt_ctr_batch(const otc_ctr_msg *, const otc_aes_key *, const uint32_t *, const uint64_t *, uint64_t, int,
+                        hipStream_t);
 void tt_set_wg_per_cu(int);
 hipError_t k_xor(const void *, const void *, void *, size_t, hipStream_t);
 hipError_t k_fill_random(void *, size_t, uint64_t, hipStream_t);
@@ -293,6 +295,38 @@ extern "C" int otc_aes_ctr_rfc3686(const void *in, void *out, size_t nbytes, con
     memcpy(cb + 4, ivec, 8);
     cb[12] = 0; cb[13] = 0; cb[14] = 0; cb[15] = 1;
     return ctr_common(in, out, nbytes, k, ctr_add(ctr_from_bytes(cb), block_offset, true), true, impl, stream);
+}
+
+extern "C" uint64_t otc_ctr_batch_plan(const otc_ctr_msg *msgs, size_t nmsg, uint32_t *tile_msg,
+                                       uint64_t *tile_first)
+{
+    const uint64_t tile_bytes = 16ull * OTC_BATCH_TILE_BLOCKS;
+    uint64_t t = 0;
+    for (size_t m = 0; m < nmsg; ++m) {
+        const uint64_t nt = (msgs[m].nbytes + tile_bytes - 1) / tile_bytes;
+        if (tile_first) tile_first[m] = t;
+        if (tile_msg)
+            for (uint64_t k = 0; k < nt; ++k) tile_msg[t + k] = (uint32_t)m;
+        t += nt;
+    }
+    return t;
+}
+
+/* Descriptors live in device memory, so per-message checks (alignment,
+ * overlap) are the planner's job on the host (our_tree_amd.ops.CtrBatch);
+ * here only the launch arguments are validated. */
+extern "C" int otc_aes_ctr_batch(const otc_ctr_msg *msgs, const otc_aes_key *keys, const uint32_t *tile_msg,
+                                 const uint64_t *tile_first, uint64_t ntiles, int nr, void *stream)
+{
+    Range rg("otc_aes_ctr_batch");
+    if (ntiles == 0) return OTC_OK;
+    if (!msgs || !keys || !tile_msg || !tile_first) return set_err(OTC_ERR_ARG, "ctr_batch: null array");
+    if (nr != 10 && nr != 12 && nr != 14) return set_err(OTC_ERR_ARG, "ctr_batch: nr must be 10, 12 or 14");
+    if ((((uintptr_t)msgs) | ((uintptr_t)keys) | ((uintptr_t)tile_first)) & 7u || ((uintptr_t)tile_msg & 3u))
+        return set_err(OTC_ERR_ARG, "ctr_batch: misaligned descriptor arrays");
+    hipError_t e = otc_impl::tt_ctr_batch(msgs, keys, tile_msg, tile_first, ntiles, nr, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "ctr_batch launch");
+    return OTC_OK;
 }
 
 extern "C" int otc_aes_cbc_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,

@@ -104,6 +104,37 @@ int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t seg_bytes, si
 int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
                            const uint8_t iv[16], void *stream);
 
+/* ---- batched CTR: many independent messages in ONE launch -----------------
+ * The serving shape (packets, sectors, objects of a few KiB, each with its own
+ * key and counter): one launch per message is launch-bound (µs each) and far
+ * from the >> 256 workgroups the chip needs.  Here the work unit is a tile of
+ * OTC_BATCH_TILE_BLOCKS 16-byte blocks of one message; every array below is
+ * DEVICE memory:
+ *   msgs[m]        message descriptor (device addresses, length, key index,
+ *                  initial 128-bit big-endian counter as two numeric halves)
+ *   keys[k]        expanded encryption keys (all with `nr` rounds)
+ *   tile_msg[t]    message of tile t          } from otc_ctr_batch_plan()
+ *   tile_first[m]  first tile of message m    }
+ * in == out (in place) is allowed per message; distinct messages must not
+ * overlap.  Messages of 0 bytes have no tiles. */
+#define OTC_BATCH_TILE_BLOCKS 256
+typedef struct {
+    uint64_t in;      /* device address of the input */
+    uint64_t out;     /* device address of the output */
+    uint64_t nbytes;
+    uint64_t ctr_hi;  /* initial counter, bytes 0..7 as a big-endian number */
+    uint64_t ctr_lo;  /* bytes 8..15 */
+    uint32_t key;     /* index into keys[] */
+    uint32_t pad;
+} otc_ctr_msg;
+
+/* Host planner: fills tile_msg (may be NULL to only count) and tile_first for
+ * host copies of the descriptors; returns the number of tiles. */
+uint64_t otc_ctr_batch_plan(const otc_ctr_msg *msgs, size_t nmsg, uint32_t *tile_msg, uint64_t *tile_first);
+
+int otc_aes_ctr_batch(const otc_ctr_msg *msgs, const otc_aes_key *keys, const uint32_t *tile_msg,
+                      const uint64_t *tile_first, uint64_t ntiles, int nr, void *stream);
+
 /* out = a ^ b (the device arc4_crypt combiner). */
 int otc_xor(const void *a, const void *b, void *out, size_t nbytes, void *stream);
 

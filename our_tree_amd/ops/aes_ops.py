@@ -104,6 +104,132 @@ def ctr(x: torch.Tensor, key: bytes, counter: bytes, out: torch.Tensor | None = 
     return out
 
 
+BATCH_TILE_BYTES = 16 * 256  # OTC_BATCH_TILE_BLOCKS (otc.h)
+
+
+class CtrBatch:
+    """A planned batch of independent AES-CTR messages -- own buffers, key and
+    counter each -- executed by ONE kernel launch per key size
+    (``otc_aes_ctr_batch``).
+
+    The serving shape: thousands of packets / sectors / objects of a few KiB.
+    One ``ctr()`` launch per message is launch-bound (microseconds of host and
+    dispatch work per message) and puts a few workgroups on a 256-CU chip; the
+    batch kernel instead deals 4 KiB tiles of all messages to persistent
+    workgroups, one per CU.  Planning (validation, descriptors, tile map, key
+    schedules; one pinned H2D copy) happens once here; ``run()`` only launches,
+    so it can be replayed with new data in the same buffers, and captured in a
+    HIP graph.
+
+    xs / outs: GPU tensors (contiguous, 16-byte aligned; ``outs[i] is xs[i]``
+    for in place); keys: AES keys (16/24/32 bytes) selected per message by
+    ``key_index`` (default: keys[i] for message i); counters: the 16-byte
+    initial counter block of every message (128-bit big-endian increment).
+    Distinct messages must not overlap.
+    """
+
+    def __init__(self, xs, keys, counters, outs=None, key_index=None):
+        import numpy as np
+
+        n = len(xs)
+        if len(counters) != n:
+            raise ValueError("one counter per message")
+        if outs is None:
+            outs = [torch.empty_like(x) for x in xs]
+        if len(outs) != n:
+            raise ValueError("one output per message")
+        if key_index is None:
+            if len(keys) != n:
+                raise ValueError("one key per message, or pass key_index")
+            key_index = range(n)
+        kidx = np.fromiter((int(k) for k in key_index), dtype=np.int64, count=n)
+        if n and (kidx.min() < 0 or kidx.max() >= len(keys)):
+            raise ValueError("key_index out of range")
+        self.outs = list(outs)
+        self._keep = list(xs)  # descriptors hold raw addresses: keep the tensors alive
+        self._launches = []
+        self.device = xs[0].device if n else None
+        if n == 0:
+            return
+        desc = np.zeros((n, 6), dtype=np.uint64)  # in, out, nbytes, ctr_hi, ctr_lo, key
+        for i, (x, o) in enumerate(zip(xs, outs)):
+            _check_dev(x, f"xs[{i}]")
+            _check_dev(o, f"outs[{i}]")
+            if x.device != self.device or o.device != self.device:
+                raise ValueError("all messages must be on one device")
+            nb = _nbytes(x)
+            if _nbytes(o) != nb:
+                raise ValueError(f"outs[{i}] must have the byte size of xs[{i}]")
+            pi, po = x.data_ptr(), o.data_ptr()
+            if nb and (pi % 16 or po % 16):
+                raise ValueError(f"message {i}: batch buffers must be 16-byte aligned (clone a sliced tensor)")
+            if pi != po and pi < po + nb and po < pi + nb:
+                raise ValueError(f"message {i}: input and output overlap partially")
+            c = bytes(counters[i])
+            if len(c) != 16:
+                raise ValueError(f"counters[{i}] must be 16 bytes")
+            desc[i, :5] = (pi, po, nb, int.from_bytes(c[:8], "big"), int.from_bytes(c[8:], "big"))
+        desc[:, 5] = kidx.astype(np.uint64)
+
+        ek = [expand_key(k) for k in keys]
+        key_blob = b"".join(bytes(k) for k in ek)  # otc_aes_key[] (256 B each)
+        nr_msg = np.array([k.nr for k in ek], dtype=np.int64)[kidx]
+        parts, launches, off = [key_blob], [], len(key_blob)
+
+        def add(b: bytes) -> int:
+            nonlocal off
+            pad = (-off) % 16
+            if pad:
+                parts.append(bytes(pad))
+                off += pad
+            at = off
+            parts.append(b)
+            off += len(b)
+            return at
+
+        for nr in (10, 12, 14):
+            sel = np.nonzero(nr_msg == nr)[0]
+            if not len(sel):
+                continue
+            d = desc[sel]
+            tiles = (d[:, 2] + (BATCH_TILE_BYTES - 1)) // BATCH_TILE_BYTES
+            ntiles = int(tiles.sum())
+            if ntiles == 0:
+                continue
+            first = np.zeros(len(sel), dtype=np.uint64)
+            first[1:] = np.cumsum(tiles)[:-1]
+            tmap = np.repeat(np.arange(len(sel), dtype=np.uint32), tiles.astype(np.int64))
+            assert tmap.size == ntiles and int(tmap.max()) < len(sel)
+            launches.append((add(d.tobytes()), add(first.tobytes()), add(tmap.tobytes()), ntiles, nr))
+        host = torch.frombuffer(bytearray(b"".join(parts)), dtype=torch.uint8).pin_memory()
+        self._plan = host.to(self.device, non_blocking=True)
+        self._ready = torch.cuda.Event()
+        self._ready.record(torch.cuda.current_stream(self.device))
+        self._launches = launches
+        self.ntiles = sum(t for *_, t, _ in launches)
+
+    def run(self, stream=None):
+        """Launch the batch on ``stream`` (default: the current stream);
+        returns the list of outputs."""
+        if not self._launches:
+            return self.outs
+        st = stream or torch.cuda.current_stream(self.device)
+        st.wait_event(self._ready)
+        base = self._plan.data_ptr()
+        lib = _lib()
+        with torch.cuda.device(self.device):
+            for o_desc, o_first, o_map, ntiles, nr in self._launches:
+                rc = lib.otc_aes_ctr_batch(base + o_desc, base, base + o_map, base + o_first, ntiles, nr,
+                                           ctypes.c_void_p(st.cuda_stream))
+                _native.check(rc, "otc_aes_ctr_batch")
+        return self.outs
+
+
+def ctr_batch(xs, keys, counters, outs=None, key_index=None):
+    """Plan and run a ``CtrBatch`` once."""
+    return CtrBatch(xs, keys, counters, outs=outs, key_index=key_index).run()
+
+
 def ctr_rfc3686(x: torch.Tensor, key: bytes, nonce: bytes, ivec: bytes, out=None, block_offset: int = 0,
                 impl="auto") -> torch.Tensor:
     """AES-CTR with the AES-NI/RFC 3686 counter block nonce||ivec||BE32(1) and

@@ -139,3 +139,52 @@ def test_aesni_shaped_api_rejects_bad_rounds(lib):
     assert lib.otc_AES_ECB_encrypt(A, A + 4096, 64, sched, 11, None) == ERR_ARG
     assert "number_of_rounds" in err(lib)
     assert lib.otc_AES_CTR_encrypt(A + 1, A + 4096, c16(), c16(), 64, sched, 10, None) == ERR_ARG
+
+
+class CtrMsg(ctypes.Structure):
+    """Mirror of otc_ctr_msg (otc.h)."""
+    _fields_ = [("inp", ctypes.c_uint64), ("out", ctypes.c_uint64), ("nbytes", ctypes.c_uint64),
+                ("ctr_hi", ctypes.c_uint64), ("ctr_lo", ctypes.c_uint64), ("key", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
+
+
+def test_ctr_batch_planner_and_python_plan_agree(lib):
+    """The C host planner (otc_ctr_batch_plan) builds the tile map ops.CtrBatch
+    builds with numpy: 4 KiB tiles, empty messages own none."""
+    import numpy as np
+
+    sizes = [0, 1, 4096, 4097, 16, 0, 3 * 4096 + 15, 100000]
+    msgs = (CtrMsg * len(sizes))(*[CtrMsg(0, 0, n, 0, 0, 0, 0) for n in sizes])
+    fn = lib.otc_ctr_batch_plan
+    fn.restype = ctypes.c_uint64
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    nt = fn(msgs, len(sizes), None, None)
+    tmap = np.zeros(nt, np.uint32)
+    first = np.zeros(len(sizes), np.uint64)
+    assert fn(msgs, len(sizes), tmap.ctypes.data, first.ctypes.data) == nt
+    tiles = (np.array(sizes, np.uint64) + 4095) // 4096
+    assert nt == tiles.sum()
+    assert (tmap == np.repeat(np.arange(len(sizes), dtype=np.uint32), tiles.astype(np.int64))).all()
+    assert first[0] == 0 and (first[1:] == np.cumsum(tiles)[:-1]).all()
+
+
+def test_ctr_batch_rejects_bad_launch_args(lib):
+    f = lib.otc_aes_ctr_batch
+    assert f(A, A, A, A, 0, 10, None) == 0  # nothing to do
+    assert f(None, A, A, A, 4, 10, None) == ERR_ARG and "null" in err(lib)
+    assert f(A, A, A, A, 4, 11, None) == ERR_ARG and "nr" in err(lib)
+    assert f(A + 4, A, A, A, 4, 10, None) == ERR_ARG and "misaligned" in err(lib)
+
+
+def test_ctr_batch_python_validation_without_gpu():
+    import torch
+
+    from our_tree_amd import ops
+
+    x = torch.zeros(16, dtype=torch.uint8)
+    with pytest.raises(ValueError, match="one counter"):
+        ops.CtrBatch([x], [bytes(16)], [])
+    with pytest.raises(ValueError, match="GPU tensor"):
+        ops.CtrBatch([x], [bytes(16)], [bytes(16)])
+    with pytest.raises(ValueError, match="key_index"):
+        ops.CtrBatch([x], [bytes(16)], [bytes(16)], key_index=[3])
