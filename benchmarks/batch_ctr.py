@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--bits", type=int, default=128)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--no-eager", action="store_true")
+    ap.add_argument("--tile", type=int, default=None, help="blocks per tile (64/128/256; default: auto)")
     args = ap.parse_args()
     if args.size % 16:
         raise SystemExit("--size must be a multiple of 16 (messages are views of one buffer)")
@@ -80,11 +81,11 @@ def main():
         res["graph"] = {"ms": round(t_graph * 1e3, 3), "msgs_per_s": round(n / t_graph), "gbps": round(n * size / t_graph / 1e9, 3)}
 
     t0 = time.perf_counter()
-    batch = ops.CtrBatch(xs, keys, ctrs, outs=outs, key_index=kidx)
+    batch = ops.CtrBatch(xs, keys, ctrs, outs=outs, key_index=kidx, tile_blocks=args.tile)
     t_plan = time.perf_counter() - t0
     t_batch = timed(batch.run, args.iters)
     res["batch"] = {"ms": round(t_batch * 1e3, 3), "msgs_per_s": round(n / t_batch), "gbps": round(n * size / t_batch / 1e9, 3),
-                    "plan_ms": round(t_plan * 1e3, 3), "tiles": batch.ntiles}
+                    "plan_ms": round(t_plan * 1e3, 3), "tiles": batch.ntiles, "tile_blocks": batch.tile_blocks}
     if "eager" in res:
         res["batch_vs_eager"] = round(t_eager / t_batch, 1)
         res["batch_vs_graph"] = round(t_graph / t_batch, 1)

@@ -326,6 +326,23 @@ __device__ __forceinline__ void st16(uint8_t *p, uint64_t blk, uint4 v)
 {
     *reinterpret_cast<uint4 *>(p + 16 * blk) = v;
 }
+/* streaming (non-temporal) variants: every plaintext/ciphertext byte is
+ * touched exactly once */
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 ld16s(const uint8_t *p, uint64_t blk)
+{
+    if (!NT) return ld16(p, blk);
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p + 16 * blk));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+template <bool NT>
+__device__ __forceinline__ void st16s(uint8_t *p, uint64_t blk, uint4 v)
+{
+    if (!NT) return st16(p, blk, v);
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p + 16 * blk));
+}
 
 enum : int { E_ECB = 0, E_CTR = 1, E_CFB_DEC = 2 };
 enum : int { D_ECB = 0, D_CBC = 1, D_CBC_SEG = 2 };
@@ -438,7 +455,7 @@ struct CtrParams {
 
 __device__ __forceinline__ uint32_t te_u(uint32_t idx) { return g_tab.te0[idx & 0xFFu]; } /* uniform lookup */
 
-template <int NR, int B, int THREADS, bool TBL4, bool ISSUE_ALL = true>
+template <int NR, int B, int THREADS, bool TBL4, bool ISSUE_ALL = true, bool NT = false>
 __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_aes_key K)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tbl[TBL4 ? 2 * 256 * 64 : 256 * 64];
@@ -486,7 +503,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_
         for (int b = 0; b < B; ++b) {
             const int64_t i = i0 + 64 * b;
             const bool ok = full || (i >= 0 && (uint64_t)i < P.nfull);
-            x[b] = ok ? ld16(P.in, (uint64_t)i) : make_uint4(0, 0, 0, 0);
+            x[b] = ok ? ld16s<NT>(P.in, (uint64_t)i) : make_uint4(0, 0, 0, 0);
             /* round 1: only T3[byte 15] varies */
             const uint32_t c15 = (b15 | (uint32_t)(64 * b) | lane) ^ (K.rk[3] >> 24);
             if (TBL4) {
@@ -516,8 +533,8 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_
             const int64_t i = i0 + 64 * b;
             const bool ok = full || (i >= 0 && (uint64_t)i < P.nfull);
             if (ok) {
-                st16(P.out, (uint64_t)i,
-                     make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
+                st16s<NT>(P.out, (uint64_t)i,
+                          make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
             } else if (i >= 0 && (uint64_t)i == P.nfull && P.tail) {
                 const uint32_t ks[4] = {s[b][0], s[b][1], s[b][2], s[b][3]};
                 for (uint32_t n = 0; n < P.tail; ++n)
@@ -853,8 +870,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_batch_tt(BatchParams P)
 }
 
 constexpr int BATCH_THREADS = 1024;
-constexpr int BATCH_B = 4;
-static_assert(64 * BATCH_B == OTC_BATCH_TILE_BLOCKS, "tile size must match otc.h");
+static_assert(64 * 4 == OTC_BATCH_TILE_BLOCKS, "largest tile must match otc.h");
 
 /* ---------------------------------------------------------------------------
  * Host-side launch helpers
@@ -966,13 +982,24 @@ hipError_t launch_seg_nr(const CbcSegParams &P, const otc_aes_key &K, hipStream_
     return hipGetLastError();
 }
 
-template <int NR>
-hipError_t launch_ctr_batch_nr(const BatchParams &P, hipStream_t st)
+template <int NR, int B>
+hipError_t launch_ctr_batch_nrb(const BatchParams &P, hipStream_t st)
 {
     /* one workgroup per CU (128 KiB LDS), 16 tiles per workgroup step */
     const int grid = grid_for(P.ntiles, BATCH_THREADS / 64, 1);
-    hipLaunchKernelGGL((k_aes_ctr_batch_tt<NR, BATCH_B, BATCH_THREADS>), dim3(grid), dim3(BATCH_THREADS), 0, st, P);
+    hipLaunchKernelGGL((k_aes_ctr_batch_tt<NR, B, BATCH_THREADS>), dim3(grid), dim3(BATCH_THREADS), 0, st, P);
     return hipGetLastError();
+}
+
+template <int NR>
+hipError_t launch_ctr_batch_nr(const BatchParams &P, int tile_blocks, hipStream_t st)
+{
+    switch (tile_blocks) {
+    case 64: return launch_ctr_batch_nrb<NR, 1>(P, st);
+    case 128: return launch_ctr_batch_nrb<NR, 2>(P, st);
+    case 256: return launch_ctr_batch_nrb<NR, 4>(P, st);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 } // namespace
@@ -981,13 +1008,13 @@ hipError_t launch_ctr_batch_nr(const BatchParams &P, hipStream_t st)
 namespace otc_impl {
 
 hipError_t tt_ctr_batch(const otc_ctr_msg *msgs, const otc_aes_key *keys, const uint32_t *tile_msg,
-                        const uint64_t *tile_first, uint64_t ntiles, int nr, hipStream_t st)
+                        const uint64_t *tile_first, uint64_t ntiles, int tile_blocks, int nr, hipStream_t st)
 {
     BatchParams P{msgs, keys, tile_msg, tile_first, ntiles};
     switch (nr) {
-    case 10: return launch_ctr_batch_nr<10>(P, st);
-    case 12: return launch_ctr_batch_nr<12>(P, st);
-    case 14: return launch_ctr_batch_nr<14>(P, st);
+    case 10: return launch_ctr_batch_nr<10>(P, tile_blocks, st);
+    case 12: return launch_ctr_batch_nr<12>(P, tile_blocks, st);
+    case 14: return launch_ctr_batch_nr<14>(P, tile_blocks, st);
     default: return hipErrorInvalidValue;
     }
 }
@@ -1003,7 +1030,7 @@ hipError_t tt_ecb_encrypt(const void *in, void *out, uint64_t nblocks, const otc
 
 int g_tt_wg_per_cu = 2; /* lowered to 1 while a co-resident bitsliced kernel runs (hybrid impl) */
 
-template <int NR, int T, int B, bool TBL4 = false, bool ISSUE_ALL = true>
+template <int NR, int T, int B, bool TBL4 = false, bool ISSUE_ALL = true, bool NT = false>
 hipError_t launch_ctr_cached_tb(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo, hipStream_t st)
 {
     constexpr uint64_t PER = (uint64_t)T * B;
@@ -1011,7 +1038,7 @@ hipError_t launch_ctr_cached_tb(CtrParams P, const otc_aes_key &K, uint64_t ctr_
     P.cbase.lo = ctr_lo - P.shift;
     const uint64_t vt = P.nfull + (P.tail ? 1 : 0) + P.shift;
     int grid = grid_for(vt, PER, TBL4 ? 1 : g_tt_wg_per_cu);
-    hipLaunchKernelGGL((k_aes_ctr_tt_cached<NR, B, T, TBL4, ISSUE_ALL>), dim3(grid), dim3(T), 0, st, P, K);
+    hipLaunchKernelGGL((k_aes_ctr_tt_cached<NR, B, T, TBL4, ISSUE_ALL, NT>), dim3(grid), dim3(T), 0, st, P, K);
     return hipGetLastError();
 }
 
@@ -1021,6 +1048,9 @@ hipError_t launch_ctr_cached(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo,
     /* OTC_TT_VARIANT=<threads>x<B>: negative threads = 1-table layout (A/B
      * measurements); default = 4-table layout, 1024 threads x 4 blocks/lane */
     const TTVariant v = tt_variant();
+    /* OTC_TT_NT=1: non-temporal plaintext loads / ciphertext stores (A/B) */
+    static const bool nt = getenv("OTC_TT_NT") && atoi(getenv("OTC_TT_NT")) != 0;
+    if (nt) return launch_ctr_cached_tb<NR, 1024, 4, true, true, true>(P, K, ctr_lo, st);
     if (v.threads == 1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, true>(P, K, ctr_lo, st);
     if (v.threads == 2 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, true, false>(P, K, ctr_lo, st);
     if (v.threads == 512 && v.b == 4) return launch_ctr_cached_tb<NR, 512, 4, true>(P, K, ctr_lo, st);

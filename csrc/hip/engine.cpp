@@ -47,7 +47,7 @@ hipError_t tt_cbc_decrypt_seg(const void *, void *, uint64_t, uint64_t, const ot
 hipError_t tt_cbc_encrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
 hipError_t bs_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
-hipError_t tt_ctr_batch(const otc_ctr_msg *, const otc_aes_key *, const uint32_t *, const uint64_t *, uint64_t, int,
+hipError_t tt_ctr_batch(const otc_ctr_msg *, const otc_aes_key *, const uint32_t *, const uint64_t *, uint64_t, int, int,
                         hipStream_t);
 void tt_set_wg_per_cu(int);
 hipError_t k_xor(const void *, const void *, void *, size_t, hipStream_t);
@@ -297,10 +297,11 @@ extern "C" int otc_aes_ctr_rfc3686(const void *in, void *out, size_t nbytes, con
     return ctr_common(in, out, nbytes, k, ctr_add(ctr_from_bytes(cb), block_offset, true), true, impl, stream);
 }
 
-extern "C" uint64_t otc_ctr_batch_plan(const otc_ctr_msg *msgs, size_t nmsg, uint32_t *tile_msg,
+extern "C" uint64_t otc_ctr_batch_plan(const otc_ctr_msg *msgs, size_t nmsg, int tile_blocks, uint32_t *tile_msg,
                                        uint64_t *tile_first)
 {
-    const uint64_t tile_bytes = 16ull * OTC_BATCH_TILE_BLOCKS;
+    if (tile_blocks != 64 && tile_blocks != 128 && tile_blocks != 256) return 0;
+    const uint64_t tile_bytes = 16ull * (uint64_t)tile_blocks;
     uint64_t t = 0;
     for (size_t m = 0; m < nmsg; ++m) {
         const uint64_t nt = (msgs[m].nbytes + tile_bytes - 1) / tile_bytes;
@@ -316,15 +317,18 @@ extern "C" uint64_t otc_ctr_batch_plan(const otc_ctr_msg *msgs, size_t nmsg, uin
  * overlap) are the planner's job on the host (our_tree_amd.ops.CtrBatch);
  * here only the launch arguments are validated. */
 extern "C" int otc_aes_ctr_batch(const otc_ctr_msg *msgs, const otc_aes_key *keys, const uint32_t *tile_msg,
-                                 const uint64_t *tile_first, uint64_t ntiles, int nr, void *stream)
+                                 const uint64_t *tile_first, uint64_t ntiles, int tile_blocks, int nr, void *stream)
 {
     Range rg("otc_aes_ctr_batch");
+    if (tile_blocks != 64 && tile_blocks != 128 && tile_blocks != 256)
+        return set_err(OTC_ERR_ARG, "ctr_batch: tile_blocks must be 64, 128 or 256");
     if (ntiles == 0) return OTC_OK;
     if (!msgs || !keys || !tile_msg || !tile_first) return set_err(OTC_ERR_ARG, "ctr_batch: null array");
     if (nr != 10 && nr != 12 && nr != 14) return set_err(OTC_ERR_ARG, "ctr_batch: nr must be 10, 12 or 14");
     if ((((uintptr_t)msgs) | ((uintptr_t)keys) | ((uintptr_t)tile_first)) & 7u || ((uintptr_t)tile_msg & 3u))
         return set_err(OTC_ERR_ARG, "ctr_batch: misaligned descriptor arrays");
-    hipError_t e = otc_impl::tt_ctr_batch(msgs, keys, tile_msg, tile_first, ntiles, nr, (hipStream_t)stream);
+    hipError_t e = otc_impl::tt_ctr_batch(msgs, keys, tile_msg, tile_first, ntiles, tile_blocks, nr,
+                                          (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "ctr_batch launch");
     return OTC_OK;
 }

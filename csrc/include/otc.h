@@ -108,8 +108,9 @@ int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_a
  * The serving shape (packets, sectors, objects of a few KiB, each with its own
  * key and counter): one launch per message is launch-bound (µs each) and far
  * from the >> 256 workgroups the chip needs.  Here the work unit is a tile of
- * OTC_BATCH_TILE_BLOCKS 16-byte blocks of one message; every array below is
- * DEVICE memory:
+ * `tile_blocks` 16-byte blocks of one message (64, 128 or 256 = one wave x 1,
+ * 2 or 4 blocks per lane: small messages waste less of a small tile, large
+ * tiles hide more LDS latency); every array below is DEVICE memory:
  *   msgs[m]        message descriptor (device addresses, length, key index,
  *                  initial 128-bit big-endian counter as two numeric halves)
  *   keys[k]        expanded encryption keys (all with `nr` rounds)
@@ -117,7 +118,7 @@ int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_a
  *   tile_first[m]  first tile of message m    }
  * in == out (in place) is allowed per message; distinct messages must not
  * overlap.  Messages of 0 bytes have no tiles. */
-#define OTC_BATCH_TILE_BLOCKS 256
+#define OTC_BATCH_TILE_BLOCKS 256 /* default and largest tile */
 typedef struct {
     uint64_t in;      /* device address of the input */
     uint64_t out;     /* device address of the output */
@@ -130,10 +131,11 @@ typedef struct {
 
 /* Host planner: fills tile_msg (may be NULL to only count) and tile_first for
  * host copies of the descriptors; returns the number of tiles. */
-uint64_t otc_ctr_batch_plan(const otc_ctr_msg *msgs, size_t nmsg, uint32_t *tile_msg, uint64_t *tile_first);
+uint64_t otc_ctr_batch_plan(const otc_ctr_msg *msgs, size_t nmsg, int tile_blocks, uint32_t *tile_msg,
+                            uint64_t *tile_first);
 
 int otc_aes_ctr_batch(const otc_ctr_msg *msgs, const otc_aes_key *keys, const uint32_t *tile_msg,
-                      const uint64_t *tile_first, uint64_t ntiles, int nr, void *stream);
+                      const uint64_t *tile_first, uint64_t ntiles, int tile_blocks, int nr, void *stream);
 
 /* out = a ^ b (the device arc4_crypt combiner). */
 int otc_xor(const void *a, const void *b, void *out, size_t nbytes, void *stream);

@@ -104,7 +104,22 @@ def ctr(x: torch.Tensor, key: bytes, counter: bytes, out: torch.Tensor | None = 
     return out
 
 
-BATCH_TILE_BYTES = 16 * 256  # OTC_BATCH_TILE_BLOCKS (otc.h)
+BATCH_TILES = (256, 128, 64)  # tile sizes in blocks the batch kernel supports (otc.h)
+# relative cost per tile block slot, measured on MI355X with 16384 x 4 KiB
+# messages (960 / 946 / 910 GB/s at 256 / 128 / 64 blocks per tile,
+# profiles/r1/batch_ctr_tiles.jsonl): fewer blocks per lane hide less LDS latency
+BATCH_TILE_COST = {256: 1.0, 128: 1.015, 64: 1.055}
+
+
+def _pick_tile(nbytes) -> int:
+    """Tile size minimising (tile slots issued) x (cost per slot)."""
+    best, best_cost = 256, None
+    for t in BATCH_TILES:
+        slots = int(((nbytes + 16 * t - 1) // (16 * t)).sum()) * t
+        cost = slots * BATCH_TILE_COST[t]
+        if best_cost is None or cost < best_cost:
+            best, best_cost = t, cost
+    return best
 
 
 class CtrBatch:
@@ -124,11 +139,12 @@ class CtrBatch:
     xs / outs: GPU tensors (contiguous, 16-byte aligned; ``outs[i] is xs[i]``
     for in place); keys: AES keys (16/24/32 bytes) selected per message by
     ``key_index`` (default: keys[i] for message i); counters: the 16-byte
-    initial counter block of every message (128-bit big-endian increment).
-    Distinct messages must not overlap.
+    initial counter block of every message (128-bit big-endian increment);
+    tile_blocks: 64 / 128 / 256 blocks per tile (default: picked from the
+    message sizes).  Distinct messages must not overlap.
     """
 
-    def __init__(self, xs, keys, counters, outs=None, key_index=None):
+    def __init__(self, xs, keys, counters, outs=None, key_index=None, tile_blocks=None):
         import numpy as np
 
         n = len(xs)
@@ -171,6 +187,12 @@ class CtrBatch:
             desc[i, :5] = (pi, po, nb, int.from_bytes(c[:8], "big"), int.from_bytes(c[8:], "big"))
         desc[:, 5] = kidx.astype(np.uint64)
 
+        if tile_blocks is None:
+            tile_blocks = _pick_tile(desc[:, 2])
+        if tile_blocks not in BATCH_TILES:
+            raise ValueError(f"tile_blocks must be one of {BATCH_TILES}")
+        self.tile_blocks = tile_blocks
+        tile_bytes = 16 * tile_blocks
         ek = [expand_key(k) for k in keys]
         key_blob = b"".join(bytes(k) for k in ek)  # otc_aes_key[] (256 B each)
         nr_msg = np.array([k.nr for k in ek], dtype=np.int64)[kidx]
@@ -192,7 +214,7 @@ class CtrBatch:
             if not len(sel):
                 continue
             d = desc[sel]
-            tiles = (d[:, 2] + (BATCH_TILE_BYTES - 1)) // BATCH_TILE_BYTES
+            tiles = (d[:, 2] + (tile_bytes - 1)) // tile_bytes
             ntiles = int(tiles.sum())
             if ntiles == 0:
                 continue
@@ -219,15 +241,15 @@ class CtrBatch:
         lib = _lib()
         with torch.cuda.device(self.device):
             for o_desc, o_first, o_map, ntiles, nr in self._launches:
-                rc = lib.otc_aes_ctr_batch(base + o_desc, base, base + o_map, base + o_first, ntiles, nr,
-                                           ctypes.c_void_p(st.cuda_stream))
+                rc = lib.otc_aes_ctr_batch(base + o_desc, base, base + o_map, base + o_first, ntiles,
+                                           self.tile_blocks, nr, ctypes.c_void_p(st.cuda_stream))
                 _native.check(rc, "otc_aes_ctr_batch")
         return self.outs
 
 
-def ctr_batch(xs, keys, counters, outs=None, key_index=None):
+def ctr_batch(xs, keys, counters, outs=None, key_index=None, tile_blocks=None):
     """Plan and run a ``CtrBatch`` once."""
-    return CtrBatch(xs, keys, counters, outs=outs, key_index=key_index).run()
+    return CtrBatch(xs, keys, counters, outs=outs, key_index=key_index, tile_blocks=tile_blocks).run()
 
 
 def ctr_rfc3686(x: torch.Tensor, key: bytes, nonce: bytes, ivec: bytes, out=None, block_offset: int = 0,

@@ -153,27 +153,35 @@ def test_ctr_batch_planner_and_python_plan_agree(lib):
     builds with numpy: 4 KiB tiles, empty messages own none."""
     import numpy as np
 
-    sizes = [0, 1, 4096, 4097, 16, 0, 3 * 4096 + 15, 100000]
+    from our_tree_amd.ops import aes_ops
+
+    sizes = [0, 1, 4096, 4097, 16, 0, 3 * 4096 + 15, 100000, 1504]
     msgs = (CtrMsg * len(sizes))(*[CtrMsg(0, 0, n, 0, 0, 0, 0) for n in sizes])
     fn = lib.otc_ctr_batch_plan
     fn.restype = ctypes.c_uint64
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
-    nt = fn(msgs, len(sizes), None, None)
-    tmap = np.zeros(nt, np.uint32)
-    first = np.zeros(len(sizes), np.uint64)
-    assert fn(msgs, len(sizes), tmap.ctypes.data, first.ctypes.data) == nt
-    tiles = (np.array(sizes, np.uint64) + 4095) // 4096
-    assert nt == tiles.sum()
-    assert (tmap == np.repeat(np.arange(len(sizes), dtype=np.uint32), tiles.astype(np.int64))).all()
-    assert first[0] == 0 and (first[1:] == np.cumsum(tiles)[:-1]).all()
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    for tb in (64, 128, 256):
+        nt = fn(msgs, len(sizes), tb, None, None)
+        tmap = np.zeros(nt, np.uint32)
+        first = np.zeros(len(sizes), np.uint64)
+        assert fn(msgs, len(sizes), tb, tmap.ctypes.data, first.ctypes.data) == nt
+        tiles = (np.array(sizes, np.uint64) + 16 * tb - 1) // (16 * tb)
+        assert nt == tiles.sum()
+        assert (tmap == np.repeat(np.arange(len(sizes), dtype=np.uint32), tiles.astype(np.int64))).all()
+        assert first[0] == 0 and (first[1:] == np.cumsum(tiles)[:-1]).all()
+    assert fn(msgs, len(sizes), 100, None, None) == 0
+    # tile choice: 4 KiB messages fill 256-block tiles exactly, 1 KiB ones 64-block tiles
+    assert aes_ops._pick_tile(np.full(100, 4096, np.uint64)) == 256
+    assert aes_ops._pick_tile(np.full(100, 1024, np.uint64)) == 64
 
 
 def test_ctr_batch_rejects_bad_launch_args(lib):
     f = lib.otc_aes_ctr_batch
-    assert f(A, A, A, A, 0, 10, None) == 0  # nothing to do
-    assert f(None, A, A, A, 4, 10, None) == ERR_ARG and "null" in err(lib)
-    assert f(A, A, A, A, 4, 11, None) == ERR_ARG and "nr" in err(lib)
-    assert f(A + 4, A, A, A, 4, 10, None) == ERR_ARG and "misaligned" in err(lib)
+    assert f(A, A, A, A, 0, 256, 10, None) == 0  # nothing to do
+    assert f(None, A, A, A, 4, 256, 10, None) == ERR_ARG and "null" in err(lib)
+    assert f(A, A, A, A, 4, 256, 11, None) == ERR_ARG and "nr" in err(lib)
+    assert f(A, A, A, A, 4, 100, 10, None) == ERR_ARG and "tile_blocks" in err(lib)
+    assert f(A + 4, A, A, A, 4, 64, 10, None) == ERR_ARG and "misaligned" in err(lib)
 
 
 def test_ctr_batch_python_validation_without_gpu():

@@ -21,9 +21,11 @@ def _messages(dev, sizes, seed):
     return [torch.randint(0, 256, (n,), dtype=torch.uint8, generator=g).to(dev) for n in sizes]
 
 
-def test_ctr_batch_matches_oracle(gpu):
+@pytest.mark.parametrize("tile_blocks", [64, 128, 256])
+def test_ctr_batch_matches_oracle(gpu, tile_blocks):
     """Odd lengths (tails), empty messages, mixed AES-128/192/256 keys shared
-    between messages, counters at the 2^64 carry and the 2^128 wrap."""
+    between messages, counters at the 2^64 carry and the 2^128 wrap, every
+    tile size."""
     rng = np.random.default_rng(5)
     sizes = [0, 1, 15, 16, 17, 4095, 4096, 4097, 65541, 300000] + [int(v) for v in rng.integers(0, 20000, 120)]
     keys = [os.urandom(b) for b in (16, 24, 32) for _ in range(4)]
@@ -32,7 +34,7 @@ def test_ctr_batch_matches_oracle(gpu):
     ctrs[3] = os.urandom(8) + (2**64 - 3).to_bytes(8, "big")
     ctrs[8] = b"\xff" * 16
     xs = _messages(gpu, sizes, 1)
-    outs = ops.ctr_batch(xs, keys, ctrs, key_index=kidx)
+    outs = ops.ctr_batch(xs, keys, ctrs, key_index=kidx, tile_blocks=tile_blocks)
     torch.cuda.synchronize()
     for i, (x, y) in enumerate(zip(xs, outs)):
         assert host(y) == cpu_ref.ctr(keys[kidx[i]], ctrs[i], host(x)), f"message {i} ({sizes[i]} bytes)"
