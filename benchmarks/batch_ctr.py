@@ -86,6 +86,13 @@ def main():
     t_batch = timed(batch.run, args.iters)
     res["batch"] = {"ms": round(t_batch * 1e3, 3), "msgs_per_s": round(n / t_batch), "gbps": round(n * size / t_batch / 1e9, 3),
                     "plan_ms": round(t_plan * 1e3, 3), "tiles": batch.ntiles, "tile_blocks": batch.tile_blocks}
+    # the same messages described as one packed buffer: vectorised planning
+    t0 = time.perf_counter()
+    packed = ops.CtrBatch.packed(src, [size] * n, keys, ctrs, out=dst, key_index=kidx, tile_blocks=args.tile)
+    t_plan_p = time.perf_counter() - t0
+    t_packed = timed(packed.run, args.iters)
+    res["batch_packed"] = {"ms": round(t_packed * 1e3, 3), "gbps": round(n * size / t_packed / 1e9, 3),
+                           "plan_ms": round(t_plan_p * 1e3, 3)}
     if "eager" in res:
         res["batch_vs_eager"] = round(t_eager / t_batch, 1)
         res["batch_vs_graph"] = round(t_graph / t_batch, 1)

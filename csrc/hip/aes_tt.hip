@@ -815,6 +815,26 @@ __device__ __forceinline__ uint64_t ufl64(uint64_t v)
     return ((uint64_t)ufl((uint32_t)(v >> 32)) << 32) | ufl((uint32_t)v);
 }
 
+/* load through the constant address space (wave-uniform address -> s_load) */
+typedef const __attribute__((address_space(4))) uint32_t *cptr32;
+typedef const __attribute__((address_space(4))) uint64_t *cptr64;
+__device__ __forceinline__ uint32_t cld32(const uint32_t *p) { return *(cptr32)p; }
+__device__ __forceinline__ uint64_t cld64(const uint64_t *p) { return *(cptr64)p; }
+/* message buffers come from descriptors as plain addresses: access them as
+ * GLOBAL memory, or hipcc emits flat_* ops, which count against lgkmcnt and
+ * make every LDS wait also wait for HBM */
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+__device__ __forceinline__ uint4 gld16(const uint8_t *p, uint64_t blk)
+{
+    const u32x4 v = *(const g_u32x4 *)(p + 16 * blk);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gst16(uint8_t *p, uint64_t blk, uint4 v)
+{
+    *(g_u32x4 *)(p + 16 * blk) = u32x4{v.x, v.y, v.z, v.w};
+}
+
 template <int NR, int B, int THREADS>
 __global__ __launch_bounds__(THREADS) void k_aes_ctr_batch_tt(BatchParams P)
 {
@@ -830,19 +850,22 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_batch_tt(BatchParams P)
     constexpr uint64_t TILE = 64u * B;
 
     for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < P.ntiles; t += (uint64_t)gridDim.x * WAVES) {
-        const uint32_t m = ufl(P.tile_msg[t]);
-        const otc_ctr_msg *D = P.msgs + m;
-        const uint8_t *in = (const uint8_t *)ufl64(D->in);
-        uint8_t *out = (uint8_t *)ufl64(D->out);
-        const uint64_t nbytes = ufl64(D->nbytes);
-        const Ctr128 c = {ufl64(D->ctr_hi), ufl64(D->ctr_lo)};
-        const otc_aes_key *Kg = P.keys + ufl(D->key);
+        /* descriptor, tile base and round keys through the constant address
+         * space: wave-uniform addresses -> scalar loads (s_load_dwordx*) into
+         * SGPRs, no VGPRs and no per-lane memory traffic */
+        const uint32_t m = cld32(P.tile_msg + t);
+        const uint64_t *D = (const uint64_t *)(P.msgs + m);
+        const uint8_t *in = (const uint8_t *)cld64(D + 0);
+        uint8_t *out = (uint8_t *)cld64(D + 1);
+        const uint64_t nbytes = cld64(D + 2);
+        const Ctr128 c = {cld64(D + 3), cld64(D + 4)};
+        const uint32_t *Kg = P.keys[0].rk + (sizeof(otc_aes_key) / 4) * (uint32_t)cld64(D + 5);
         otc_aes_key K;
 #pragma unroll
-        for (int q = 0; q < 4 * (NR + 1); ++q) K.rk[q] = ufl(Kg->rk[q]);
+        for (int q = 0; q < 4 * (NR + 1); ++q) K.rk[q] = cld32(Kg + q);
         const uint64_t nfull = nbytes >> 4;
         const uint32_t tail = (uint32_t)(nbytes & 15u);
-        const uint64_t i0 = (t - ufl64(P.tile_first[m])) * TILE + lane;
+        const uint64_t i0 = (t - cld64(P.tile_first + m)) * TILE + lane;
 
         uint32_t s[B][4];
         uint4 x[B];
@@ -850,7 +873,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_batch_tt(BatchParams P)
         for (int b = 0; b < B; ++b) {
             const uint64_t i = i0 + 64u * b;
             ctr_words(c, i, false, s[b][0], s[b][1], s[b][2], s[b][3]);
-            x[b] = i < nfull ? ld16(in, i) : make_uint4(0, 0, 0, 0);
+            x[b] = i < nfull ? gld16(in, i) : make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int j = 0; j < 4; ++j) s[b][j] ^= K.rk[j];
         }
@@ -859,11 +882,13 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_batch_tt(BatchParams P)
         for (int b = 0; b < B; ++b) {
             const uint64_t i = i0 + 64u * b;
             if (i < nfull) {
-                st16(out, i, make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
+                gst16(out, i, make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
             } else if (i == nfull && tail) {
                 const uint32_t ks[4] = {s[b][0], s[b][1], s[b][2], s[b][3]};
+                const g_u8 *gi = (const g_u8 *)in;
+                g_u8 *go = (g_u8 *)out;
                 for (uint32_t n = 0; n < tail; ++n)
-                    out[16 * i + n] = in[16 * i + n] ^ (uint8_t)(ks[n >> 2] >> (8 * (n & 3)));
+                    go[16 * i + n] = gi[16 * i + n] ^ (uint8_t)(ks[n >> 2] >> (8 * (n & 3)));
             }
         }
     }

@@ -165,6 +165,7 @@ class CtrBatch:
         self._keep = list(xs)  # descriptors hold raw addresses: keep the tensors alive
         self._launches = []
         self.device = xs[0].device if n else None
+        self.ntiles, self.tile_blocks = 0, tile_blocks or 256
         if n == 0:
             return
         desc = np.zeros((n, 6), dtype=np.uint64)  # in, out, nbytes, ctr_hi, ctr_lo, key
@@ -186,6 +187,90 @@ class CtrBatch:
                 raise ValueError(f"counters[{i}] must be 16 bytes")
             desc[i, :5] = (pi, po, nb, int.from_bytes(c[:8], "big"), int.from_bytes(c[8:], "big"))
         desc[:, 5] = kidx.astype(np.uint64)
+
+        self._build(desc, keys, kidx, tile_blocks)
+
+    @classmethod
+    def packed(cls, buf: torch.Tensor, lengths, keys, counters, out: torch.Tensor | None = None, offsets=None,
+               key_index=None, tile_blocks=None) -> "CtrBatch":
+        """Messages packed in ONE device buffer (the usual serving layout):
+        message i is ``buf[offsets[i] : offsets[i] + lengths[i]]`` (offsets
+        default to back-to-back 16-byte aligned slots) and lands at the same
+        offset of ``out`` (default: a new buffer; ``out is buf`` for in
+        place).  counters: (n, 16) uint8 array / tensor or a list of 16-byte
+        blocks.  Planning is vectorised (no per-message Python work); the
+        outputs are ``self.out``."""
+        import numpy as np
+
+        nb = _nbytes(buf)
+        lens = np.asarray(lengths, dtype=np.int64).reshape(-1)
+        n = lens.size
+        if offsets is None:
+            offs = np.zeros(n, dtype=np.int64)
+            if n > 1:
+                offs[1:] = np.cumsum((lens[:-1] + 15) // 16 * 16)
+        else:
+            offs = np.asarray(offsets, dtype=np.int64).reshape(-1)
+        if offs.size != n:
+            raise ValueError("one offset per message")
+        if n and ((lens < 0).any() or (offs < 0).any() or (offs + lens > nb).any()):
+            raise ValueError("messages must lie inside the buffer")
+        if n and (offs % 16).any():
+            raise ValueError("message offsets must be multiples of 16")
+        nz = np.nonzero(lens)[0]  # disjoint messages (empty ones occupy nothing)
+        if nz.size > 1:
+            so, sl = offs[nz], lens[nz]
+            o = np.argsort(so, kind="stable")
+            if ((so[o][:-1] + sl[o][:-1]) > so[o][1:]).any():
+                raise ValueError("messages overlap")
+        ctr = counters.cpu().numpy() if isinstance(counters, torch.Tensor) else counters
+        if isinstance(ctr, np.ndarray):
+            c = np.ascontiguousarray(ctr, dtype=np.uint8).reshape(-1, 16)
+        else:
+            if len(ctr) != n or any(len(bytes(x)) != 16 for x in ctr):
+                raise ValueError("one 16-byte counter per message")
+            c = np.frombuffer(b"".join(bytes(x) for x in ctr), dtype=np.uint8).reshape(-1, 16)
+        if c.shape[0] != n:
+            raise ValueError("one 16-byte counter per message")
+        if key_index is None:
+            if len(keys) != n:
+                raise ValueError("one key per message, or pass key_index")
+            kidx = np.arange(n, dtype=np.int64)
+        else:
+            kidx = np.asarray(key_index, dtype=np.int64).reshape(-1)
+            if kidx.size != n:
+                raise ValueError("one key index per message")
+        if n and (kidx.min() < 0 or kidx.max() >= len(keys)):
+            raise ValueError("key_index out of range")
+        _check_dev(buf, "buf")
+        out = _out_like(buf, out)
+        pi, po = buf.data_ptr(), out.data_ptr()
+        if (pi | po) % 16:
+            raise ValueError("buf / out must be 16-byte aligned")
+        if pi != po and pi < po + nb and po < pi + nb:
+            raise ValueError("buf and out overlap partially")
+        self = cls.__new__(cls)
+        self.out = out
+        self.outs = [out]
+        self._keep = [buf]
+        self._launches = []
+        self.device = buf.device
+        if n == 0:
+            self.ntiles, self.tile_blocks = 0, tile_blocks or 256
+            return self
+        desc = np.zeros((n, 6), dtype=np.uint64)
+        desc[:, 0] = np.uint64(pi) + offs.astype(np.uint64)
+        desc[:, 1] = np.uint64(po) + offs.astype(np.uint64)
+        desc[:, 2] = lens.astype(np.uint64)
+        desc[:, 3] = c[:, :8].copy().view(">u8").reshape(-1).astype(np.uint64)
+        desc[:, 4] = c[:, 8:].copy().view(">u8").reshape(-1).astype(np.uint64)
+        desc[:, 5] = kidx.astype(np.uint64)
+        self._build(desc, keys, kidx, tile_blocks)
+        return self
+
+    def _build(self, desc, keys, kidx, tile_blocks):
+        """Tile map + key schedules + descriptors -> one pinned upload."""
+        import numpy as np
 
         if tile_blocks is None:
             tile_blocks = _pick_tile(desc[:, 2])

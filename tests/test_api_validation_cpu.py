@@ -196,3 +196,25 @@ def test_ctr_batch_python_validation_without_gpu():
         ops.CtrBatch([x], [bytes(16)], [bytes(16)])
     with pytest.raises(ValueError, match="key_index"):
         ops.CtrBatch([x], [bytes(16)], [bytes(16)], key_index=[3])
+
+
+def test_packed_batch_validation_without_gpu():
+    """Packed-buffer planning rejects bad layouts before touching a device."""
+    import torch
+
+    from our_tree_amd import ops
+
+    buf = torch.zeros(4096, dtype=torch.uint8)
+    k, c = [bytes(16)], [bytes(16)] * 2
+    with pytest.raises(ValueError, match="inside the buffer"):
+        ops.CtrBatch.packed(buf, [4000, 200], k, c, key_index=[0, 0])
+    with pytest.raises(ValueError, match="multiples of 16"):
+        ops.CtrBatch.packed(buf, [10, 10], k, c, offsets=[0, 24], key_index=[0, 0])
+    with pytest.raises(ValueError, match="overlap"):
+        ops.CtrBatch.packed(buf, [100, 100], k, c, offsets=[0, 64], key_index=[0, 0])
+    with pytest.raises(ValueError, match="16-byte counter"):
+        ops.CtrBatch.packed(buf, [100, 100], k, [bytes(16)], key_index=[0, 0])
+    with pytest.raises(ValueError, match="key_index"):
+        ops.CtrBatch.packed(buf, [100, 100], k, c, key_index=[0, 1])
+    with pytest.raises(ValueError, match="GPU tensor"):  # layout valid: only the device is wrong
+        ops.CtrBatch.packed(buf, [100, 100], k, c, key_index=[0, 0])

@@ -40,6 +40,37 @@ def test_ctr_batch_matches_oracle(gpu, tile_blocks):
         assert host(y) == cpu_ref.ctr(keys[kidx[i]], ctrs[i], host(x)), f"message {i} ({sizes[i]} bytes)"
 
 
+def test_packed_batch_matches_oracle(gpu):
+    """Messages packed in one buffer (default back-to-back 16-byte slots and
+    explicit offsets), counters as an (n, 16) array, in place and out of place."""
+    rng = np.random.default_rng(9)
+    lens = [int(v) for v in rng.integers(0, 9000, 300)] + [0, 1, 4096]
+    slots = [(n + 15) // 16 * 16 for n in lens]
+    buf = _messages(gpu, [sum(slots)], 10)[0]
+    keys = [os.urandom(16), os.urandom(32)]
+    kidx = [i % 2 for i in range(len(lens))]
+    ctrs = rng.integers(0, 256, (len(lens), 16), dtype=np.uint8)
+    ctrs[5, 8:] = 0xFF  # 2^64 carry
+    src = host(buf)
+    b = ops.CtrBatch.packed(buf, lens, keys, ctrs, key_index=kidx)
+    b.run()
+    torch.cuda.synchronize()
+    got, off = host(b.out), 0
+    for i, n in enumerate(lens):
+        assert got[off:off + n] == cpu_ref.ctr(keys[kidx[i]], ctrs[i].tobytes(), src[off:off + n]), f"message {i}"
+        off += slots[i]
+    # explicit offsets, reversed order, in place
+    offs = np.cumsum([0] + slots[:-1])[::-1].copy()
+    lens_r = lens[::-1]
+    b2 = ops.CtrBatch.packed(buf, lens_r, keys, ctrs[::-1], out=buf, offsets=offs, key_index=kidx[::-1])
+    b2.run()
+    torch.cuda.synchronize()
+    got = host(buf)
+    for j, n in enumerate(lens_r):
+        o = int(offs[j])
+        assert got[o:o + n] == cpu_ref.ctr(keys[kidx[::-1][j]], ctrs[::-1][j].tobytes(), src[o:o + n])
+
+
 def test_ctr_batch_in_place_replay(gpu):
     """in == out, planned once and run twice: CTR twice is the identity."""
     sizes = [4096 * 3, 1000, 8192 + 48]
