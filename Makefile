@@ -19,7 +19,7 @@ CXX     ?= g++
 INC      := -Icsrc/include -Icsrc/hip
 CFLAGS   ?= -O2 -g -Wall -Wextra -std=gnu99 -fPIC
 CXXFLAGS ?= -O2 -g -Wall -std=c++17 -fPIC
-HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wno-unused-result
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 SANLD :=
 ifeq ($(SAN),1)
 CFLAGS   += -fsanitize=address,undefined -fno-omit-frame-pointer

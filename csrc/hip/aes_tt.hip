@@ -810,10 +810,6 @@ struct BatchParams {
 };
 
 __device__ __forceinline__ uint32_t ufl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ uint64_t ufl64(uint64_t v)
-{
-    return ((uint64_t)ufl((uint32_t)(v >> 32)) << 32) | ufl((uint32_t)v);
-}
 
 /* load through the constant address space (wave-uniform address -> s_load) */
 typedef const __attribute__((address_space(4))) uint32_t *cptr32;

@@ -102,12 +102,6 @@ Ctr128 ctr_add(Ctr128 c, uint64_t n, bool wrap64)
     return c;
 }
 
-void ctr_to_bytes(Ctr128 c, uint8_t out[16])
-{
-    for (int i = 0; i < 8; ++i) out[i] = (uint8_t)(c.hi >> (56 - 8 * i));
-    for (int i = 0; i < 8; ++i) out[8 + i] = (uint8_t)(c.lo >> (56 - 8 * i));
-}
-
 int pick_impl(int impl, int bits)
 {
     if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_HYBRID) return impl;
