@@ -118,3 +118,18 @@ def test_cpp_blockcipher_interface(gpu):
         pytest.fail("bin/bc_test not built (make)")
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "bc_test: OK" in r.stdout, r.stdout + r.stderr
+
+
+def test_cli_gpu_selftest_and_file_job(gpu, tmp_path):
+    """`python -m our_tree_amd` (in process): GPU known-answer vectors and a
+    resumable file job through the pinned GPU pipeline, CTR twice = identity."""
+    from our_tree_amd.__main__ import main
+
+    assert main(["selftest", "--gpu"]) == 0
+    src, mid, back = tmp_path / "a.bin", tmp_path / "b.bin", tmp_path / "c.bin"
+    data = os.urandom(300_007)
+    src.write_bytes(data)
+    for s, d in ((src, mid), (mid, back)):
+        assert main(["crypt", str(s), str(d), "--key", "22" * 16, "--iv", "ff" * 16, "--chunk", "64K"]) == 0
+    assert mid.read_bytes() == cpu_ref.ctr(b"\x22" * 16, b"\xff" * 16, data)
+    assert back.read_bytes() == data
