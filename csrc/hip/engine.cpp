@@ -970,6 +970,10 @@ static int rccl_job_init(RcclJob &J, int ngpus, size_t S)
 std::mutex g_rccl_mu;
 RcclJob *g_rccl = nullptr;
 
+/* strategy 0 (direct ingest): one cached pipeline engine per GPU */
+std::mutex g_direct_mu;
+std::vector<otc_engine *> g_direct;
+
 static int rccl_job_run(RcclJob &J, int mode, const uint8_t *hin, uint8_t *hout, size_t nbytes,
                         const otc_aes_key *k, const uint8_t ivc[16], int impl, double timeout_s);
 
@@ -1064,9 +1068,16 @@ static int rccl_job_run(RcclJob &J, int mode, const uint8_t *hin, uint8_t *hout,
 
 extern "C" void otc_multi_release(void)
 {
-    std::lock_guard<std::mutex> lk(g_rccl_mu);
-    delete g_rccl;
-    g_rccl = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_rccl_mu);
+        delete g_rccl;
+        g_rccl = nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_direct_mu);
+    for (otc_engine *&e : g_direct) {
+        otc_engine_destroy(e);
+        e = nullptr;
+    }
 }
 
 extern "C" int otc_multi_run(int ngpus, int strategy, int mode, const void *host_in, void *host_out, size_t nbytes,
@@ -1086,14 +1097,32 @@ extern "C" int otc_multi_run(int ngpus, int strategy, int mode, const void *host
     int rc = OTC_OK;
 
     if (strategy == 0) {
+        /* one host thread per GPU, each driving that GPU's cached pipeline
+         * engine (pinned ring + 3 streams: created on first use, reused by
+         * later calls with the same chunk size, freed by otc_multi_release).
+         * Error messages are thread_local: a worker's is carried back so
+         * otc_last_error() on the calling thread reports it. */
+        std::lock_guard<std::mutex> lk(g_direct_mu);
+        const size_t C = chunk_bytes ? ((chunk_bytes + 15) & ~(size_t)15) : (256ull << 20);
+        if (g_direct.size() < (size_t)ngpus) g_direct.resize(ngpus, nullptr);
         std::vector<std::thread> th;
         std::vector<int> res(ngpus, 0);
+        std::vector<std::string> msg(ngpus);
         for (int g = 0; g < ngpus; ++g) {
             th.emplace_back([&, g]() {
                 const size_t b0 = std::min(boff[g] * 16, nbytes), b1 = std::min(boff[g + 1] * 16, nbytes);
                 if (b1 <= b0) return;
-                otc_engine *e = otc_engine_create(g, chunk_bytes, 3);
-                if (!e) { res[g] = OTC_ERR_NOMEM; return; }
+                otc_engine *&e = g_direct[g];
+                if (e && e->chunk != C) {
+                    otc_engine_destroy(e);
+                    e = nullptr;
+                }
+                if (!e) e = otc_engine_create(g, C, 3);
+                if (!e) {
+                    res[g] = OTC_ERR_NOMEM;
+                    msg[g] = g_err;
+                    return;
+                }
                 uint8_t iv_local[16];
                 const uint8_t *ivp = ivc;
                 uint64_t bo = 0;
@@ -1104,12 +1133,19 @@ extern "C" int otc_multi_run(int ngpus, int strategy, int mode, const void *host
                 }
                 res[g] = otc_engine_run(e, mode, (const uint8_t *)host_in + b0, (uint8_t *)host_out + b0, b1 - b0, k,
                                         ivp, bo, impl, nullptr);
-                otc_engine_destroy(e);
+                if (res[g]) {
+                    msg[g] = g_err;
+                    otc_engine_destroy(e); /* unknown state: rebuild next time */
+                    e = nullptr;
+                }
             });
         }
         for (auto &t : th) t.join();
         for (int g = 0; g < ngpus; ++g)
-            if (res[g]) rc = res[g];
+            if (res[g]) {
+                rc = res[g];
+                set_err(rc, "GPU " + std::to_string(g) + ": " + msg[g]);
+            }
     } else {
         rc = rccl_scatter_gather(ngpus, mode, (const uint8_t *)host_in, (uint8_t *)host_out, nbytes, k, ivc, impl,
                                  chunk_bytes);
