@@ -28,22 +28,32 @@ from . import shard as sh
 
 
 def init_from_env(backend: str | None = None):
-    """Initialise the default process group from torchrun's env; binds the
-    rank to LOCAL_RANK's GPU.  Returns (rank, world, local_rank)."""
+    """Initialise the default process group from torchrun's env and bind the
+    rank to its GPU.  Returns (rank, world, gpu): gpu = LOCAL_RANK (one
+    process per GPU).
+
+    Rehearsal knobs (multi-rank code paths on a box with fewer GPUs than
+    ranks, e.g. 2 ranks on one MI355X): OTC_DIST_BACKEND=gloo picks the
+    backend (RCCL refuses two ranks on one device) and OTC_SHARE_GPUS=1 maps
+    rank r to GPU r mod device_count instead of failing."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    backend = backend or os.environ.get("OTC_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    gpu = local
+    if torch.cuda.is_available():
+        n = torch.cuda.device_count()
+        if local >= n:
+            if os.environ.get("OTC_SHARE_GPUS") != "1":
+                raise RuntimeError(f"LOCAL_RANK {local} but only {n} GPU(s) visible (OTC_SHARE_GPUS=1 to share)")
+            gpu = local % n
+        torch.cuda.set_device(gpu)
     if world > 1 and not dist.is_initialized():
         if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+            dist.init_process_group(backend, device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group(backend)
-    elif torch.cuda.is_available():
-        torch.cuda.set_device(local)
-    return rank, world, local
+    return rank, world, gpu
 
 
 def _world():
@@ -251,7 +261,8 @@ def allreduce_max(value: float, device=None) -> float:
     if world == 1:
         return value
     if device is None:
-        device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+        on_gpu = torch.cuda.is_available() and dist.get_backend() == "nccl"
+        device = torch.device("cuda", torch.cuda.current_device()) if on_gpu else "cpu"
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
