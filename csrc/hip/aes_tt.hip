@@ -845,7 +845,12 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_batch_tt(BatchParams P)
     constexpr uint32_t WAVES = THREADS / 64;
     constexpr uint64_t TILE = 64u * B;
 
-    for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < P.ntiles; t += (uint64_t)gridDim.x * WAVES) {
+    /* each wave walks a CONTIGUOUS run of tiles: consecutive tiles share
+     * tile-map / descriptor cache lines (and usually the message), so the
+     * dependent scalar loads at a tile start hit the scalar cache */
+    const uint64_t nw = (uint64_t)gridDim.x * WAVES, wid = (uint64_t)blockIdx.x * WAVES + wave;
+    const uint64_t t_end = (wid + 1) * P.ntiles / nw;
+    for (uint64_t t = wid * P.ntiles / nw; t < t_end; ++t) {
         /* descriptor, tile base and round keys through the constant address
          * space: wave-uniform addresses -> scalar loads (s_load_dwordx*) into
          * SGPRs, no VGPRs and no per-lane memory traffic */
