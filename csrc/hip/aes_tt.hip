@@ -860,36 +860,80 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_batch_tt(BatchParams P)
         uint8_t *out = (uint8_t *)cld64(D + 1);
         const uint64_t nbytes = cld64(D + 2);
         const Ctr128 c = {cld64(D + 3), cld64(D + 4)};
-        const uint32_t *Kg = P.keys[0].rk + (sizeof(otc_aes_key) / 4) * (uint32_t)cld64(D + 5);
+        const uint64_t kw = cld64(D + 5); /* key index | align word << 32 */
+        const uint32_t *Kg = P.keys[0].rk + (sizeof(otc_aes_key) / 4) * (uint32_t)kw;
+        const uint32_t align = (uint32_t)(kw >> 32);
         otc_aes_key K;
 #pragma unroll
         for (int q = 0; q < 4 * (NR + 1); ++q) K.rk[q] = cld32(Kg + q);
         const uint64_t nfull = nbytes >> 4;
         const uint32_t tail = (uint32_t)(nbytes & 15u);
-        const uint64_t i0 = (t - cld64(P.tile_first + m)) * TILE + lane;
+        const uint64_t vb = (t - cld64(P.tile_first + m)) * TILE; /* tile base (virtual block) */
 
         uint32_t s[B][4];
         uint4 x[B];
+        int64_t i0;
+        if (align & OTC_BATCH_ALIGNED) {
+            /* counter-aligned tiles (large messages): virtual block v = real
+             * block + shift with shift = ctr0.lo mod TILE, so within a tile the
+             * counters are C + 64b + lane with no carry out of the low byte
+             * and the bulk kernel's counter-mode caching applies: rounds 1-2
+             * cost 1 + 4 LDS lookups per block instead of 32 (133 vs 160) */
+            const uint64_t shift = align & 0xFFFFu;
+            const uint64_t cb = c.lo - shift; /* no borrow: shift <= ctr0.lo mod TILE */
+            const uint64_t clo = cb + vb;
+            const uint64_t chi = c.hi + (clo < cb ? 1u : 0u);
+            const uint32_t w0 = bswap32((uint32_t)(chi >> 32)) ^ K.rk[0];
+            const uint32_t w1 = bswap32((uint32_t)chi) ^ K.rk[1];
+            const uint32_t w2 = bswap32((uint32_t)(clo >> 32)) ^ K.rk[2];
+            const uint32_t w3u = bswap32((uint32_t)clo) ^ K.rk[3];
+            const uint32_t U0 = te_u(w0) ^ rotl8(te_u(w1 >> 8)) ^ rotl16(te_u(w2 >> 16)) ^ K.rk[4];
+            const uint32_t t1 = te_u(w1) ^ rotl8(te_u(w2 >> 8)) ^ rotl16(te_u(w3u >> 16)) ^ rotl24(te_u(w0 >> 24)) ^ K.rk[5];
+            const uint32_t t2 = te_u(w2) ^ rotl8(te_u(w3u >> 8)) ^ rotl16(te_u(w0 >> 16)) ^ rotl24(te_u(w1 >> 24)) ^ K.rk[6];
+            const uint32_t t3 = te_u(w3u) ^ rotl8(te_u(w0 >> 8)) ^ rotl16(te_u(w1 >> 16)) ^ rotl24(te_u(w2 >> 24)) ^ K.rk[7];
+            const uint32_t V0 = rotl8(te_u(t1 >> 8)) ^ rotl16(te_u(t2 >> 16)) ^ rotl24(te_u(t3 >> 24)) ^ K.rk[8];
+            const uint32_t V1 = te_u(t1) ^ rotl8(te_u(t2 >> 8)) ^ rotl16(te_u(t3 >> 16)) ^ K.rk[9];
+            const uint32_t V2 = te_u(t2) ^ rotl8(te_u(t3 >> 8)) ^ rotl24(te_u(t1 >> 24)) ^ K.rk[10];
+            const uint32_t V3 = te_u(t3) ^ rotl16(te_u(t1 >> 16)) ^ rotl24(te_u(t2 >> 24)) ^ K.rk[11];
+            const uint32_t b15 = (uint32_t)(clo & 0xFFu);
+            i0 = (int64_t)vb - (int64_t)shift + lane;
 #pragma unroll
-        for (int b = 0; b < B; ++b) {
-            const uint64_t i = i0 + 64u * b;
-            ctr_words(c, i, false, s[b][0], s[b][1], s[b][2], s[b][3]);
-            x[b] = i < nfull ? gld16(in, i) : make_uint4(0, 0, 0, 0);
+            for (int b = 0; b < B; ++b) {
+                const int64_t i = i0 + 64 * b;
+                x[b] = (i >= 0 && (uint64_t)i < nfull) ? gld16(in, (uint64_t)i) : make_uint4(0, 0, 0, 0);
+                const uint32_t c15 = (b15 | (uint32_t)(64 * b) | lane) ^ (K.rk[3] >> 24);
+                const uint32_t s0 = U0 ^ lds_at(tbl, (c15 << 8) | lk[3]);
+                s[b][0] = V0 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[0], SEL_HI(0)));
+                s[b][1] = V1 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[3], SEL_HI(3)));
+                s[b][2] = V2 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[2], SEL_HI(2)));
+                s[b][3] = V3 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[1], SEL_HI(1)));
+            }
+            enc_rounds4_from<3, NR, B>(tbl, lk, K, s);
+        } else {
+            i0 = (int64_t)vb + lane;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) s[b][j] ^= K.rk[j];
+            for (int b = 0; b < B; ++b) {
+                const uint64_t i = (uint64_t)i0 + 64u * b;
+                ctr_words(c, i, false, s[b][0], s[b][1], s[b][2], s[b][3]);
+                x[b] = i < nfull ? gld16(in, i) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) s[b][j] ^= K.rk[j];
+            }
+            enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
         }
-        enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
 #pragma unroll
         for (int b = 0; b < B; ++b) {
-            const uint64_t i = i0 + 64u * b;
-            if (i < nfull) {
-                gst16(out, i, make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
-            } else if (i == nfull && tail) {
+            const int64_t i = i0 + 64 * b;
+            if (i < 0) continue;
+            if ((uint64_t)i < nfull) {
+                gst16(out, (uint64_t)i,
+                      make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
+            } else if ((uint64_t)i == nfull && tail) {
                 const uint32_t ks[4] = {s[b][0], s[b][1], s[b][2], s[b][3]};
                 const g_u8 *gi = (const g_u8 *)in;
                 g_u8 *go = (g_u8 *)out;
                 for (uint32_t n = 0; n < tail; ++n)
-                    go[16 * i + n] = gi[16 * i + n] ^ (uint8_t)(ks[n >> 2] >> (8 * (n & 3)));
+                    go[16 * (uint64_t)i + n] = gi[16 * (uint64_t)i + n] ^ (uint8_t)(ks[n >> 2] >> (8 * (n & 3)));
             }
         }
     }

@@ -298,7 +298,8 @@ extern "C" uint64_t otc_ctr_batch_plan(const otc_ctr_msg *msgs, size_t nmsg, int
     const uint64_t tile_bytes = 16ull * (uint64_t)tile_blocks;
     uint64_t t = 0;
     for (size_t m = 0; m < nmsg; ++m) {
-        const uint64_t nt = (msgs[m].nbytes + tile_bytes - 1) / tile_bytes;
+        const uint64_t shift = (msgs[m].align & OTC_BATCH_ALIGNED) ? 16ull * (msgs[m].align & 0xFFFFu) : 0;
+        const uint64_t nt = msgs[m].nbytes ? (msgs[m].nbytes + shift + tile_bytes - 1) / tile_bytes : 0;
         if (tile_first) tile_first[m] = t;
         if (tile_msg)
             for (uint64_t k = 0; k < nt; ++k) tile_msg[t + k] = (uint32_t)m;

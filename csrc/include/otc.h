@@ -126,11 +126,20 @@ typedef struct {
     uint64_t ctr_hi;  /* initial counter, bytes 0..7 as a big-endian number */
     uint64_t ctr_lo;  /* bytes 8..15 */
     uint32_t key;     /* index into keys[] */
-    uint32_t pad;
+    uint32_t align;   /* 0: tiles start at the message's first block.
+                         OTC_BATCH_ALIGNED | shift: counter-aligned tiles,
+                         shift = ctr_lo mod tile_blocks, so every tile
+                         starts at a counter multiple of tile_blocks (the first
+                         tile is partial) and rounds 1-2 are mostly computed
+                         once per tile (counter-mode caching: 133 instead of
+                         160 LDS lookups per AES-128 block) -- for messages of
+                         many tiles */
 } otc_ctr_msg;
+#define OTC_BATCH_ALIGNED 0x80000000u
 
 /* Host planner: fills tile_msg (may be NULL to only count) and tile_first for
- * host copies of the descriptors; returns the number of tiles. */
+ * host copies of the descriptors (honouring each message's `align` word);
+ * returns the number of tiles. */
 uint64_t otc_ctr_batch_plan(const otc_ctr_msg *msgs, size_t nmsg, int tile_blocks, uint32_t *tile_msg,
                             uint64_t *tile_first);
 

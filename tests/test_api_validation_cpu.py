@@ -145,7 +145,7 @@ class CtrMsg(ctypes.Structure):
     """Mirror of otc_ctr_msg (otc.h)."""
     _fields_ = [("inp", ctypes.c_uint64), ("out", ctypes.c_uint64), ("nbytes", ctypes.c_uint64),
                 ("ctr_hi", ctypes.c_uint64), ("ctr_lo", ctypes.c_uint64), ("key", ctypes.c_uint32),
-                ("pad", ctypes.c_uint32)]
+                ("align", ctypes.c_uint32)]
 
 
 def test_ctr_batch_planner_and_python_plan_agree(lib):
@@ -170,6 +170,9 @@ def test_ctr_batch_planner_and_python_plan_agree(lib):
         assert (tmap == np.repeat(np.arange(len(sizes), dtype=np.uint32), tiles.astype(np.int64))).all()
         assert first[0] == 0 and (first[1:] == np.cumsum(tiles)[:-1]).all()
     assert fn(msgs, len(sizes), 100, None, None) == 0
+    # counter-aligned messages (OTC_BATCH_ALIGNED | shift) own ceil((bytes + 16 shift) / tile) tiles
+    al = (CtrMsg * 2)(CtrMsg(0, 0, 4096 * 10, 0, 0, 0, 0x80000000 | 5), CtrMsg(0, 0, 4096 * 10, 0, 0, 0, 0x80000000))
+    assert fn(al, 2, 256, None, None) == 11 + 10
     # tile choice: 4 KiB messages fill 256-block tiles exactly, 1 KiB ones 64-block tiles
     assert aes_ops._pick_tile(np.full(100, 4096, np.uint64)) == 256
     assert aes_ops._pick_tile(np.full(100, 1024, np.uint64)) == 64

@@ -32,7 +32,8 @@ def test_ctr_batch_matches_oracle(gpu, tile_blocks):
     kidx = [int(v) for v in rng.integers(0, len(keys), len(sizes))]
     ctrs = [os.urandom(16) for _ in sizes]
     ctrs[3] = os.urandom(8) + (2**64 - 3).to_bytes(8, "big")
-    ctrs[8] = b"\xff" * 16
+    ctrs[8] = b"\xff" * 16                                   # 2^128 wrap inside a counter-aligned message
+    ctrs[9] = os.urandom(8) + (2**64 - 5000).to_bytes(8, "big")  # 2^64 carry inside one
     xs = _messages(gpu, sizes, 1)
     outs = ops.ctr_batch(xs, keys, ctrs, key_index=kidx, tile_blocks=tile_blocks)
     torch.cuda.synchronize()
