@@ -16,6 +16,11 @@ round r (root ingress) is issued asynchronously on its own communicator and
 overlaps the scatter of round r+1 (root egress) -- xGMI links are full
 duplex.  --no-overlap serialises both on one communicator (A/B).
 
+--decrypt: exact single-stream CBC decryption instead -- every scattered
+piece carries the 16-byte ciphertext block in front of it (the halo), so each
+rank decrypts its piece independently and the gathered result equals the
+serial decryption of the whole stream.
+
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 benchmarks/cbc_scatter.py
     python benchmarks/cbc_scatter.py --gib-per-gpu 4        # 1 GPU
 """
@@ -42,6 +47,8 @@ def main():
     ap.add_argument("--sector", type=int, default=4096)
     ap.add_argument("--bits", type=int, default=256)
     ap.add_argument("--no-overlap", action="store_true", help="serial scatter -> encrypt -> gather rounds")
+    ap.add_argument("--decrypt", action="store_true",
+                    help="exact single-stream CBC decryption: every piece travels with its 16-byte halo")
     args = ap.parse_args()
 
     rank, world, local = pdist.init_from_env()
@@ -53,14 +60,33 @@ def main():
     key = bytes(range(args.bits // 8))
     iv0 = bytes(range(0xA0, 0xB0))
     seg = args.sector
-    pipe = pdist.ScatterGatherPipeline(chunk, root=0, device=dev, overlap=not args.no_overlap)
+    # decrypt: a piece is [16-byte halo | chunk of ciphertext]; the halo is the
+    # ciphertext block in front of the chunk in the single stream (the IV for
+    # the very first one), so every rank decrypts exactly
+    H = 16 if args.decrypt else 0
+    piece_bytes = chunk + H
+    pipe = pdist.ScatterGatherPipeline(piece_bytes, root=0, device=dev, overlap=not args.no_overlap)
+    carry = torch.tensor(list(iv0), dtype=torch.uint8, device=dev)  # last block of the previous round (root)
 
     def produce(send, r):
-        ops.fill_random_(send, seed=r)
+        if not args.decrypt:
+            ops.fill_random_(send, seed=r)
+            return
+        v = send.view(world, piece_bytes)
+        for g in range(world):  # synthetic ciphertext, piece by piece (rows are strided)
+            ops.fill_random_(v[g, H:], seed=r * world + g)
+        v[0, :H].copy_(carry)
+        v[1:, :H].copy_(v[:-1, -H:])
+        carry.copy_(v[-1, -H:])
 
     def work(piece, out, r):
-        gofs = (r * world + rank) * chunk
-        ops.cbc_encrypt_segments(piece, key, sh.ctr_add(iv0, gofs // seg), seg, out=out)
+        if not args.decrypt:
+            gofs = (r * world + rank) * chunk
+            ops.cbc_encrypt_segments(piece, key, sh.ctr_add(iv0, gofs // seg), seg, out=out)
+            return
+        # IV 0, then XOR the halo into the first block: no host round trip
+        ops.cbc_decrypt(piece[H:], key, bytes(16), out=out[H:])
+        out[H:2 * H].bitwise_xor_(piece[:H])
 
     verdict = {}
 
@@ -70,11 +96,17 @@ def main():
         torch.cuda.synchronize()
         n = 4 * seg
         ok = True
+        send = pipe.send[r % len(pipe.send)]
         for g in (0, world - 1):
-            a = g * chunk
-            pt = pipe.send[r % len(pipe.send)][a:a + n].cpu().numpy().tobytes()
-            exp = cpu_ref.cbc_segments(key, sh.ctr_add(iv0, (r * world + g) * chunk // seg), pt, seg)
-            ok = ok and gathered[a:a + n].cpu().numpy().tobytes() == exp
+            a = g * piece_bytes
+            src = send[a + H:a + H + n].cpu().numpy().tobytes()
+            if args.decrypt:
+                exp = cpu_ref.cbc(key, send[a:a + H].cpu().numpy().tobytes(), src, decrypt=True)
+            else:
+                exp = cpu_ref.cbc_segments(key, sh.ctr_add(iv0, (r * world + g) * chunk // seg), src, seg)
+            ok = ok and gathered[a + H:a + H + n].cpu().numpy().tobytes() == exp
+        if args.decrypt and world > 1:  # halo of rank 1 = last ciphertext block of rank 0
+            ok = ok and torch.equal(send[piece_bytes:piece_bytes + H], send[piece_bytes - H:piece_bytes])
         verdict["ok"] = ok
 
     pipe.run(1, produce, work, verify)  # warmup + verification
@@ -88,7 +120,8 @@ def main():
         torch.distributed.barrier()
     el = pdist.allreduce_max(time.perf_counter() - t0)
     if rank == 0:
-        print(json.dumps({"metric": f"GB/s AES-{args.bits}-CBC (sector-parallel) root scatter/gather",
+        what = "decrypt, exact single stream (halos)" if args.decrypt else "sector-parallel encrypt"
+        print(json.dumps({"metric": f"GB/s AES-{args.bits}-CBC ({what}) root scatter/gather",
                           "n_gpus": world, "total_bytes": total, "rounds": rounds, "chunk_per_rank": chunk,
                           "overlap": pipe.overlap, "seconds": round(el, 3), "value": round(total / el / 1e9, 3),
                           "unit": "GB/s", "verified_sample": bool(verdict.get("ok")),
