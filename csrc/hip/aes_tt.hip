@@ -961,6 +961,21 @@ int grid_for(uint64_t work_items, uint64_t per_wg, int wg_per_cu)
     return (int)(need < cap ? need : cap);
 }
 
+/* Small inputs: a persistent 1024 x 4 workgroup takes 4096 blocks per step,
+ * so a 1 MiB message (65536 blocks) occupies only 16 CUs and takes as long as
+ * one CU needs for 4096 blocks (~10 us).  Below these sizes the launch uses
+ * smaller steps so that (up to) every CU gets work: 256 threads x 1 block per
+ * lane up to 256 x 256 blocks (1 MiB), 1024 x 1 up to 256 x 1024 (4 MiB). */
+enum SmallShape { SHAPE_BULK = 0, SHAPE_256x1 = 1, SHAPE_1024x1 = 2 };
+inline SmallShape small_shape(uint64_t nblocks)
+{
+    static const bool off = getenv("OTC_TT_NOSMALL") != nullptr; /* A/B */
+    if (off) return SHAPE_BULK;
+    if (nblocks <= 256ull * 256) return SHAPE_256x1;
+    if (nblocks <= 256ull * 1024) return SHAPE_1024x1;
+    return SHAPE_BULK;
+}
+
 constexpr int ENC_THREADS = 1024; /* measured best of 256..1024 x B=1..4 (docs/PERF.md) */
 constexpr int ENC_B = 4;
 constexpr int DEC_THREADS = 1024;
@@ -1002,7 +1017,11 @@ hipError_t launch_enc_nr(const EncParams &P, const otc_aes_key &K, hipStream_t s
     const TTVariant v = tt_variant();
     if (v.threads == 1024 && v.b == 2) return launch_enc_tb<NR, MODE, 1024, 2>(P, K, st);
     if (v.threads == 512 && v.b == 4) return launch_enc_tb<NR, MODE, 512, 4>(P, K, st);
-    return launch_enc_tb<NR, MODE, ENC_THREADS, ENC_B>(P, K, st);
+    switch (small_shape(P.nfull + (P.tail ? 1 : 0))) {
+    case SHAPE_256x1: return launch_enc_tb<NR, MODE, 256, 1>(P, K, st);
+    case SHAPE_1024x1: return launch_enc_tb<NR, MODE, 1024, 1>(P, K, st);
+    default: return launch_enc_tb<NR, MODE, ENC_THREADS, ENC_B>(P, K, st);
+    }
 }
 
 template <int MODE>
@@ -1019,8 +1038,18 @@ hipError_t launch_enc(const EncParams &P, const otc_aes_key &K, hipStream_t st)
 template <int NR, int MODE>
 hipError_t launch_dec_nr(const DecParams &P, const otc_aes_key &K, hipStream_t st)
 {
-    int grid = grid_for(P.nfull, (uint64_t)DEC_THREADS * DEC_B, 1);
-    hipLaunchKernelGGL((k_aes_dec_tt<NR, MODE, DEC_B, DEC_THREADS>), dim3(grid), dim3(DEC_THREADS), 0, st, P, K);
+    switch (small_shape(P.nfull)) {
+    case SHAPE_256x1:
+        hipLaunchKernelGGL((k_aes_dec_tt<NR, MODE, 1, 256>), dim3(grid_for(P.nfull, 256, 1)), dim3(256), 0, st, P, K);
+        break;
+    case SHAPE_1024x1:
+        hipLaunchKernelGGL((k_aes_dec_tt<NR, MODE, 1, 1024>), dim3(grid_for(P.nfull, 1024, 1)), dim3(1024), 0, st, P,
+                           K);
+        break;
+    default:
+        hipLaunchKernelGGL((k_aes_dec_tt<NR, MODE, DEC_B, DEC_THREADS>),
+                           dim3(grid_for(P.nfull, (uint64_t)DEC_THREADS * DEC_B, 1)), dim3(DEC_THREADS), 0, st, P, K);
+    }
     return hipGetLastError();
 }
 
@@ -1126,7 +1155,11 @@ hipError_t launch_ctr_cached(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo,
     if (v.threads == 512 && v.b == 4) return launch_ctr_cached_tb<NR, 512, 4, true>(P, K, ctr_lo, st);
     if (v.threads == -1024 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, false>(P, K, ctr_lo, st);
     if (v.threads == -1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, false>(P, K, ctr_lo, st);
-    return launch_ctr_cached_tb<NR, 1024, 4, true>(P, K, ctr_lo, st);
+    switch (small_shape(P.nfull + (P.tail ? 1 : 0))) {
+    case SHAPE_256x1: return launch_ctr_cached_tb<NR, 256, 1, true>(P, K, ctr_lo, st);
+    case SHAPE_1024x1: return launch_ctr_cached_tb<NR, 1024, 1, true>(P, K, ctr_lo, st);
+    default: return launch_ctr_cached_tb<NR, 1024, 4, true>(P, K, ctr_lo, st);
+    }
 }
 
 void tt_set_wg_per_cu(int n) { g_tt_wg_per_cu = n < 1 ? 1 : n; }
