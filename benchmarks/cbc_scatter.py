@@ -111,12 +111,12 @@ def main():
 
     pipe.run(1, produce, work, verify)  # warmup + verification
     torch.cuda.synchronize()
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.barrier()
     t0 = time.perf_counter()
     pipe.run(rounds, produce, work)
     torch.cuda.synchronize()
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.barrier()
     el = pdist.allreduce_max(time.perf_counter() - t0)
     if rank == 0:
@@ -126,7 +126,7 @@ def main():
                           "overlap": pipe.overlap, "seconds": round(el, 3), "value": round(total / el / 1e9, 3),
                           "unit": "GB/s", "verified_sample": bool(verdict.get("ok")),
                           "data": "synthetic random (root GPU fill)"}), flush=True)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

@@ -35,7 +35,8 @@ def init_from_env(backend: str | None = None):
     Rehearsal knobs (multi-rank code paths on a box with fewer GPUs than
     ranks, e.g. 2 ranks on one MI355X): OTC_DIST_BACKEND=gloo picks the
     backend (RCCL refuses two ranks on one device) and OTC_SHARE_GPUS=1 maps
-    rank r to GPU r mod device_count instead of failing."""
+    rank r to GPU r mod device_count instead of failing; OTC_DIST_FORCE=1
+    creates the process group even at world size 1."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -48,7 +49,8 @@ def init_from_env(backend: str | None = None):
                 raise RuntimeError(f"LOCAL_RANK {local} but only {n} GPU(s) visible (OTC_SHARE_GPUS=1 to share)")
             gpu = local % n
         torch.cuda.set_device(gpu)
-    if world > 1 and not dist.is_initialized():
+    force = os.environ.get("OTC_DIST_FORCE") == "1"  # a 1-rank group too (exercises the RCCL path)
+    if (world > 1 or force) and not dist.is_initialized():
         if backend == "nccl":
             dist.init_process_group(backend, device_id=torch.device("cuda", gpu))
         else:
@@ -56,10 +58,20 @@ def init_from_env(backend: str | None = None):
     return rank, world, gpu
 
 
+def _pg_on() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
 def _world():
-    if dist.is_available() and dist.is_initialized():
+    if _pg_on():
         return dist.get_rank(), dist.get_world_size()
     return 0, 1
+
+
+def reset_groups():
+    """Forget the cached duplex communicators (call after
+    destroy_process_group, before initialising a new default group)."""
+    _DUPLEX_GROUPS.clear()
 
 
 def _ctr_local(x: torch.Tensor, key: bytes, counter: bytes, block_offset: int, impl="auto") -> torch.Tensor:
@@ -121,7 +133,7 @@ def duplex_groups():
     time: xGMI links are full duplex, and one communicator would serialise the
     two directions.  Collective on first use (every rank calls it in the same
     order); cached afterwards."""
-    if not (dist.is_available() and dist.is_initialized()):
+    if not _pg_on():
         return None, None
     key = (dist.get_backend(), dist.get_world_size())
     if key not in _DUPLEX_GROUPS:
@@ -151,7 +163,10 @@ class ScatterGatherPipeline:
                       else torch.device("cpu"))
         self.device = torch.device(device)
         self.chunk = max(sh.BLOCK, chunk_per_rank - chunk_per_rank % sh.BLOCK)
-        self.overlap = overlap and self.world > 1
+        # collectives whenever a process group exists, even at world size 1
+        # (a 1-rank RCCL group runs the same scatter/gather code path)
+        self.comm = _pg_on()
+        self.overlap = overlap and self.comm
         self.g_sc, self.g_ga = duplex_groups() if self.overlap else (None, None)
         nslot = 2 if self.overlap else 1
 
@@ -185,13 +200,13 @@ class ScatterGatherPipeline:
                 pending[s] = None
             if is_root:
                 produce(self.send[s], r)
-            if self.world > 1:
+            if self.comm:
                 dist.scatter(self.recv[s], list(self.send[s].chunk(self.world)) if is_root else None,
                              src=self.root, group=self.g_sc)
             else:
                 self.recv[s].copy_(self.send[s])
             fn(self.recv[s], self.out[s], r)
-            if self.world > 1:
+            if self.comm:
                 work = dist.gather(self.out[s], list(self.gath[s].chunk(self.world)) if is_root else None,
                                    dst=self.root, group=self.g_ga, async_op=self.overlap)
             else:
@@ -257,8 +272,7 @@ def scatter_ctr(full: torch.Tensor | None, nbytes: int, key: bytes, counter: byt
 
 
 def allreduce_max(value: float, device=None) -> float:
-    rank, world = _world()
-    if world == 1:
+    if not _pg_on():
         return value
     if device is None:
         on_gpu = torch.cuda.is_available() and dist.get_backend() == "nccl"

@@ -59,7 +59,7 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_gloo_data_parallel(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

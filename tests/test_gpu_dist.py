@@ -1,0 +1,78 @@
+"""The RCCL (torch.distributed backend "nccl") code path on a real MI355X.
+
+Multi-rank RCCL needs one GPU per rank, so on the one-GPU test box this runs a
+world-size-1 RCCL group in-process: ScatterGatherPipeline issues the same
+RCCL scatter / async gather on its two extra communicators as at 8 ranks, and
+allreduce_max runs an RCCL all-reduce on a device tensor.  Results are checked
+against the CPU oracle.  Multi-rank correctness is covered by
+tests/test_dist_cpu.py (gloo, world sizes 2 and 3)."""
+import os
+import socket
+
+import pytest
+import torch
+
+from our_tree_amd.models import cpu_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture
+def rccl_world1(gpu):
+    import torch.distributed as dist
+
+    from our_tree_amd.parallel import dist as pdist
+
+    if dist.is_initialized():
+        pytest.skip("a process group already exists in this process")
+    store = dist.TCPStore("127.0.0.1", _free_port(), 1, is_master=True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=gpu)
+    pdist.reset_groups()
+    try:
+        yield pdist
+    finally:
+        dist.destroy_process_group()
+        pdist.reset_groups()
+
+
+def test_rccl_scatter_gather_pipeline(gpu, rccl_world1):
+    pdist = rccl_world1
+    import torch.distributed as dist
+
+    assert dist.get_backend() == "nccl"
+    key, ctr0 = os.urandom(16), (2**64 - 7).to_bytes(16, "big")
+    n = (3 << 20) + 37  # 4 rounds of 1 MiB, uneven tail
+    g = torch.Generator().manual_seed(3)
+    full = torch.randint(0, 256, (n,), dtype=torch.uint8, generator=g).to(gpu)
+    exp = cpu_ref.ctr(key, ctr0, full.cpu().numpy().tobytes())
+    for overlap in (True, False):
+        res = pdist.scatter_ctr(full, n, key, ctr0, chunk_per_rank=1 << 20, overlap=overlap)
+        torch.cuda.synchronize()
+        assert res.device.type == "cuda"
+        assert res.cpu().numpy().tobytes() == exp, f"overlap={overlap}"
+    pipe = pdist.ScatterGatherPipeline(1 << 16, device=gpu)
+    assert pipe.comm and pipe.overlap and pipe.g_sc is not None
+    assert pdist.allreduce_max(2.5) == 2.5
+
+
+def test_rccl_sharded_cbc_decrypt(gpu, rccl_world1):
+    pdist = rccl_world1
+    key, iv = os.urandom(32), os.urandom(16)
+    pt = os.urandom(16 * 5000)
+    ct = torch.frombuffer(bytearray(cpu_ref.cbc(key, iv, pt)), dtype=torch.uint8).to(gpu)
+    out = pdist.cbc_decrypt_sharded(ct, key, iv)
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tobytes() == pt
+    loc = torch.frombuffer(bytearray(pt), dtype=torch.uint8).to(gpu)
+    ctr0 = os.urandom(16)
+    pdist.sharded_ctr_(loc, key[:16], ctr0)
+    torch.cuda.synchronize()
+    assert loc.cpu().numpy().tobytes() == cpu_ref.ctr(key[:16], ctr0, pt)
