@@ -77,6 +77,121 @@ __device__ __forceinline__ uint32_t sbox_addr(uint32_t x, uint32_t lane4)
     return t | (x & 3u) | lane4;
 }
 
+/* Output modes: RC4_KS = keystream only (no input); RC4_VEC = input, in/out
+ * 16-byte aligned and len a multiple of 16 (host-checked), so every lane
+ * uses 16-byte accesses and the input chunk is loaded one chunk ahead;
+ * RC4_ANY = input with arbitrary alignment. */
+enum { RC4_KS = 0, RC4_VEC = 1, RC4_ANY = 2 };
+
+__device__ __forceinline__ void rc4_emit(const uint8_t *in, uint8_t *out, uint64_t pos, uint32_t kb, bool live)
+{
+    if (live) out[pos] = in ? (uint8_t)(in[pos] ^ kb) : (uint8_t)kb;
+}
+
+__device__ __forceinline__ uint4 rc4_ld16(const uint8_t *p)
+{
+    return *reinterpret_cast<const uint4 *>(p);
+}
+
+__device__ __forceinline__ void rc4_st16x(uint8_t *p, const uint32_t (&w)[4], uint4 x, bool live)
+{
+    if (live) *reinterpret_cast<uint4 *>(p) = make_uint4(w[0] ^ x.x, w[1] ^ x.y, w[2] ^ x.z, w[3] ^ x.w);
+}
+
+/* RC4_KS / RC4_ANY: 16 bytes at pos, 16-byte access where both pointers allow */
+__device__ __forceinline__ void rc4_store16_any(const uint8_t *in, uint8_t *out, uint64_t pos, const uint32_t (&w)[4],
+                                                bool live)
+{
+    if (!live) return;
+    if ((((uintptr_t)(out + pos) | (in ? (uintptr_t)(in + pos) : 0)) & 15u) == 0) {
+        rc4_st16x(out + pos, w, in ? rc4_ld16(in + pos) : make_uint4(0, 0, 0, 0), true);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) rc4_emit(in, out, pos + q, (w[q >> 2] >> (8 * (q & 3))) & 0xFFu, true);
+    }
+}
+
+/* Main loop over 16-byte chunks while m + LIM <= len.  RC4_VEC: the input
+ * chunk of the NEXT 16 bytes is loaded (unconditionally, at a clamped,
+ * always-valid address) while the current ones are generated, in two
+ * alternating registers -- a load issued at store time exposes the whole HBM
+ * latency once per 16 bytes, and a register copy of a just-loaded value
+ * waits for it. */
+#define RC4_MAIN_LOOP(LIM, GEN16)                                                                              \
+    if constexpr (MODE == RC4_VEC) {                                                                           \
+        uint4 xa = make_uint4(0, 0, 0, 0), xb;                                                                 \
+        if (m + (LIM) <= len) xa = rc4_ld16(in + base + m);                                                    \
+        while (m + (LIM) <= len) {                                                                             \
+            xb = rc4_ld16(in + base + (m + 16 < len - 16 ? m + 16 : len - 16));                                \
+            {                                                                                                  \
+                uint32_t w[4] = {0, 0, 0, 0};                                                                  \
+                GEN16(w);                                                                                      \
+                rc4_st16x(out + base + m, w, xa, live);                                                        \
+            }                                                                                                  \
+            m += 16;                                                                                           \
+            if (m + (LIM) > len) break;                                                                        \
+            xa = rc4_ld16(in + base + (m + 16 < len - 16 ? m + 16 : len - 16));                                \
+            {                                                                                                  \
+                uint32_t w[4] = {0, 0, 0, 0};                                                                  \
+                GEN16(w);                                                                                      \
+                rc4_st16x(out + base + m, w, xb, live);                                                        \
+            }                                                                                                  \
+            m += 16;                                                                                           \
+        }                                                                                                      \
+    } else {                                                                                                   \
+        while (m + (LIM) <= len) {                                                                             \
+            uint32_t w[4] = {0, 0, 0, 0};                                                                      \
+            GEN16(w);                                                                                          \
+            rc4_store16_any(in, out, base + m, w, live);                                                       \
+            m += 16;                                                                                           \
+        }                                                                                                      \
+    }
+
+/* PRGA: the loop of arc4_prep (reference arc4.c:72-97), one stream per lane.
+ * Measured and rejected (profiles/r1/otbench_rc4_prefetch_pipe_ab.jsonl,
+ * rocprof/rc4_counters.txt): a software-pipelined variant that writes each
+ * swap two iterations late and corrects the reads issued before it in
+ * registers (no LDS round trip left in the j chain) -- 4-8% slower: a wave
+ * issues at most one instruction per 4 cycles, and the corrections add half
+ * again to the ~27 instructions per byte, which bound the loop with 2 waves
+ * per SIMD more than the LDS latency does. */
+template <int MODE>
+__device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i, uint32_t j, uint64_t len,
+                                               const uint8_t *in, uint8_t *out, uint64_t base, bool live)
+{
+#define RC4_STEP(O)                                                                                            \
+    do {                                                                                                       \
+        i = (i + 1) & 0xFFu;                                                                                   \
+        const uint32_t ai_ = sbox_addr(i, lane4);                                                              \
+        const uint32_t a_ = S[ai_];                                                                            \
+        j = (j + a_) & 0xFFu;                                                                                  \
+        const uint32_t aj_ = sbox_addr(j, lane4);                                                              \
+        const uint32_t b_ = S[aj_];                                                                            \
+        S[ai_] = (uint8_t)b_;                                                                                  \
+        S[aj_] = (uint8_t)a_;                                                                                  \
+        O = S[sbox_addr(a_ + b_, lane4)];                                                                      \
+    } while (0)
+#define RC4_GEN16(w)                                                                                           \
+    _Pragma("unroll") for (int q = 0; q < 16; ++q)                                                             \
+    {                                                                                                          \
+        uint32_t o;                                                                                            \
+        RC4_STEP(o);                                                                                           \
+        w[q >> 2] |= o << (8 * (q & 3));                                                                       \
+    }
+    uint64_t m = 0;
+    RC4_MAIN_LOOP(16, RC4_GEN16)
+    for (; m < len; ++m) {
+        uint32_t o;
+        RC4_STEP(o);
+        rc4_emit(in, out, base + m, o, live);
+    }
+#undef RC4_GEN16
+#undef RC4_STEP
+}
+
+#undef RC4_MAIN_LOOP
+
+template <int MODE>
 __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keylen, uint64_t nstreams, uint64_t len,
                                                    uint64_t drop, const uint8_t *in, uint8_t *out)
 {
@@ -90,7 +205,7 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     for (uint32_t q = 0; q < 64; ++q)
         *reinterpret_cast<uint32_t *>(S + ((q << 8) | lane4)) = 0x03020100u + 0x04040404u * q;
 
-    /* KSA */
+    /* KSA (reference arc4.c:43-67) */
     const uint8_t *key = keys + (live ? sid : 0) * (uint64_t)keylen;
     uint32_t j = 0;
     int kpos = 0;
@@ -105,7 +220,7 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
         S[aj] = (uint8_t)a;
     }
 
-    /* PRGA */
+    /* RC4-drop: discard the first `drop` keystream bytes */
     uint32_t i = 0;
     j = 0;
     for (uint64_t n = 0; n < drop; ++n) {
@@ -119,55 +234,8 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
         S[aj] = (uint8_t)a;
     }
     const uint64_t base = (live ? sid : 0) * len;
-    uint64_t n = 0;
-    for (; n + 16 <= len; n += 16) {
-        uint32_t w[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int bidx = 0; bidx < 4; ++bidx) {
-                i = (i + 1) & 0xFFu;
-                const uint32_t ai = sbox_addr(i, lane4);
-                const uint32_t a = S[ai];
-                j = (j + a) & 0xFFu;
-                const uint32_t aj = sbox_addr(j, lane4);
-                const uint32_t b = S[aj];
-                S[ai] = (uint8_t)b;
-                S[aj] = (uint8_t)a;
-                v |= (uint32_t)S[sbox_addr(a + b, lane4)] << (8 * bidx);
-            }
-            w[q] = v;
-        }
-        if (live) {
-            uint4 o = make_uint4(w[0], w[1], w[2], w[3]);
-            /* 16-byte path only where both pointers are 16-byte aligned */
-            if ((((uintptr_t)(out + base + n) | (in ? (uintptr_t)(in + base + n) : 0)) & 15u) == 0) {
-                if (in) {
-                    const uint4 x = *reinterpret_cast<const uint4 *>(in + base + n);
-                    o.x ^= x.x; o.y ^= x.y; o.z ^= x.z; o.w ^= x.w;
-                }
-                *reinterpret_cast<uint4 *>(out + base + n) = o;
-            } else {
-                for (int q = 0; q < 16; ++q) {
-                    uint8_t kb = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
-                    out[base + n + q] = in ? (uint8_t)(in[base + n + q] ^ kb) : kb;
-                }
-            }
-        }
-    }
-    for (; n < len; ++n) {
-        i = (i + 1) & 0xFFu;
-        const uint32_t ai = sbox_addr(i, lane4);
-        const uint32_t a = S[ai];
-        j = (j + a) & 0xFFu;
-        const uint32_t aj = sbox_addr(j, lane4);
-        const uint32_t b = S[aj];
-        S[ai] = (uint8_t)b;
-        S[aj] = (uint8_t)a;
-        const uint8_t kb = S[sbox_addr(a + b, lane4)];
-        if (live) out[base + n] = in ? (uint8_t)(in[base + n] ^ kb) : kb;
-    }
+    const uint8_t *src = MODE == RC4_KS ? nullptr : in;
+    rc4_prga<MODE>(S, lane4, i, j, len, src, out, base, live);
 }
 
 int g_cus_s = 0;
@@ -250,8 +318,11 @@ hipError_t k_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t 
                        void *out, hipStream_t st)
 {
     const uint64_t wgs = (nstreams + 63) / 64;
-    hipLaunchKernelGGL(k_rc4_kernel, dim3((unsigned)wgs), dim3(64), 0, st, keys, keylen, (uint64_t)nstreams,
-                       (uint64_t)len, (uint64_t)drop, (const uint8_t *)in, (uint8_t *)out);
+    const int mode = !in ? RC4_KS
+                     : ((((uintptr_t)in | (uintptr_t)out) & 15u) == 0 && len % 16 == 0) ? RC4_VEC : RC4_ANY;
+    auto kern = mode == RC4_KS ? k_rc4_kernel<RC4_KS> : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC> : k_rc4_kernel<RC4_ANY>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(64), 0, st, keys, keylen, (uint64_t)nstreams, (uint64_t)len,
+                       (uint64_t)drop, (const uint8_t *)in, (uint8_t *)out);
     return hipGetLastError();
 }
 

@@ -1,0 +1,14 @@
+#!/bin/bash
+# RC4 many-stream kernel after the input-prefetch change: tests + shapes.
+set -o pipefail
+export TMPDIR=/tmp
+OUT=gpurun_out/rc4final
+mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -k "rc4 or xor" -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+for shape in "131072 8K" "65536 4K" "1048576 1K"; do
+  set -- $shape
+  timeout -k 10 120 ./bin/otbench --mode rc4 --streams $1 --len $2 --iters 5 --warmup 1 --clock \
+    | sed "s/}$/, \"streams\": $1, \"len\": \"$2\"}/" >> $OUT/rc4.jsonl 2>> $OUT/err.log || exit 1
+done
+cat $OUT/rc4.jsonl
