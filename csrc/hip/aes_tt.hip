@@ -947,7 +947,7 @@ static_assert(64 * 4 == OTC_BATCH_TILE_BLOCKS, "largest tile must match otc.h");
  * ------------------------------------------------------------------------- */
 int g_num_cus = 0;
 
-int grid_for(uint64_t work_items, uint64_t per_wg, int wg_per_cu)
+int num_cus()
 {
     if (g_num_cus <= 0) {
         int dev = 0;
@@ -955,8 +955,13 @@ int grid_for(uint64_t work_items, uint64_t per_wg, int wg_per_cu)
         (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (g_num_cus <= 0) g_num_cus = 256;
     }
+    return g_num_cus;
+}
+
+int grid_for(uint64_t work_items, uint64_t per_wg, int wg_per_cu)
+{
     uint64_t need = (work_items + per_wg - 1) / per_wg;
-    uint64_t cap = (uint64_t)g_num_cus * (uint64_t)wg_per_cu;
+    uint64_t cap = (uint64_t)num_cus() * (uint64_t)wg_per_cu;
     if (need < 1) need = 1;
     return (int)(need < cap ? need : cap);
 }
@@ -965,14 +970,26 @@ int grid_for(uint64_t work_items, uint64_t per_wg, int wg_per_cu)
  * so a 1 MiB message (65536 blocks) occupies only 16 CUs and takes as long as
  * one CU needs for 4096 blocks (~10 us).  Below these sizes the launch uses
  * smaller steps so that (up to) every CU gets work: 256 threads x 1 block per
- * lane up to 256 x 256 blocks (1 MiB), 1024 x 1 up to 256 x 1024 (4 MiB). */
+ * lane up to 256 x 256 blocks (1 MiB), 1024 x 1 up to 256 x 1024 (4 MiB).
+ * Mid sizes: the busiest CU does ceil(steps / CUs) steps, so 10 MiB (160
+ * steps of 4096 blocks) leaves 96 CUs idle and 100 MiB (1600 steps) runs 7
+ * rounds for 6.25 rounds of work; 1024-block steps are used whenever they cut
+ * the busiest CU's block count by 5% or more. */
 enum SmallShape { SHAPE_BULK = 0, SHAPE_256x1 = 1, SHAPE_1024x1 = 2 };
+inline uint64_t busiest_cu_blocks(uint64_t nblocks, uint64_t step)
+{
+    const uint64_t cus = (uint64_t)num_cus();
+    return ((nblocks + step - 1) / step + cus - 1) / cus * step;
+}
 inline SmallShape small_shape(uint64_t nblocks)
 {
     static const bool off = getenv("OTC_TT_NOSMALL") != nullptr; /* A/B */
+    static const bool nomid = getenv("OTC_TT_NOMID") != nullptr;  /* A/B */
     if (off) return SHAPE_BULK;
     if (nblocks <= 256ull * 256) return SHAPE_256x1;
     if (nblocks <= 256ull * 1024) return SHAPE_1024x1;
+    if (!nomid && busiest_cu_blocks(nblocks, 1024) * 20 <= busiest_cu_blocks(nblocks, 4096) * 19)
+        return SHAPE_1024x1;
     return SHAPE_BULK;
 }
 

@@ -59,12 +59,18 @@ def _bytes(t: torch.Tensor) -> torch.Tensor:
     return t.reshape(-1).view(torch.uint8)
 
 
-def _run(x: torch.Tensor, out: torch.Tensor, call):
+def _run(x: torch.Tensor, out: torch.Tensor, call, inplace_ok: bool = True):
     """call(in_ptr, out_ptr) -> rc.  The kernels move 16 bytes per lane, so the
     native API requires 16-byte aligned buffers; a misaligned tensor (e.g. a
     byte slice ``t[3:]``) is staged through an aligned temporary (torch's
-    allocator aligns every fresh allocation) and copied back."""
+    allocator aligns every fresh allocation) and copied back.  Modes whose
+    parallel kernel reads ciphertext block i-1 while block i-1's output is
+    written (CBC / CFB decryption, ``inplace_ok=False``) run in place through
+    a copy of the input."""
     xp, op = x.data_ptr(), out.data_ptr()
+    if not inplace_ok and xp == op and _nbytes(x) > 16:
+        x = _bytes(x).clone()
+        xp = x.data_ptr()
     if not (xp % 16 or op % 16) or _nbytes(x) == 0:
         return call(xp, op)
     xi = _bytes(x).clone() if xp % 16 else _bytes(x)
@@ -387,13 +393,14 @@ def ecb_decrypt(x: torch.Tensor, key: bytes, out=None) -> torch.Tensor:
 
 
 def cbc_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None) -> torch.Tensor:
-    """Parallel CBC decryption (out must not alias x)."""
+    """Parallel CBC decryption.  In place (out=x) runs through a copy of the
+    input: block i needs ciphertext block i-1, which its own output overwrites."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     k = expand_key(key, decrypt=True)
     with torch.cuda.device(x.device):
         rc = _run(x, out, lambda ip, op: _lib().otc_aes_cbc_decrypt(ip, op, _nbytes(x), ctypes.byref(k), _b16(iv, "iv"),
-            _stream(x)))
+            _stream(x)), inplace_ok=False)
     _native.check(rc, "otc_aes_cbc_decrypt")
     return out
 
@@ -423,7 +430,7 @@ def cbc_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes:
     k = expand_key(key, decrypt=True)
     with torch.cuda.device(x.device):
         rc = _run(x, out, lambda ip, op: _lib().otc_aes_cbc_decrypt_segments(ip, op, segment_bytes, n // segment_bytes,
-            ctypes.byref(k), _b16(iv0, "iv0"), _stream(x)))
+            ctypes.byref(k), _b16(iv0, "iv0"), _stream(x)), inplace_ok=False)
     _native.check(rc, "otc_aes_cbc_decrypt_segments")
     return out
 
@@ -434,6 +441,6 @@ def cfb128_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None) -> torch.Te
     k = expand_key(key)
     with torch.cuda.device(x.device):
         rc = _run(x, out, lambda ip, op: _lib().otc_aes_cfb128_decrypt(ip, op, _nbytes(x), ctypes.byref(k), _b16(iv, "iv"),
-            _stream(x)))
+            _stream(x)), inplace_ok=False)
     _native.check(rc, "otc_aes_cfb128_decrypt")
     return out

@@ -209,9 +209,15 @@ def test_errors_are_loud(gpu):
         ops.ecb_encrypt(x, os.urandom(16))  # not a multiple of 16
     with pytest.raises(ValueError):
         ops.ctr(x, os.urandom(15), os.urandom(16))
-    y = rnd(32, gpu)
-    with pytest.raises(RuntimeError):
-        ops.cbc_decrypt(y, os.urandom(16), os.urandom(16), out=y)  # in-place unsupported
+    y = rnd(64, gpu)
+    with pytest.raises(RuntimeError):  # partial overlap of input and output
+        ops.cbc_decrypt(y[:48], os.urandom(16), os.urandom(16), out=y[16:])
+    # exact in place is staged through a copy of the input (the kernel itself
+    # would overwrite ciphertext block i-1 before block i reads it)
+    key, iv = os.urandom(16), os.urandom(16)
+    ref = cpu_ref.cbc(key, iv, host(y), decrypt=True)
+    ops.cbc_decrypt(y, key, iv, out=y)
+    assert host(y) == ref
 
 
 @pytest.mark.parametrize("off_in,off_out", [(1, 0), (0, 3), (5, 5), (8, 8)])
