@@ -17,18 +17,50 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 namespace {
 
+/* U independent 16-byte loads per lane per trip (all issued before any
+ * store) keep more HBM requests in flight per wave than one; NT selects
+ * non-temporal loads/stores (once-touched data).  The variant is chosen at
+ * run time by k_xor() (A/B: profiles/r1/otbench_xor_variants.jsonl). */
+typedef uint32_t xu32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ xu32x4 xor_ld(const xu32x4 *p)
+{
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void xor_st(xu32x4 v, xu32x4 *p)
+{
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_xor_kernel(const uint8_t *a, const uint8_t *b, uint8_t *o, uint64_t n)
 {
     const uint64_t n16 = n / 16;
+    const xu32x4 *A = reinterpret_cast<const xu32x4 *>(a);
+    const xu32x4 *B = reinterpret_cast<const xu32x4 *>(b);
+    xu32x4 *O = reinterpret_cast<xu32x4 *>(o);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
-        uint4 x = reinterpret_cast<const uint4 *>(a)[i];
-        uint4 y = reinterpret_cast<const uint4 *>(b)[i];
-        reinterpret_cast<uint4 *>(o)[i] = make_uint4(x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w);
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    /* full trips: U strided elements per lane, all in range */
+    for (; i + (U - 1) * stride < n16; i += U * stride) {
+        xu32x4 x[U], y[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            x[u] = xor_ld<NT>(A + i + u * stride);
+            y[u] = xor_ld<NT>(B + i + u * stride);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) xor_st<NT>(x[u] ^ y[u], O + i + u * stride);
     }
+    for (; i < n16; i += stride) xor_st<NT>(xor_ld<NT>(A + i) ^ xor_ld<NT>(B + i), O + i);
     if (blockIdx.x == 0 && threadIdx.x < (n & 15)) {
         const uint64_t j = n16 * 16 + threadIdx.x;
         o[j] = a[j] ^ b[j];
@@ -294,7 +326,24 @@ hipError_t k_clock(uint64_t *out, uint64_t delay_ticks, uint64_t ticks, hipStrea
 
 hipError_t k_xor(const void *a, const void *b, void *out, size_t n, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_xor_kernel, dim3(grid_stream(n / 16, 8)), dim3(256), 0, st, (const uint8_t *)a,
+    /* OTC_XOR_VARIANT="U,per_cu,nt" (A/B only) */
+    static int U = 1, per_cu = 8, nt = 0;
+    static bool init = false;
+    if (!init) {
+        if (const char *e = getenv("OTC_XOR_VARIANT")) sscanf(e, "%d,%d,%d", &U, &per_cu, &nt);
+        if (U != 1 && U != 2 && U != 4 && U != 8) U = 1;
+        if (per_cu < 1 || per_cu > 64) per_cu = 8;
+        init = true;
+    }
+    auto kern = nt ? (U == 1   ? k_xor_kernel<1, true>
+                      : U == 2 ? k_xor_kernel<2, true>
+                      : U == 4 ? k_xor_kernel<4, true>
+                               : k_xor_kernel<8, true>)
+                   : (U == 1   ? k_xor_kernel<1, false>
+                      : U == 2 ? k_xor_kernel<2, false>
+                      : U == 4 ? k_xor_kernel<4, false>
+                               : k_xor_kernel<8, false>);
+    hipLaunchKernelGGL(kern, dim3(grid_stream(n / 16, per_cu)), dim3(256), 0, st, (const uint8_t *)a,
                        (const uint8_t *)b, (uint8_t *)out, (uint64_t)n);
     return hipGetLastError();
 }
