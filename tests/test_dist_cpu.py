@@ -1,5 +1,5 @@
 """One-process-per-rank data parallelism over torch.distributed with the gloo
-backend on CPU (world_size 2 and 3): sharded CTR, CBC-decrypt halo exchange
+backend on CPU (world sizes 1, 2, 3, 4 and 8): sharded CTR, CBC-decrypt halo exchange
 (ring send/recv) and root scatter/gather must equal the single-stream oracle.
 The same code runs with backend nccl (= RCCL) on MI355X GPUs."""
 import os
@@ -59,7 +59,7 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e)))
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
 def test_gloo_data_parallel(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
