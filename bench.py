@@ -148,7 +148,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_GBPS, 2),
-            "dtype": "bf16",
+            "dtype": "uint8",  # cipher engine: byte data, no floating-point compute
             "data": "synthetic random plaintext (splitmix64), random 128-bit key and counter",
             "config": {
                 "model": "AES-128-CTR",
@@ -168,7 +168,6 @@ def main():
             "verified_sample": True,
             **extra,
         }
-        line["dtype"] = "uint8"  # cipher engine: byte data (no floating-point compute)
         print(json.dumps(line), flush=True)
     if torch.distributed.is_initialized():
         torch.distributed.barrier()

@@ -1,0 +1,50 @@
+"""bench.py driver contract: one JSON line with the fields the round driver
+reads (metric/value/unit/n_gpus/steps/warmup/ms_per_step/...), the metric and
+config BASELINE.json names, and value consistent with ms_per_step.
+
+The GPU test runs the real headline step on a small shard (0.25 GiB instead of
+64 GiB, so it finishes in seconds); the CPU test only checks the CLI surface."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")
+
+
+def test_bench_cli_help():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    for flag in ("--gpus", "--steps", "--warmup"):
+        assert flag in r.stdout
+
+
+@pytest.mark.gpu
+def test_bench_json_line(gpu):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--gib", "0.25", "--no-clock", "--no-aes256", "--no-bitslice"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in REQUIRED:
+        assert k in d, k
+    assert d["metric"] == "GB/s AES-128-CTR (whole node)"
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1
+    assert d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert d["config"]["model"] == "AES-128-CTR" and d["config"]["parallelism"] == "dp1"
+    assert d["verified_sample"] is True
+    nbytes = d["config"]["per_gpu_bytes"]
+    assert nbytes == int(0.25 * (1 << 30))
+    # value (GB/s) and ms_per_step describe the same timed region
+    assert d["value"] == pytest.approx(nbytes / (d["ms_per_step"] * 1e-3) / 1e9, rel=0.01)
+    assert d["value"] > 100.0  # the HIP kernel ran (an eager fallback would be far slower)
