@@ -187,7 +187,14 @@ __device__ __forceinline__ void rc4_store16_any(const uint8_t *in, uint8_t *out,
  * issues at most one instruction per 4 cycles, and the corrections add half
  * again to the ~27 instructions per byte, which bound the loop with 2 waves
  * per SIMD more than the LDS latency does. */
-template <int MODE>
+/* i-aligned PRGA main loop (drop % 16 == 0): every 16-byte chunk starts at
+ * i = 16k, so S[i] of step q (i = 16k + q + 1) sits at a compile-time byte
+ * offset from one per-chunk lane address -- the i side of every step becomes a
+ * ds_read_u8 / ds_write_b8 immediate offset, with no SALU index arithmetic and
+ * no VALU address op (the loop is issue-bound at ~2 waves per SIMD). */
+__device__ __forceinline__ constexpr uint32_t rc4_ioff(int m) { return ((uint32_t)(m >> 2) << 8) | (uint32_t)(m & 3); }
+
+template <int MODE, bool ALIGNED>
 __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i, uint32_t j, uint64_t len,
                                                const uint8_t *in, uint8_t *out, uint64_t base, bool live)
 {
@@ -210,20 +217,53 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i,
         RC4_STEP(o);                                                                                           \
         w[q >> 2] |= o << (8 * (q & 3));                                                                       \
     }
+#define RC4_STEP_AT(O, SI, OFF)                                                                                \
+    do {                                                                                                       \
+        const uint32_t a_ = (SI)[OFF];                                                                         \
+        j = (j + a_) & 0xFFu;                                                                                  \
+        const uint32_t aj_ = sbox_addr(j, lane4);                                                              \
+        const uint32_t b_ = S[aj_];                                                                            \
+        (SI)[OFF] = (uint8_t)b_;                                                                               \
+        S[aj_] = (uint8_t)a_;                                                                                  \
+        O = S[sbox_addr(a_ + b_, lane4)];                                                                      \
+    } while (0)
+#define RC4_GEN16A(w)                                                                                          \
+    {                                                                                                          \
+        uint8_t *Sk = S + ((k << 10) | lane4);                                                                 \
+        k = (k + 1) & 15u;                                                                                     \
+        uint8_t *Sn = S + ((k << 10) | lane4);                                                                 \
+        _Pragma("unroll") for (int q = 0; q < 15; ++q)                                                         \
+        {                                                                                                      \
+            uint32_t o;                                                                                        \
+            RC4_STEP_AT(o, Sk, rc4_ioff(q + 1));                                                               \
+            w[q >> 2] |= o << (8 * (q & 3));                                                                   \
+        }                                                                                                      \
+        uint32_t o15;                                                                                          \
+        RC4_STEP_AT(o15, Sn, 0);                                                                               \
+        w[3] |= o15 << 24;                                                                                     \
+    }
     uint64_t m = 0;
-    RC4_MAIN_LOOP(16, RC4_GEN16)
+    if constexpr (ALIGNED) {
+        uint32_t k = (i >> 4) & 15u; /* i % 16 == 0 here (host checks drop % 16) */
+        RC4_MAIN_LOOP(16, RC4_GEN16A)
+        i = k << 4;
+    } else {
+        RC4_MAIN_LOOP(16, RC4_GEN16)
+    }
     for (; m < len; ++m) {
         uint32_t o;
         RC4_STEP(o);
         rc4_emit(in, out, base + m, o, live);
     }
+#undef RC4_GEN16A
+#undef RC4_STEP_AT
 #undef RC4_GEN16
 #undef RC4_STEP
 }
 
 #undef RC4_MAIN_LOOP
 
-template <int MODE>
+template <int MODE, bool ALIGNED>
 __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keylen, uint64_t nstreams, uint64_t len,
                                                    uint64_t drop, const uint8_t *in, uint8_t *out)
 {
@@ -267,7 +307,7 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     }
     const uint64_t base = (live ? sid : 0) * len;
     const uint8_t *src = MODE == RC4_KS ? nullptr : in;
-    rc4_prga<MODE>(S, lane4, i, j, len, src, out, base, live);
+    rc4_prga<MODE, ALIGNED>(S, lane4, i, j, len, src, out, base, live);
 }
 
 int g_cus_s = 0;
@@ -369,7 +409,15 @@ hipError_t k_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t 
     const uint64_t wgs = (nstreams + 63) / 64;
     const int mode = !in ? RC4_KS
                      : ((((uintptr_t)in | (uintptr_t)out) & 15u) == 0 && len % 16 == 0) ? RC4_VEC : RC4_ANY;
-    auto kern = mode == RC4_KS ? k_rc4_kernel<RC4_KS> : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC> : k_rc4_kernel<RC4_ANY>;
+    /* OTC_RC4_ALIGNED=0: generic index arithmetic (A/B only) */
+    static const bool allow_aligned = !getenv("OTC_RC4_ALIGNED") || atoi(getenv("OTC_RC4_ALIGNED")) != 0;
+    const bool al = allow_aligned && drop % 16 == 0;
+    auto kern = al ? (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, true>
+                      : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, true>
+                                        : k_rc4_kernel<RC4_ANY, true>)
+                   : (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, false>
+                      : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, false>
+                                        : k_rc4_kernel<RC4_ANY, false>);
     hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(64), 0, st, keys, keylen, (uint64_t)nstreams, (uint64_t)len,
                        (uint64_t)drop, (const uint8_t *)in, (uint8_t *)out);
     return hipGetLastError();
