@@ -194,7 +194,7 @@ __device__ __forceinline__ void rc4_store16_any(const uint8_t *in, uint8_t *out,
  * no VALU address op (the loop is issue-bound at ~2 waves per SIMD). */
 __device__ __forceinline__ constexpr uint32_t rc4_ioff(int m) { return ((uint32_t)(m >> 2) << 8) | (uint32_t)(m & 3); }
 
-template <int MODE, bool ALIGNED>
+template <int MODE, int AL>
 __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i, uint32_t j, uint64_t len,
                                                const uint8_t *in, uint8_t *out, uint64_t base, bool live)
 {
@@ -242,10 +242,42 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i,
         RC4_STEP_AT(o15, Sn, 0);                                                                               \
         w[3] |= o15 << 24;                                                                                     \
     }
+    /* AL == 2 (default): S[i+1] read ahead together with S[j], before the swap
+ * writes, and corrected when the swap moved it (i + 1 == j -> a), so the j
+ * chain carries one LDS round trip per byte instead of two. */
+#define RC4_GEN16P(w)                                                                                          \
+    {                                                                                                          \
+        uint8_t *Sk = S + ((k << 10) | lane4);                                                                 \
+        const uint32_t ib = k << 4;                                                                            \
+        k = (k + 1) & 15u;                                                                                     \
+        uint8_t *Sn = S + ((k << 10) | lane4);                                                                 \
+        const uint32_t nb = k << 4;                                                                            \
+        _Pragma("unroll") for (int q = 0; q < 16; ++q)                                                         \
+        {                                                                                                      \
+            uint8_t *si_ = q < 15 ? Sk + rc4_ioff(q + 1) : Sn;                                                 \
+            uint8_t *sp_ = q < 14 ? Sk + rc4_ioff(q + 2) : (q == 14 ? Sn : Sn + 1);                            \
+            const uint32_t a_ = an;                                                                            \
+            j = (j + a_) & 0xFFu;                                                                              \
+            const uint32_t aj_ = sbox_addr(j, lane4);                                                          \
+            const uint32_t b_ = S[aj_];                                                                        \
+            const uint32_t pn_ = *sp_;                                                                         \
+            const uint32_t inx_ = q < 14 ? ib + (uint32_t)(q + 2) : nb + (uint32_t)(q - 14);                   \
+            an = (j == inx_) ? a_ : pn_;                                                                       \
+            *si_ = (uint8_t)b_;                                                                                \
+            S[aj_] = (uint8_t)a_;                                                                              \
+            const uint32_t o_ = S[sbox_addr(a_ + b_, lane4)];                                                  \
+            w[q >> 2] |= o_ << (8 * (q & 3));                                                                  \
+        }                                                                                                      \
+    }
     uint64_t m = 0;
-    if constexpr (ALIGNED) {
+    if constexpr (AL == 1) {
         uint32_t k = (i >> 4) & 15u; /* i % 16 == 0 here (host checks drop % 16) */
         RC4_MAIN_LOOP(16, RC4_GEN16A)
+        i = k << 4;
+    } else if constexpr (AL == 2) {
+        uint32_t k = (i >> 4) & 15u;
+        uint32_t an = S[((k << 10) | lane4) + 1]; /* S[i + 1] */
+        RC4_MAIN_LOOP(16, RC4_GEN16P)
         i = k << 4;
     } else {
         RC4_MAIN_LOOP(16, RC4_GEN16)
@@ -255,6 +287,7 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i,
         RC4_STEP(o);
         rc4_emit(in, out, base + m, o, live);
     }
+#undef RC4_GEN16P
 #undef RC4_GEN16A
 #undef RC4_STEP_AT
 #undef RC4_GEN16
@@ -263,7 +296,7 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i,
 
 #undef RC4_MAIN_LOOP
 
-template <int MODE, bool ALIGNED>
+template <int MODE, int AL>
 __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keylen, uint64_t nstreams, uint64_t len,
                                                    uint64_t drop, const uint8_t *in, uint8_t *out)
 {
@@ -307,7 +340,7 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     }
     const uint64_t base = (live ? sid : 0) * len;
     const uint8_t *src = MODE == RC4_KS ? nullptr : in;
-    rc4_prga<MODE, ALIGNED>(S, lane4, i, j, len, src, out, base, live);
+    rc4_prga<MODE, AL>(S, lane4, i, j, len, src, out, base, live);
 }
 
 int g_cus_s = 0;
@@ -409,15 +442,19 @@ hipError_t k_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t 
     const uint64_t wgs = (nstreams + 63) / 64;
     const int mode = !in ? RC4_KS
                      : ((((uintptr_t)in | (uintptr_t)out) & 15u) == 0 && len % 16 == 0) ? RC4_VEC : RC4_ANY;
-    /* OTC_RC4_ALIGNED=0: generic index arithmetic (A/B only) */
-    static const bool allow_aligned = !getenv("OTC_RC4_ALIGNED") || atoi(getenv("OTC_RC4_ALIGNED")) != 0;
-    const bool al = allow_aligned && drop % 16 == 0;
-    auto kern = al ? (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, true>
-                      : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, true>
-                                        : k_rc4_kernel<RC4_ANY, true>)
-                   : (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, false>
-                      : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, false>
-                                        : k_rc4_kernel<RC4_ANY, false>);
+    /* default (2): i-aligned + S[i+1] read-ahead; OTC_RC4_ALIGNED=1: aligned
+     * only, 0: generic index arithmetic (A/B: profiles/r1/otbench_rc4_readahead_ab.jsonl) */
+    static const int al_mode = getenv("OTC_RC4_ALIGNED") ? atoi(getenv("OTC_RC4_ALIGNED")) : 2;
+    const int al = drop % 16 == 0 ? (al_mode == 2 ? 2 : al_mode != 0 ? 1 : 0) : 0;
+    auto kern = al == 2   ? (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 2>
+                             : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, 2>
+                                               : k_rc4_kernel<RC4_ANY, 2>)
+                : al == 1 ? (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 1>
+                             : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, 1>
+                                               : k_rc4_kernel<RC4_ANY, 1>)
+                          : (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 0>
+                             : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, 0>
+                                               : k_rc4_kernel<RC4_ANY, 0>);
     hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(64), 0, st, keys, keylen, (uint64_t)nstreams, (uint64_t)len,
                        (uint64_t)drop, (const uint8_t *)in, (uint8_t *)out);
     return hipGetLastError();
