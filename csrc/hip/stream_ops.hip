@@ -109,6 +109,19 @@ __device__ __forceinline__ uint32_t sbox_addr(uint32_t x, uint32_t lane4)
     return t | (x & 3u) | lane4;
 }
 
+/* RC4 S-box address, two layouts (kernel template AL >= 3 selects BL):
+ *   BL = false: byte x of lane l at ((x>>2)<<8) | l<<2 | (x&3) -- every lane
+ *               owns a bank (conflict-free), 3 VALU per address;
+ *   BL = true:  byte x of lane l at (x<<6) | l -- 1-2 VALU per address; the 4
+ *               lanes of a dword share a bank, so equal x&3 with different
+ *               rows conflict (~2-way on random data).
+ * `lt` is the lane term (l<<2 or l). */
+template <bool BL>
+__device__ __forceinline__ uint32_t rc4_addr(uint32_t x, uint32_t lt)
+{
+    return BL ? (((x & 0xFFu) << 6) | lt) : sbox_addr(x, lt);
+}
+
 /* Output modes: RC4_KS = keystream only (no input); RC4_VEC = input, in/out
  * 16-byte aligned and len a multiple of 16 (host-checked), so every lane
  * uses 16-byte accesses and the input chunk is loaded one chunk ahead;
@@ -192,23 +205,28 @@ __device__ __forceinline__ void rc4_store16_any(const uint8_t *in, uint8_t *out,
  * offset from one per-chunk lane address -- the i side of every step becomes a
  * ds_read_u8 / ds_write_b8 immediate offset, with no SALU index arithmetic and
  * no VALU address op (the loop is issue-bound at ~2 waves per SIMD). */
-__device__ __forceinline__ constexpr uint32_t rc4_ioff(int m) { return ((uint32_t)(m >> 2) << 8) | (uint32_t)(m & 3); }
+template <bool BL>
+__device__ __forceinline__ constexpr uint32_t rc4_ioff(int m)
+{
+    return BL ? (uint32_t)m << 6 : ((uint32_t)(m >> 2) << 8) | (uint32_t)(m & 3);
+}
 
 template <int MODE, int AL>
 __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i, uint32_t j, uint64_t len,
                                                const uint8_t *in, uint8_t *out, uint64_t base, bool live)
 {
+    constexpr bool BL = AL >= 3;
 #define RC4_STEP(O)                                                                                            \
     do {                                                                                                       \
         i = (i + 1) & 0xFFu;                                                                                   \
-        const uint32_t ai_ = sbox_addr(i, lane4);                                                              \
+        const uint32_t ai_ = rc4_addr<BL>(i, lane4);                                                              \
         const uint32_t a_ = S[ai_];                                                                            \
         j = (j + a_) & 0xFFu;                                                                                  \
-        const uint32_t aj_ = sbox_addr(j, lane4);                                                              \
+        const uint32_t aj_ = rc4_addr<BL>(j, lane4);                                                              \
         const uint32_t b_ = S[aj_];                                                                            \
         S[ai_] = (uint8_t)b_;                                                                                  \
         S[aj_] = (uint8_t)a_;                                                                                  \
-        O = S[sbox_addr(a_ + b_, lane4)];                                                                      \
+        O = S[rc4_addr<BL>(a_ + b_, lane4)];                                                                      \
     } while (0)
 #define RC4_GEN16(w)                                                                                           \
     _Pragma("unroll") for (int q = 0; q < 16; ++q)                                                             \
@@ -221,11 +239,11 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i,
     do {                                                                                                       \
         const uint32_t a_ = (SI)[OFF];                                                                         \
         j = (j + a_) & 0xFFu;                                                                                  \
-        const uint32_t aj_ = sbox_addr(j, lane4);                                                              \
+        const uint32_t aj_ = rc4_addr<BL>(j, lane4);                                                              \
         const uint32_t b_ = S[aj_];                                                                            \
         (SI)[OFF] = (uint8_t)b_;                                                                               \
         S[aj_] = (uint8_t)a_;                                                                                  \
-        O = S[sbox_addr(a_ + b_, lane4)];                                                                      \
+        O = S[rc4_addr<BL>(a_ + b_, lane4)];                                                                      \
     } while (0)
 #define RC4_GEN16A(w)                                                                                          \
     {                                                                                                          \
@@ -235,7 +253,7 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i,
         _Pragma("unroll") for (int q = 0; q < 15; ++q)                                                         \
         {                                                                                                      \
             uint32_t o;                                                                                        \
-            RC4_STEP_AT(o, Sk, rc4_ioff(q + 1));                                                               \
+            RC4_STEP_AT(o, Sk, rc4_ioff<BL>(q + 1));                                                               \
             w[q >> 2] |= o << (8 * (q & 3));                                                                   \
         }                                                                                                      \
         uint32_t o15;                                                                                          \
@@ -254,18 +272,18 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i,
         const uint32_t nb = k << 4;                                                                            \
         _Pragma("unroll") for (int q = 0; q < 16; ++q)                                                         \
         {                                                                                                      \
-            uint8_t *si_ = q < 15 ? Sk + rc4_ioff(q + 1) : Sn;                                                 \
-            uint8_t *sp_ = q < 14 ? Sk + rc4_ioff(q + 2) : (q == 14 ? Sn : Sn + 1);                            \
+            uint8_t *si_ = q < 15 ? Sk + rc4_ioff<BL>(q + 1) : Sn;                                                 \
+            uint8_t *sp_ = q < 14 ? Sk + rc4_ioff<BL>(q + 2) : (q == 14 ? Sn : Sn + rc4_ioff<BL>(1));                            \
             const uint32_t a_ = an;                                                                            \
             j = (j + a_) & 0xFFu;                                                                              \
-            const uint32_t aj_ = sbox_addr(j, lane4);                                                          \
+            const uint32_t aj_ = rc4_addr<BL>(j, lane4);                                                          \
             const uint32_t b_ = S[aj_];                                                                        \
             const uint32_t pn_ = *sp_;                                                                         \
             const uint32_t inx_ = q < 14 ? ib + (uint32_t)(q + 2) : nb + (uint32_t)(q - 14);                   \
             an = (j == inx_) ? a_ : pn_;                                                                       \
             *si_ = (uint8_t)b_;                                                                                \
             S[aj_] = (uint8_t)a_;                                                                              \
-            const uint32_t o_ = S[sbox_addr(a_ + b_, lane4)];                                                  \
+            const uint32_t o_ = S[rc4_addr<BL>(a_ + b_, lane4)];                                                  \
             w[q >> 2] |= o_ << (8 * (q & 3));                                                                  \
         }                                                                                                      \
     }
@@ -274,9 +292,9 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i,
         uint32_t k = (i >> 4) & 15u; /* i % 16 == 0 here (host checks drop % 16) */
         RC4_MAIN_LOOP(16, RC4_GEN16A)
         i = k << 4;
-    } else if constexpr (AL == 2) {
+    } else if constexpr (AL >= 2) {
         uint32_t k = (i >> 4) & 15u;
-        uint32_t an = S[((k << 10) | lane4) + 1]; /* S[i + 1] */
+        uint32_t an = S[((k << 10) | lane4) + rc4_ioff<BL>(1)]; /* S[i + 1] */
         RC4_MAIN_LOOP(16, RC4_GEN16P)
         i = k << 4;
     } else {
@@ -302,24 +320,32 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
 {
     __shared__ __attribute__((aligned(16))) uint8_t S[64 * 256];
     const uint32_t lane = threadIdx.x;
-    const uint32_t lane4 = lane << 2;
+    constexpr bool BL = AL >= 3;
+    const uint32_t lane4 = BL ? lane : lane << 2; /* lane term of rc4_addr */
     const uint64_t sid = (uint64_t)blockIdx.x * 64 + lane;
     const bool live = sid < nstreams;
 
-    /* identity permutation: dword q of lane l = bytes 4q..4q+3 */
-    for (uint32_t q = 0; q < 64; ++q)
-        *reinterpret_cast<uint32_t *>(S + ((q << 8) | lane4)) = 0x03020100u + 0x04040404u * q;
+    if (BL) {
+        /* identity permutation: row x (64 bytes, one per lane) = x */
+        for (uint32_t q = lane; q < 64 * 256 / 4; q += 64)
+            reinterpret_cast<uint32_t *>(S)[q] = (q >> 4) * 0x01010101u;
+        __syncthreads();
+    } else {
+        /* identity permutation: dword q of lane l = bytes 4q..4q+3 */
+        for (uint32_t q = 0; q < 64; ++q)
+            *reinterpret_cast<uint32_t *>(S + ((q << 8) | lane4)) = 0x03020100u + 0x04040404u * q;
+    }
 
     /* KSA (reference arc4.c:43-67) */
     const uint8_t *key = keys + (live ? sid : 0) * (uint64_t)keylen;
     uint32_t j = 0;
     int kpos = 0;
     for (uint32_t i = 0; i < 256; ++i) {
-        const uint32_t ai = sbox_addr(i, lane4);
+        const uint32_t ai = rc4_addr<BL>(i, lane4);
         const uint32_t a = S[ai];
         j = (j + a + key[kpos]) & 0xFFu;
         if (++kpos == keylen) kpos = 0;
-        const uint32_t aj = sbox_addr(j, lane4);
+        const uint32_t aj = rc4_addr<BL>(j, lane4);
         const uint32_t b = S[aj];
         S[ai] = (uint8_t)b;
         S[aj] = (uint8_t)a;
@@ -330,10 +356,10 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     j = 0;
     for (uint64_t n = 0; n < drop; ++n) {
         i = (i + 1) & 0xFFu;
-        const uint32_t ai = sbox_addr(i, lane4);
+        const uint32_t ai = rc4_addr<BL>(i, lane4);
         const uint32_t a = S[ai];
         j = (j + a) & 0xFFu;
-        const uint32_t aj = sbox_addr(j, lane4);
+        const uint32_t aj = rc4_addr<BL>(j, lane4);
         const uint32_t b = S[aj];
         S[ai] = (uint8_t)b;
         S[aj] = (uint8_t)a;
@@ -443,10 +469,15 @@ hipError_t k_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t 
     const int mode = !in ? RC4_KS
                      : ((((uintptr_t)in | (uintptr_t)out) & 15u) == 0 && len % 16 == 0) ? RC4_VEC : RC4_ANY;
     /* default (2): i-aligned + S[i+1] read-ahead; OTC_RC4_ALIGNED=1: aligned
-     * only, 0: generic index arithmetic (A/B: profiles/r1/otbench_rc4_readahead_ab.jsonl) */
+     * only, 0: generic index arithmetic (A/B: profiles/r1/otbench_rc4_readahead_ab.jsonl),
+     * 3: read-ahead on the byte-interleaved layout (measured slower:
+     * profiles/r1/otbench_rc4_bytelayout_negative.jsonl) */
     static const int al_mode = getenv("OTC_RC4_ALIGNED") ? atoi(getenv("OTC_RC4_ALIGNED")) : 2;
-    const int al = drop % 16 == 0 ? (al_mode == 2 ? 2 : al_mode != 0 ? 1 : 0) : 0;
-    auto kern = al == 2   ? (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 2>
+    const int al = drop % 16 == 0 ? (al_mode == 3 ? 3 : al_mode == 2 ? 2 : al_mode != 0 ? 1 : 0) : 0;
+    auto kern = al == 3   ? (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 3>
+                             : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, 3>
+                                               : k_rc4_kernel<RC4_ANY, 3>)
+                : al == 2 ? (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 2>
                              : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, 2>
                                                : k_rc4_kernel<RC4_ANY, 2>)
                 : al == 1 ? (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 1>
