@@ -10,7 +10,8 @@ import sys
 
 
 def summarize(path: str) -> str:
-    db = sqlite3.connect(path)
+    # read-only: a mistyped path must not create an empty database file
+    db = sqlite3.connect(f"file:{path}?mode=ro", uri=True)
     rows = list(db.execute(
         "select name, count(*), sum(duration), avg(duration), min(duration), max(duration), "
         "max(grid_x), max(workgroup_x), max(vgpr_count), max(accum_vgpr_count), max(sgpr_count), "
@@ -26,5 +27,8 @@ def summarize(path: str) -> str:
 
 
 if __name__ == "__main__":
+    if len(sys.argv) < 2 or sys.argv[1] in ("-h", "--help"):
+        sys.stdout.write(__doc__)
+        sys.exit(0)
     for p in sys.argv[1:]:
         sys.stdout.write(summarize(p))
