@@ -486,7 +486,15 @@ hipError_t k_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t 
                           : (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 0>
                              : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, 0>
                                                : k_rc4_kernel<RC4_ANY, 0>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(64), 0, st, keys, keylen, (uint64_t)nstreams, (uint64_t)len,
+    /* OTC_RC4_WG_PER_CU=N caps resident workgroups per CU at N by reserving
+     * unused dynamic LDS (each holds 16 KiB of S-boxes; 160 KiB per CU). */
+    static const int wg_cap = getenv("OTC_RC4_WG_PER_CU") ? atoi(getenv("OTC_RC4_WG_PER_CU")) : 0;
+    size_t dyn_lds = 0;
+    if (wg_cap >= 1 && wg_cap < 10) {
+        const size_t per_wg = (160u * 1024u / (size_t)wg_cap) & ~(size_t)1023;
+        dyn_lds = per_wg - 64u * 256u;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(64), dyn_lds, st, keys, keylen, (uint64_t)nstreams, (uint64_t)len,
                        (uint64_t)drop, (const uint8_t *)in, (uint8_t *)out);
     return hipGetLastError();
 }
