@@ -486,9 +486,19 @@ hipError_t k_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t 
                           : (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 0>
                              : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, 0>
                                                : k_rc4_kernel<RC4_ANY, 0>);
-    /* OTC_RC4_WG_PER_CU=N caps resident workgroups per CU at N by reserving
-     * unused dynamic LDS (each holds 16 KiB of S-boxes; 160 KiB per CU). */
-    static const int wg_cap = getenv("OTC_RC4_WG_PER_CU") ? atoi(getenv("OTC_RC4_WG_PER_CU")) : 0;
+    /* Resident-workgroup cap per CU, by reserving unused dynamic LDS (each
+     * workgroup holds 16 KiB of S-boxes; 160 KiB per CU).  Measured
+     * (profiles/r1/otbench_rc4_wgcap_ab.jsonl, otbench_rc4_cap10_ab.jsonl):
+     * a launch that would put all 10 per CU in one round runs 563 GB/s, the
+     * same work in two rounds of <= 6 per CU 690 GB/s; every other shape is
+     * best uncapped.  OTC_RC4_WG_PER_CU=N forces cap N (0: never cap). */
+    static const int wg_env = getenv("OTC_RC4_WG_PER_CU") ? atoi(getenv("OTC_RC4_WG_PER_CU")) : -1;
+    int wg_cap = wg_env;
+    if (wg_env < 0) {
+        (void)grid_stream(1, 1); /* initialises the CU count */
+        const uint64_t cus = (uint64_t)g_cus_s;
+        wg_cap = (wgs > 9 * cus && wgs <= 10 * cus) ? 6 : 0;
+    }
     size_t dyn_lds = 0;
     if (wg_cap >= 1 && wg_cap < 10) {
         const size_t per_wg = (160u * 1024u / (size_t)wg_cap) & ~(size_t)1023;

@@ -192,6 +192,21 @@ def test_rc4_multi(gpu, keylen, length, drop):
     assert torch.equal(y, x ^ ks)
 
 
+def test_rc4_multi_capped_launch(gpu):
+    """10 workgroups (640 streams) per CU: the launch that reserves extra LDS
+    to cap residency at 6 per CU (two rounds); sampled streams vs the oracle,
+    first, last and strided"""
+    ns = torch.cuda.get_device_properties(0).multi_processor_count * 640
+    length = 48
+    keys = rnd(ns * 16, gpu, 11).view(ns, 16)
+    ks = ops.rc4_multi(keys, length)
+    torch.cuda.synchronize()
+    kh = keys.cpu().numpy()
+    kso = ks.cpu().numpy()
+    for s in list(range(0, ns, 997)) + [ns - 1]:
+        assert kso[s].tobytes() == cpu_ref.arc4_keystream(bytes(kh[s]), length), s
+
+
 def test_fill_and_checksum(gpu):
     a = torch.empty(1 << 20, dtype=torch.uint8, device=gpu)
     b = torch.empty(1 << 20, dtype=torch.uint8, device=gpu)
