@@ -316,7 +316,7 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i,
 
 template <int MODE, int AL>
 __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keylen, uint64_t nstreams, uint64_t len,
-                                                   uint64_t drop, const uint8_t *in, uint8_t *out)
+                                                   uint64_t drop, const uint8_t *in, uint8_t *out, int ksa16)
 {
     __shared__ __attribute__((aligned(16))) uint8_t S[64 * 256];
     const uint32_t lane = threadIdx.x;
@@ -339,16 +339,38 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     /* KSA (reference arc4.c:43-67) */
     const uint8_t *key = keys + (live ? sid : 0) * (uint64_t)keylen;
     uint32_t j = 0;
-    int kpos = 0;
-    for (uint32_t i = 0; i < 256; ++i) {
-        const uint32_t ai = rc4_addr<BL>(i, lane4);
-        const uint32_t a = S[ai];
-        j = (j + a + key[kpos]) & 0xFFu;
-        if (++kpos == keylen) kpos = 0;
-        const uint32_t aj = rc4_addr<BL>(j, lane4);
-        const uint32_t b = S[aj];
-        S[ai] = (uint8_t)b;
-        S[aj] = (uint8_t)a;
+    if (keylen == 16 && ksa16) {
+        /* 16-byte keys: the key is loaded once into registers (one byte per
+         * VGPR, all 16 loads in flight together) instead of one dependent
+         * global byte load per KSA step, and i runs in 16-step chunks whose
+         * S[i] accesses are LDS immediate offsets. */
+        uint32_t kb[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) kb[q] = key[q];
+        for (uint32_t c = 0; c < 16; ++c) {
+            uint8_t *Sc = S + ((c << 10) | lane4);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const uint32_t a = Sc[rc4_ioff<BL>(q)];
+                j = (j + a + kb[q]) & 0xFFu;
+                const uint32_t aj = rc4_addr<BL>(j, lane4);
+                const uint32_t b = S[aj];
+                Sc[rc4_ioff<BL>(q)] = (uint8_t)b;
+                S[aj] = (uint8_t)a;
+            }
+        }
+    } else {
+        int kpos = 0;
+        for (uint32_t i = 0; i < 256; ++i) {
+            const uint32_t ai = rc4_addr<BL>(i, lane4);
+            const uint32_t a = S[ai];
+            j = (j + a + key[kpos]) & 0xFFu;
+            if (++kpos == keylen) kpos = 0;
+            const uint32_t aj = rc4_addr<BL>(j, lane4);
+            const uint32_t b = S[aj];
+            S[ai] = (uint8_t)b;
+            S[aj] = (uint8_t)a;
+        }
     }
 
     /* RC4-drop: discard the first `drop` keystream bytes */
@@ -499,13 +521,15 @@ hipError_t k_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t 
         const uint64_t cus = (uint64_t)g_cus_s;
         wg_cap = (wgs > 9 * cus && wgs <= 10 * cus) ? 6 : 0;
     }
+    /* OTC_RC4_KSA16=0: generic KSA for 16-byte keys too (A/B only) */
+    static const int ksa16 = !getenv("OTC_RC4_KSA16") || atoi(getenv("OTC_RC4_KSA16")) != 0;
     size_t dyn_lds = 0;
     if (wg_cap >= 1 && wg_cap < 10) {
         const size_t per_wg = (160u * 1024u / (size_t)wg_cap) & ~(size_t)1023;
         dyn_lds = per_wg - 64u * 256u;
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(64), dyn_lds, st, keys, keylen, (uint64_t)nstreams, (uint64_t)len,
-                       (uint64_t)drop, (const uint8_t *)in, (uint8_t *)out);
+                       (uint64_t)drop, (const uint8_t *)in, (uint8_t *)out, ksa16);
     return hipGetLastError();
 }
 
