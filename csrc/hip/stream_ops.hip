@@ -376,7 +376,27 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     /* RC4-drop: discard the first `drop` keystream bytes */
     uint32_t i = 0;
     j = 0;
-    for (uint64_t n = 0; n < drop; ++n) {
+    uint64_t n = 0;
+    if constexpr (AL >= 1) {
+        /* drop % 16 == 0 here (host): 16-step chunks, i = 16c + q + 1, S[i]
+         * at immediate offsets (the last step of a chunk wraps into c + 1) */
+        for (uint32_t c = 0; n < drop; n += 16, c = (c + 1) & 15u) {
+            uint8_t *Sc = S + ((c << 10) | lane4);
+            uint8_t *Sn = S + ((((c + 1) & 15u) << 10) | lane4);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                uint8_t *si = q < 15 ? Sc + rc4_ioff<BL>(q + 1) : Sn;
+                const uint32_t a = *si;
+                j = (j + a) & 0xFFu;
+                const uint32_t aj = rc4_addr<BL>(j, lane4);
+                const uint32_t b = S[aj];
+                *si = (uint8_t)b;
+                S[aj] = (uint8_t)a;
+            }
+        }
+        i = (uint32_t)(drop & 0xFFu);
+    }
+    for (; n < drop; ++n) {
         i = (i + 1) & 0xFFu;
         const uint32_t ai = rc4_addr<BL>(i, lane4);
         const uint32_t a = S[ai];
