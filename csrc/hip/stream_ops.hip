@@ -339,26 +339,40 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     /* KSA (reference arc4.c:43-67) */
     const uint8_t *key = keys + (live ? sid : 0) * (uint64_t)keylen;
     uint32_t j = 0;
-    if (keylen == 16 && ksa16) {
-        /* 16-byte keys: the key is loaded once into registers (one byte per
-         * VGPR, all 16 loads in flight together) instead of one dependent
-         * global byte load per KSA step, and i runs in 16-step chunks whose
-         * S[i] accesses are LDS immediate offsets. */
-        uint32_t kb[16];
+    if (ksa16 && (keylen == 1 || keylen == 2 || keylen == 4 || keylen == 8 || keylen == 16 || keylen == 32)) {
+        /* key lengths dividing 32: the key is loaded once into registers (one
+         * byte per VGPR, all loads in flight together) instead of one
+         * dependent global byte load per KSA step, and i runs in 16-step
+         * chunks whose S[i] accesses are LDS immediate offsets. */
+#define RC4_KSA_CHUNK(C, KB)                                                                                   \
+    {                                                                                                          \
+        uint8_t *Sc = S + (((uint32_t)(C) << 10) | lane4);                                                     \
+        _Pragma("unroll") for (int q = 0; q < 16; ++q)                                                         \
+        {                                                                                                      \
+            const uint32_t a = Sc[rc4_ioff<BL>(q)];                                                            \
+            j = (j + a + (KB)[q]) & 0xFFu;                                                                     \
+            const uint32_t aj = rc4_addr<BL>(j, lane4);                                                        \
+            const uint32_t b = S[aj];                                                                          \
+            Sc[rc4_ioff<BL>(q)] = (uint8_t)b;                                                                  \
+            S[aj] = (uint8_t)a;                                                                                \
+        }                                                                                                      \
+    }
+        if (keylen == 32) {
+            uint32_t kb[32];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) kb[q] = key[q];
-        for (uint32_t c = 0; c < 16; ++c) {
-            uint8_t *Sc = S + ((c << 10) | lane4);
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const uint32_t a = Sc[rc4_ioff<BL>(q)];
-                j = (j + a + kb[q]) & 0xFFu;
-                const uint32_t aj = rc4_addr<BL>(j, lane4);
-                const uint32_t b = S[aj];
-                Sc[rc4_ioff<BL>(q)] = (uint8_t)b;
-                S[aj] = (uint8_t)a;
+            for (int q = 0; q < 32; ++q) kb[q] = key[q];
+            for (uint32_t c = 0; c < 16; c += 2) {
+                RC4_KSA_CHUNK(c, kb)
+                RC4_KSA_CHUNK(c + 1, kb + 16)
             }
+        } else {
+            const uint32_t km = (uint32_t)keylen - 1u;
+            uint32_t kb[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) kb[q] = key[(uint32_t)q & km];
+            for (uint32_t c = 0; c < 16; ++c) RC4_KSA_CHUNK(c, kb)
         }
+#undef RC4_KSA_CHUNK
     } else {
         int kpos = 0;
         for (uint32_t i = 0; i < 256; ++i) {
@@ -541,7 +555,7 @@ hipError_t k_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t 
         const uint64_t cus = (uint64_t)g_cus_s;
         wg_cap = (wgs > 9 * cus && wgs <= 10 * cus) ? 6 : 0;
     }
-    /* OTC_RC4_KSA16=0: generic KSA for 16-byte keys too (A/B only) */
+    /* OTC_RC4_KSA16=0: generic KSA for every key length (A/B only) */
     static const int ksa16 = !getenv("OTC_RC4_KSA16") || atoi(getenv("OTC_RC4_KSA16")) != 0;
     size_t dyn_lds = 0;
     if (wg_cap >= 1 && wg_cap < 10) {
