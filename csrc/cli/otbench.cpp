@@ -9,7 +9,7 @@
  *           [--e2e --chunk 256M]            host-resident, pinned pipeline
  *           [--gpus N --strategy direct|rccl] single-process multi-GPU (e2e)
  *           [--seg 4096]                    CBC segment size
- *           [--streams 65536 --len 4096]    RC4 many-stream shape
+ *           [--streams 65536 --len 4096 --keylen 16 --drop 0]    RC4 many-stream shape
  *
  * Kernel-only numbers come from hipEvents around `iters` back-to-back launches
  * on resident data (no allocation, no copies in the timed region: contrast the
@@ -52,7 +52,7 @@ struct Cfg {
     size_t chunk = 256ull << 20;
     int gpus = 1, strategy = 0;
     size_t seg = 4096;
-    size_t streams = 65536, len = 4096;
+    size_t streams = 65536, len = 4096, keylen = 16, drop = 0;
 };
 
 struct OpArg {
@@ -74,7 +74,7 @@ static int run_op(void *p)
         return otc_aes_cbc_encrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
     if (c.mode == "cfb-dec") return otc_aes_cfb128_decrypt(a->in, a->out, c.bytes, a->k, a->iv, nullptr);
     if (c.mode == "xor") return otc_xor(a->in, a->out, a->out, c.bytes, nullptr);
-    if (c.mode == "rc4") return otc_rc4_multi(a->keys, 16, c.streams, c.len, 0, a->in, a->out, nullptr);
+    if (c.mode == "rc4") return otc_rc4_multi(a->keys, (int)c.keylen, c.streams, c.len, c.drop, a->in, a->out, nullptr);
     return OTC_ERR_ARG;
 }
 
@@ -139,6 +139,8 @@ int main(int argc, char **argv)
         else if (a == "--seg") c.seg = parse_size(nx());
         else if (a == "--streams") c.streams = parse_size(nx());
         else if (a == "--len") c.len = parse_size(nx());
+        else if (a == "--keylen") c.keylen = parse_size(nx());
+        else if (a == "--drop") c.drop = parse_size(nx());
         else {
             fprintf(stderr, "unknown option %s\n", a.c_str());
             return 2;
@@ -212,8 +214,8 @@ int main(int argc, char **argv)
     otc_fill_random(a.in, c.bytes, 42, nullptr);
     if (!c.inplace) otc_fill_random(a.out, c.bytes, 43, nullptr);
     if (c.mode == "rc4") {
-        a.keys = (uint8_t *)otc_dev_malloc(c.streams * 16);
-        otc_fill_random(a.keys, c.streams * 16, 44, nullptr);
+        a.keys = (uint8_t *)otc_dev_malloc(c.streams * c.keylen);
+        otc_fill_random(a.keys, c.streams * c.keylen, 44, nullptr);
     }
     otc_device_sync();
     bool ok = true;
