@@ -347,16 +347,31 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
 #define RC4_KSA_CHUNK(C, KB)                                                                                   \
     {                                                                                                          \
         uint8_t *Sc = S + (((uint32_t)(C) << 10) | lane4);                                                     \
+        uint8_t *Sn = S + (((((uint32_t)(C) + 1u) & 15u) << 10) | lane4);                                      \
+        const uint32_t ib = (uint32_t)(C) << 4;                                                                \
         _Pragma("unroll") for (int q = 0; q < 16; ++q)                                                         \
         {                                                                                                      \
-            const uint32_t a = Sc[rc4_ioff<BL>(q)];                                                            \
-            j = (j + a + (KB)[q]) & 0xFFu;                                                                     \
-            const uint32_t aj = rc4_addr<BL>(j, lane4);                                                        \
-            const uint32_t b = S[aj];                                                                          \
-            Sc[rc4_ioff<BL>(q)] = (uint8_t)b;                                                                  \
-            S[aj] = (uint8_t)a;                                                                                \
+            if constexpr (AL >= 2) { /* S[i+1] read ahead, fixed up when the swap moved it */                 \
+                const uint32_t a = an;                                                                         \
+                j = (j + a + (KB)[q]) & 0xFFu;                                                                 \
+                const uint32_t aj = rc4_addr<BL>(j, lane4);                                                    \
+                const uint32_t b = S[aj];                                                                      \
+                const uint32_t pn = q < 15 ? Sc[rc4_ioff<BL>(q + 1)] : Sn[0];                                  \
+                an = (j == ((ib + (uint32_t)q + 1u) & 0xFFu)) ? a : pn;                                        \
+                Sc[rc4_ioff<BL>(q)] = (uint8_t)b;                                                              \
+                S[aj] = (uint8_t)a;                                                                            \
+            } else {                                                                                           \
+                const uint32_t a = Sc[rc4_ioff<BL>(q)];                                                        \
+                j = (j + a + (KB)[q]) & 0xFFu;                                                                 \
+                const uint32_t aj = rc4_addr<BL>(j, lane4);                                                    \
+                const uint32_t b = S[aj];                                                                      \
+                Sc[rc4_ioff<BL>(q)] = (uint8_t)b;                                                              \
+                S[aj] = (uint8_t)a;                                                                            \
+            }                                                                                                  \
         }                                                                                                      \
     }
+        uint32_t an = S[lane4]; /* S[0] */
+        (void)an;
         if (keylen == 32) {
             uint32_t kb[32];
 #pragma unroll
@@ -394,18 +409,34 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     if constexpr (AL >= 1) {
         /* drop % 16 == 0 here (host): 16-step chunks, i = 16c + q + 1, S[i]
          * at immediate offsets (the last step of a chunk wraps into c + 1) */
+        uint32_t an = S[lane4 + rc4_ioff<BL>(1)]; /* S[1] */
+        (void)an;
         for (uint32_t c = 0; n < drop; n += 16, c = (c + 1) & 15u) {
             uint8_t *Sc = S + ((c << 10) | lane4);
             uint8_t *Sn = S + ((((c + 1) & 15u) << 10) | lane4);
+            const uint32_t ib = c << 4, nb = ((c + 1) & 15u) << 4;
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 uint8_t *si = q < 15 ? Sc + rc4_ioff<BL>(q + 1) : Sn;
-                const uint32_t a = *si;
-                j = (j + a) & 0xFFu;
-                const uint32_t aj = rc4_addr<BL>(j, lane4);
-                const uint32_t b = S[aj];
-                *si = (uint8_t)b;
-                S[aj] = (uint8_t)a;
+                if constexpr (AL >= 2) { /* S[i+1] read ahead, as in the PRGA */
+                    uint8_t *sp = q < 14 ? Sc + rc4_ioff<BL>(q + 2) : (q == 14 ? Sn : Sn + rc4_ioff<BL>(1));
+                    const uint32_t a = an;
+                    j = (j + a) & 0xFFu;
+                    const uint32_t aj = rc4_addr<BL>(j, lane4);
+                    const uint32_t b = S[aj];
+                    const uint32_t pn = *sp;
+                    const uint32_t inx = q < 14 ? ib + (uint32_t)(q + 2) : nb + (uint32_t)(q - 14);
+                    an = (j == inx) ? a : pn;
+                    *si = (uint8_t)b;
+                    S[aj] = (uint8_t)a;
+                } else {
+                    const uint32_t a = *si;
+                    j = (j + a) & 0xFFu;
+                    const uint32_t aj = rc4_addr<BL>(j, lane4);
+                    const uint32_t b = S[aj];
+                    *si = (uint8_t)b;
+                    S[aj] = (uint8_t)a;
+                }
             }
         }
         i = (uint32_t)(drop & 0xFFu);
