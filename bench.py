@@ -11,6 +11,17 @@ Timing: W untimed warmup steps, barrier + synchronize, K timed steps,
 synchronize + barrier, MAX over ranks.  Correctness is checked on a sample of
 every shard against the CPU oracle before timing.
 
+Multi-GPU: ``python bench.py --gpus N`` without a launcher spawns N fresh
+worker processes itself (parallel/launch.py) before anything touches the GPU;
+under torchrun WORLD_SIZE must equal --gpus.  Fewer visible GPUs than --gpus
+is an error (exit 2) -- a multi-GPU request is never measured on fewer GPUs.
+
+Communication: the resident CTR step needs none (every rank owns its shard),
+so an extra, separately timed pass runs BASELINE config 4 in miniature -- an
+AES-256-CBC stream on the root GPU dealt to all ranks by RCCL scatter over
+xGMI, sector-encrypted, gathered back -- and reports the communicator's rank
+count (``rccl_ranks``) and the bytes it moved between GPUs.
+
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--gib 64]
         torchrun --nproc-per-node N bench.py --gpus N ...
 """
@@ -40,17 +51,26 @@ def main():
     ap.add_argument("--no-aes256", action="store_true")
     ap.add_argument("--no-bitslice", action="store_true")
     ap.add_argument("--no-clock", action="store_true")
+    ap.add_argument("--no-scatter", action="store_true", help="skip the RCCL scatter/gather AES-256-CBC pass")
+    ap.add_argument("--scatter-mib", type=int, default=512, help="per-rank bytes per scatter round (MiB)")
+    ap.add_argument("--scatter-rounds", type=int, default=4)
     args = ap.parse_args()
+
+    # decide the launch before any HIP call (spawned ranks re-enter here with
+    # RANK/WORLD_SIZE set); exits on error or when the spawned run finished
+    from our_tree_amd.parallel import launch
+
+    launch.dispatch(args.gpus, os.path.abspath(__file__), sys.argv[1:])
 
     from our_tree_amd import ops
     from our_tree_amd.models import cpu_ref
     from our_tree_amd.parallel import dist as pdist
     from our_tree_amd.utils import device as dinfo
 
-    rank, world, local = pdist.init_from_env()
-    if world != args.gpus:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    # a process group even at N=1 (a 1-rank RCCL group) so the scatter pass
+    # always runs the collective code path
+    rank, world, local = pdist.init_from_env(force=not args.no_scatter)
+    assert world == args.gpus, (world, args.gpus)  # launch.dispatch guarantees it
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -135,6 +155,20 @@ def main():
         el256 = timed(k256_steps, key256)
         extra["aes256_ctr_gbps_whole_node"] = round(nbytes * world * k256_steps / el256 / 1e9, 3)
         extra["aes256_vs_cpu_aesni_ctr256"] = round(extra["aes256_ctr_gbps_whole_node"] / BASELINE_GBPS, 1)
+
+    if not args.no_scatter:
+        from our_tree_amd.parallel import jobs
+
+        del buf  # the scatter pass needs its own buffers (4 x world x chunk on the root)
+        torch.cuda.empty_cache()
+        sc = jobs.cbc_scatter_job(args.scatter_rounds, args.scatter_mib << 20, key256,
+                                  bytes(range(0xA0, 0xB0)), sector=4096, device=dev)
+        extra["rccl_cbc256_scatter_gbps"] = round(sc["gbps"], 3)
+        extra["rccl_ranks"] = sc["ranks"]
+        extra["rccl_backend"] = sc["backend"]
+        extra["rccl_xgmi_bytes"] = sc["xgmi_bytes"]
+        extra["rccl_scatter_bytes"] = sc["total_bytes"]
+        extra["rccl_scatter_verified"] = sc["verified"]
 
     if rank == 0:
         line = {

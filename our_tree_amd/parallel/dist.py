@@ -27,7 +27,7 @@ from ..models import cpu_ref
 from . import shard as sh
 
 
-def init_from_env(backend: str | None = None):
+def init_from_env(backend: str | None = None, force: bool = False):
     """Initialise the default process group from torchrun's env and bind the
     rank to its GPU.  Returns (rank, world, gpu): gpu = LOCAL_RANK (one
     process per GPU).
@@ -36,7 +36,9 @@ def init_from_env(backend: str | None = None):
     ranks, e.g. 2 ranks on one MI355X): OTC_DIST_BACKEND=gloo picks the
     backend (RCCL refuses two ranks on one device) and OTC_SHARE_GPUS=1 maps
     rank r to GPU r mod device_count instead of failing; OTC_DIST_FORCE=1
-    creates the process group even at world size 1."""
+    creates the process group even at world size 1 (so does ``force``; a
+    missing MASTER_ADDR/MASTER_PORT then defaults to 127.0.0.1 and a free
+    port)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -49,8 +51,15 @@ def init_from_env(backend: str | None = None):
                 raise RuntimeError(f"LOCAL_RANK {local} but only {n} GPU(s) visible (OTC_SHARE_GPUS=1 to share)")
             gpu = local % n
         torch.cuda.set_device(gpu)
-    force = os.environ.get("OTC_DIST_FORCE") == "1"  # a 1-rank group too (exercises the RCCL path)
+    force = force or os.environ.get("OTC_DIST_FORCE") == "1"  # a 1-rank group too (exercises the RCCL path)
     if (world > 1 or force) and not dist.is_initialized():
+        if world == 1:
+            from .launch import free_port
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group(backend, device_id=torch.device("cuda", gpu))
         else:
@@ -88,13 +97,40 @@ def _ctr_local(x: torch.Tensor, key: bytes, counter: bytes, block_offset: int, i
 def sharded_ctr_(local: torch.Tensor, key: bytes, counter: bytes, global_nbytes: int | None = None,
                  impl="auto") -> torch.Tensor:
     """In-place CTR on this rank's shard of a globally contiguous stream
-    (equal-size shards in rank order; the counter offset is derived from the
-    rank).  No communication."""
+    (shards in rank order, any sizes; all but the last a multiple of 16 bytes).
+
+    The counter offset is this shard's byte offset / 16.  With
+    ``global_nbytes`` the layout is taken to be ``shard.plan(global_nbytes,
+    world)`` (checked against the local size) and no communication happens;
+    otherwise the offset is the exclusive prefix sum of the local sizes (one
+    small all_gather)."""
     rank, world = _world()
     n = local.numel() * local.element_size()
     if n % sh.BLOCK and rank != world - 1:
         raise ValueError("all shards but the last must be a multiple of 16 bytes")
-    return _ctr_local(local, key, counter, rank * (n // sh.BLOCK), impl)
+    if global_nbytes is not None:
+        s = sh.plan(global_nbytes, world)[rank]
+        if s.nbytes != n:
+            raise ValueError(f"rank {rank}: local shard has {n} bytes but plan({global_nbytes}, {world}) "
+                             f"gives it {s.nbytes}")
+        offset = s.offset
+    elif world > 1:
+        sizes = _all_gather_int(n)
+        offset = sum(sizes[:rank])
+        if any(v % sh.BLOCK for v in sizes[:-1]):
+            raise ValueError("all shards but the last must be a multiple of 16 bytes")
+    else:
+        offset = 0
+    return _ctr_local(local, key, counter, offset // sh.BLOCK, impl)
+
+
+def _all_gather_int(v: int) -> list[int]:
+    on_gpu = torch.cuda.is_available() and dist.get_backend() == "nccl"
+    device = torch.device("cuda", torch.cuda.current_device()) if on_gpu else "cpu"
+    t = torch.tensor([v], dtype=torch.int64, device=device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [int(x.item()) for x in out]
 
 
 def cbc_decrypt_sharded(local_ct: torch.Tensor, key: bytes, iv: bytes) -> torch.Tensor:

@@ -1,0 +1,86 @@
+#!/bin/bash
+# One parametrised GPU runner (run it on the box through gpurun):
+#
+#   gpurun --timeout 900 -- bash scripts/run.sh <suite> [args...]
+#
+# suites
+#   validate            pytest -m gpu, smoke(), default bench.py   (round-end checks)
+#   test [pytest args]  pytest -m gpu (optionally a subset: test tests/test_gpu_engine.py -k cbc)
+#   bench [bench args]  bench.py with the given flags
+#   rehearse N [args]   bench.py --gpus N self-spawned, N ranks sharing the box's GPU (gloo)
+#   kt NAME -- CMD...   rocprofv3 kernel trace + stats of CMD, summarised to gpurun_out/NAME/kernels.txt
+#   pmc NAME "COUNTERS" -- CMD...   one counter pass (<= 8 SQ, 4 TCC, ...) of CMD, CSV in gpurun_out/NAME
+#   otbench [otbench args]          bin/otbench JSON lines
+#   cmd -- CMD...       anything else, under a time limit
+#
+# Every GPU step runs under its own `timeout -k 10`, steps are chained with &&
+# and the script stops at the first failure (no retries).  Output goes under
+# gpurun_out/ (merged back by gpurun); copy what is worth keeping to profiles/.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+suite=${1:-validate}
+shift || true
+OUT=gpurun_out
+mkdir -p $OUT
+
+pytest_gpu() {
+    timeout -k 10 900 python -u -m pytest -m gpu -x -v --timeout 120 --timeout-method thread "$@"
+}
+
+case "$suite" in
+validate)
+    D=$OUT/validate
+    mkdir -p $D
+    pytest_gpu tests > $D/pytest_gpu.log 2>&1 || { tail -40 $D/pytest_gpu.log; exit 1; }
+    tail -1 $D/pytest_gpu.log
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 || { cat $D/smoke.log; exit 1; }
+    tail -1 $D/smoke.log
+    timeout -k 10 600 python bench.py > $D/bench.json 2> $D/bench.err || { tail -20 $D/bench.err; exit 1; }
+    cat $D/bench.json
+    ;;
+test)
+    [ $# -gt 0 ] || set -- tests
+    pytest_gpu "$@" > $OUT/pytest_gpu.log 2>&1
+    rc=$?
+    tail -30 $OUT/pytest_gpu.log
+    exit $rc
+    ;;
+bench)
+    timeout -k 10 900 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+    cat $OUT/bench.json
+    ;;
+rehearse)
+    n=${1:-2}
+    shift || true
+    OTC_DIST_BACKEND=gloo OTC_SHARE_GPUS=1 timeout -k 10 600 python bench.py --gpus "$n" --no-clock "$@" \
+        > $OUT/rehearse_dp$n.txt 2>&1 || { tail -30 $OUT/rehearse_dp$n.txt; exit 1; }
+    grep '^{' $OUT/rehearse_dp$n.txt
+    ;;
+kt)
+    name=$1; shift; [ "$1" = "--" ] && shift
+    mkdir -p $OUT/$name
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/$name/db -o run -- "$@" > $OUT/$name/run.log 2>&1 ||
+        { tail -20 $OUT/$name/run.log; exit 1; }
+    db=$(find $OUT/$name/db -name '*.db' | head -1)
+    python tools/rocpd_summary.py "$db" > $OUT/$name/kernels.txt && cat $OUT/$name/kernels.txt
+    ;;
+pmc)
+    name=$1; counters=$2; shift 2; [ "$1" = "--" ] && shift
+    mkdir -p $OUT/$name
+    timeout -s KILL 120 rocprofv3 --pmc $counters --output-format csv -d $OUT/$name -o run -- "$@" \
+        > $OUT/$name/run.log 2>&1 || { tail -20 $OUT/$name/run.log; exit 1; }
+    find $OUT/$name -name '*counter_collection.csv' | head -3
+    ;;
+otbench)
+    timeout -k 10 600 ./bin/otbench "$@" > $OUT/otbench.jsonl 2> $OUT/otbench.err || { tail -20 $OUT/otbench.err; exit 1; }
+    cat $OUT/otbench.jsonl
+    ;;
+cmd)
+    [ "$1" = "--" ] && shift
+    timeout -k 10 900 "$@"
+    ;;
+*)
+    echo "unknown suite: $suite" >&2
+    exit 2
+    ;;
+esac

@@ -30,7 +30,8 @@ def test_bench_json_line(gpu):
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--gib", "0.25", "--no-clock", "--no-aes256", "--no-bitslice"],
+                        "--gib", "0.25", "--no-clock", "--no-aes256", "--no-bitslice",
+                        "--scatter-mib", "64", "--scatter-rounds", "2"],
                        capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -48,3 +49,6 @@ def test_bench_json_line(gpu):
     # value (GB/s) and ms_per_step describe the same timed region
     assert d["value"] == pytest.approx(nbytes / (d["ms_per_step"] * 1e-3) / 1e9, rel=0.01)
     assert d["value"] > 100.0  # the HIP kernel ran (an eager fallback would be far slower)
+    # the communication pass ran through a (1-rank) RCCL group and verified
+    assert d["rccl_ranks"] == 1 and d["rccl_backend"] == "nccl"
+    assert d["rccl_scatter_verified"] is True and d["rccl_cbc256_scatter_gbps"] > 0

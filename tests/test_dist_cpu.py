@@ -53,7 +53,22 @@ def _worker(rank, world, port, q):
             ok3 = ok3 and (res is None if rank != 0 else res.numpy().tobytes() == ref_ctr[:n])
         m = pdist.allreduce_max(float(rank))
         ok4 = m == world - 1
-        q.put((rank, ok1, ok2, ok3, ok4))
+
+        # uneven shards (shard.plan: the first ranks get one extra block, the
+        # last takes the partial tail): offsets from the plan and from the
+        # all_gather prefix sum must both equal the single-stream keystream
+        from our_tree_amd.parallel import shard as sh
+
+        tot = 16 * (257 * world + 3) + 5
+        s = sh.plan(tot, world)[rank]
+        stream = torch.randint(0, 256, (tot,), dtype=torch.uint8, generator=torch.Generator().manual_seed(1))
+        ok5 = True
+        for gn in (tot, None):
+            mine = stream[s.offset:s.end].clone()
+            src = mine.numpy().tobytes()
+            pdist.sharded_ctr_(mine, key, ctr0, global_nbytes=gn)
+            ok5 = ok5 and mine.numpy().tobytes() == cpu_ref.ctr(key, ctr0, src, s.block_offset)
+        q.put((rank, ok1, ok2, ok3, ok4, ok5))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
         q.put((rank, repr(e)))
@@ -71,5 +86,5 @@ def test_gloo_data_parallel(world):
     for p in procs:
         p.join(timeout=60)
     for r in res:
-        assert len(r) == 5, f"worker failed: {r}"
+        assert len(r) == 6, f"worker failed: {r}"
         assert all(r[1:]), f"rank {r[0]} mismatch: {r}"
