@@ -35,10 +35,10 @@ endif
 LIBDIR := our_tree_amd/lib
 OBJ    := build/obj
 
-CPU_SRC := csrc/cpu/aes.c csrc/cpu/arc4.c csrc/cpu/rc4.c csrc/cpu/aesni.c
+CPU_SRC := csrc/cpu/aes.c csrc/cpu/arc4.c csrc/cpu/rc4.c csrc/cpu/aesni.c csrc/cpu/numa.c
 CPU_OBJ := $(patsubst csrc/cpu/%.c,$(OBJ)/cpu/%.o,$(CPU_SRC)) $(OBJ)/cpu/bs_selftest.o
 HIP_SRC := csrc/hip/aes_tt.hip csrc/hip/aes_bs.hip csrc/hip/stream_ops.hip
-HIP_OBJ := $(patsubst csrc/hip/%.hip,$(OBJ)/hip/%.o,$(HIP_SRC)) $(OBJ)/hip/engine.o
+HIP_OBJ := $(patsubst csrc/hip/%.hip,$(OBJ)/hip/%.o,$(HIP_SRC)) $(OBJ)/hip/engine.o $(OBJ)/hip/pipeline.o
 
 BINS := bin/test bin/aes_test bin/aes_ecb_e bin/aes_ecb_d bin/otbench bin/bc_test
 
@@ -67,7 +67,7 @@ $(OBJ)/hip/%.o: csrc/hip/%.hip csrc/hip/otc_device.h csrc/include/otc.h csrc/inc
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) $(INC) -c $< -o $@
 
-$(OBJ)/hip/engine.o: csrc/hip/engine.cpp csrc/hip/otc_device.h csrc/include/otc.h
+$(OBJ)/hip/%.o: csrc/hip/%.cpp csrc/hip/otc_device.h csrc/hip/engine_internal.h $(wildcard csrc/include/*.h)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -x hip $(INC) -c $< -o $@
 

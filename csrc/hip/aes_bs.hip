@@ -244,17 +244,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     aes_bs_task<NR, MODE, false, 0, LS>(P, K, stage);
 }
 
-int g_cus = 0;
-
 template <int NR, int MODE>
 hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
 {
-    if (g_cus <= 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (g_cus <= 0) g_cus = 256;
-    }
     const uint64_t vt = P.nblocks + (MODE == BS_CTR ? P.shift : 0);
     const uint64_t tasks = (vt + 2047) / 2048;
     uint64_t wgs = (tasks + 3) / 4;
@@ -310,7 +302,7 @@ hipError_t launch(const BsParams &P, const otc_aes_key &K, hipStream_t st)
 
 namespace otc_impl {
 
-hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
+hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t, int);
 
 hipError_t bs_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
                   hipStream_t st)
@@ -321,7 +313,7 @@ hipError_t bs_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K
         Ctr128 ct = c;
         ct.lo = c.lo + full / 16;
         if (!wrap64 && ct.lo < c.lo) ct.hi += 1;
-        hipError_t e = tt_ctr((const uint8_t *)in + full, (uint8_t *)out + full, nbytes % 16, K, ct, wrap64, st);
+        hipError_t e = tt_ctr((const uint8_t *)in + full, (uint8_t *)out + full, nbytes % 16, K, ct, wrap64, st, 2);
         if (e != hipSuccess) return e;
         nbytes = full;
         if (nbytes == 0) return hipSuccess;

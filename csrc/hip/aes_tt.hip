@@ -945,18 +945,7 @@ static_assert(64 * 4 == OTC_BATCH_TILE_BLOCKS, "largest tile must match otc.h");
 /* ---------------------------------------------------------------------------
  * Host-side launch helpers
  * ------------------------------------------------------------------------- */
-int g_num_cus = 0;
-
-int num_cus()
-{
-    if (g_num_cus <= 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (g_num_cus <= 0) g_num_cus = 256;
-    }
-    return g_num_cus;
-}
+inline int num_cus() { return otc_dev::device_cus(); }
 
 int grid_for(uint64_t work_items, uint64_t per_wg, int wg_per_cu)
 {
@@ -1144,46 +1133,46 @@ hipError_t tt_ecb_encrypt(const void *in, void *out, uint64_t nblocks, const otc
     return launch_enc<E_ECB>(P, K, st);
 }
 
-int g_tt_wg_per_cu = 2; /* lowered to 1 while a co-resident bitsliced kernel runs (hybrid impl) */
-
+/* wg_per_cu: resident workgroups per CU of the 1-table layouts (2; 1 while a
+ * co-resident bitsliced kernel runs, hybrid impl).  A launch parameter, not
+ * process state: the multi-GPU paths launch from one host thread per GPU. */
 template <int NR, int T, int B, bool TBL4 = false, bool ISSUE_ALL = true, bool NT = false>
-hipError_t launch_ctr_cached_tb(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo, hipStream_t st)
+hipError_t launch_ctr_cached_tb(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo, int wg_per_cu, hipStream_t st)
 {
     constexpr uint64_t PER = (uint64_t)T * B;
     P.shift = ctr_lo & (PER - 1);
     P.cbase.lo = ctr_lo - P.shift;
     const uint64_t vt = P.nfull + (P.tail ? 1 : 0) + P.shift;
-    int grid = grid_for(vt, PER, TBL4 ? 1 : g_tt_wg_per_cu);
+    int grid = grid_for(vt, PER, TBL4 ? 1 : wg_per_cu);
     hipLaunchKernelGGL((k_aes_ctr_tt_cached<NR, B, T, TBL4, ISSUE_ALL, NT>), dim3(grid), dim3(T), 0, st, P, K);
     return hipGetLastError();
 }
 
 template <int NR>
-hipError_t launch_ctr_cached(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo, hipStream_t st)
+hipError_t launch_ctr_cached(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo, int wpc, hipStream_t st)
 {
     /* OTC_TT_VARIANT=<threads>x<B>: negative threads = 1-table layout (A/B
      * measurements); default = 4-table layout, 1024 threads x 4 blocks/lane */
     const TTVariant v = tt_variant();
     /* OTC_TT_NT=1: non-temporal plaintext loads / ciphertext stores (A/B) */
     static const bool nt = getenv("OTC_TT_NT") && atoi(getenv("OTC_TT_NT")) != 0;
-    if (nt) return launch_ctr_cached_tb<NR, 1024, 4, true, true, true>(P, K, ctr_lo, st);
-    if (v.threads == 1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, true>(P, K, ctr_lo, st);
-    if (v.threads == 2 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, true, false>(P, K, ctr_lo, st);
-    if (v.threads == 512 && v.b == 4) return launch_ctr_cached_tb<NR, 512, 4, true>(P, K, ctr_lo, st);
-    if (v.threads == -1024 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, false>(P, K, ctr_lo, st);
-    if (v.threads == -1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, false>(P, K, ctr_lo, st);
+    if (nt) return launch_ctr_cached_tb<NR, 1024, 4, true, true, true>(P, K, ctr_lo, wpc, st);
+    if (v.threads == 1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, true>(P, K, ctr_lo, wpc, st);
+    if (v.threads == 2 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, true, false>(P, K, ctr_lo, wpc, st);
+    if (v.threads == 512 && v.b == 4) return launch_ctr_cached_tb<NR, 512, 4, true>(P, K, ctr_lo, wpc, st);
+    if (v.threads == -1024 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, false>(P, K, ctr_lo, wpc, st);
+    if (v.threads == -1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, false>(P, K, ctr_lo, wpc, st);
     switch (small_shape(P.nfull + (P.tail ? 1 : 0))) {
-    case SHAPE_256x1: return launch_ctr_cached_tb<NR, 256, 1, true>(P, K, ctr_lo, st);
-    case SHAPE_1024x1: return launch_ctr_cached_tb<NR, 1024, 1, true>(P, K, ctr_lo, st);
-    default: return launch_ctr_cached_tb<NR, 1024, 4, true>(P, K, ctr_lo, st);
+    case SHAPE_256x1: return launch_ctr_cached_tb<NR, 256, 1, true>(P, K, ctr_lo, wpc, st);
+    case SHAPE_1024x1: return launch_ctr_cached_tb<NR, 1024, 1, true>(P, K, ctr_lo, wpc, st);
+    default: return launch_ctr_cached_tb<NR, 1024, 4, true>(P, K, ctr_lo, wpc, st);
     }
 }
 
-void tt_set_wg_per_cu(int n) { g_tt_wg_per_cu = n < 1 ? 1 : n; }
-
 hipError_t tt_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
-                  hipStream_t st)
+                  hipStream_t st, int wg_per_cu)
 {
+    const int wpc = wg_per_cu < 1 ? 1 : wg_per_cu;
     if (getenv("OTC_TT_NOCACHE") == nullptr) {
         CtrParams P{};
         P.in = (const uint8_t *)in;
@@ -1193,9 +1182,9 @@ hipError_t tt_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K
         P.wrap64 = wrap64 ? 1u : 0u;
         P.cbase.hi = c.hi;
         switch (K.nr) {
-        case 10: return launch_ctr_cached<10>(P, K, c.lo, st);
-        case 12: return launch_ctr_cached<12>(P, K, c.lo, st);
-        case 14: return launch_ctr_cached<14>(P, K, c.lo, st);
+        case 10: return launch_ctr_cached<10>(P, K, c.lo, wpc, st);
+        case 12: return launch_ctr_cached<12>(P, K, c.lo, wpc, st);
+        case 14: return launch_ctr_cached<14>(P, K, c.lo, wpc, st);
         default: return hipErrorInvalidValue;
         }
     }

@@ -34,13 +34,14 @@
 #include "otc.h"
 #include "otc_aesni.h"
 #include "otc_device.h"
+#include "engine_internal.h"
 
 using otc_dev::Ctr128;
 
 namespace otc_impl {
 hipError_t tt_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
 hipError_t tt_ecb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
-hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
+hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t, int wg_per_cu = 2);
 hipError_t tt_cfb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, hipStream_t);
 hipError_t tt_cbc_decrypt(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t tt_cbc_decrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
@@ -49,7 +50,6 @@ hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, boo
 hipError_t bs_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
 hipError_t tt_ctr_batch(const otc_ctr_msg *, const otc_aes_key *, const uint32_t *, const uint64_t *, uint64_t, int, int,
                         hipStream_t);
-void tt_set_wg_per_cu(int);
 hipError_t k_xor(const void *, const void *, void *, size_t, hipStream_t);
 hipError_t k_fill_random(void *, size_t, uint64_t, hipStream_t);
 hipError_t k_checksum(const void *, size_t, uint64_t *, hipStream_t);
@@ -58,9 +58,11 @@ hipError_t k_rc4_multi(const uint8_t *, int, size_t, size_t, size_t, const void 
 } // namespace otc_impl
 
 /* ------------------------------------------------------------------------- */
-namespace {
+namespace otc_rt {
 
+namespace {
 thread_local std::string g_err;
+}
 
 int set_err(int code, const std::string &msg)
 {
@@ -68,23 +70,12 @@ int set_err(int code, const std::string &msg)
     return code;
 }
 
+std::string last_err() { return g_err; }
+
 int hip_fail(hipError_t e, const char *what)
 {
     return set_err(OTC_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
-
-#define HIPCHK(expr)                                          \
-    do {                                                      \
-        hipError_t _e = (expr);                               \
-        if (_e != hipSuccess) return hip_fail(_e, #expr);     \
-    } while (0)
-
-#define RCCLCHK(expr)                                                                      \
-    do {                                                                                   \
-        ncclResult_t _r = (expr);                                                          \
-        if (_r != ncclSuccess)                                                             \
-            return set_err(OTC_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
-    } while (0)
 
 Ctr128 ctr_from_bytes(const uint8_t c[16])
 {
@@ -102,6 +93,22 @@ Ctr128 ctr_add(Ctr128 c, uint64_t n, bool wrap64)
     return c;
 }
 
+int check_key(const otc_aes_key *k, int dir)
+{
+    if (!k) return set_err(OTC_ERR_ARG, "null key");
+    if (k->nr != 10 && k->nr != 12 && k->nr != 14) return set_err(OTC_ERR_ARG, "bad key (nr)");
+    if (k->dir != dir)
+        return set_err(OTC_ERR_ARG, dir == OTC_DIR_ENCRYPT ? "key schedule is not an encryption schedule"
+                                                           : "key schedule is not a decryption schedule");
+    return OTC_OK;
+}
+
+} // namespace otc_rt
+
+using namespace otc_rt;
+
+namespace {
+
 int pick_impl(int impl, int bits)
 {
     if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_HYBRID) return impl;
@@ -114,26 +121,6 @@ int pick_impl(int impl, int bits)
     (void)bits;
     return OTC_IMPL_TTABLE; /* default: the measured winner (see docs/PERF.md) */
 }
-
-int check_key(const otc_aes_key *k, int dir)
-{
-    if (!k) return set_err(OTC_ERR_ARG, "null key");
-    if (k->nr != 10 && k->nr != 12 && k->nr != 14) return set_err(OTC_ERR_ARG, "bad key (nr)");
-    if (k->dir != dir)
-        return set_err(OTC_ERR_ARG, dir == OTC_DIR_ENCRYPT ? "key schedule is not an encryption schedule"
-                                                           : "key schedule is not a decryption schedule");
-    return OTC_OK;
-}
-
-/* roctx range for rocprofv3 --marker-trace (a no-op unless a tool is attached):
- * every public entry point is one named range, so traces show the API call
- * around its kernels and copies. */
-struct Range {
-    explicit Range(const char *name) { roctxRangePushA(name); }
-    ~Range() { roctxRangePop(); }
-    Range(const Range &) = delete;
-    Range &operator=(const Range &) = delete;
-};
 
 /* Device buffers of the cipher ops: non-null, 16-byte aligned (every kernel
  * moves 16 B per lane with global_load/store_dwordx4), and either the same
@@ -158,7 +145,12 @@ int check_bufs(const void *in, const void *out, size_t nbytes, bool inplace_ok, 
 } // namespace
 
 /* ---- errors / keys ------------------------------------------------------ */
-extern "C" const char *otc_last_error(void) { return g_err.c_str(); }
+extern "C" const char *otc_last_error(void)
+{
+    thread_local std::string copy;
+    copy = last_err();
+    return copy.c_str();
+}
 
 extern "C" int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir)
 {
@@ -207,7 +199,59 @@ struct AuxStream {
     hipStream_t s = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
 };
-thread_local AuxStream g_aux[16];
+
+/* Auxiliary streams for the hybrid split, pooled per device: a call takes one
+ * (creating it on first use), enqueues, and returns it -- so concurrent
+ * callers (one host thread per GPU in otc_multi_run) never share the events
+ * they order on.  otc_release_resources() destroys the pool. */
+std::mutex g_aux_mu;
+std::vector<AuxStream> g_aux_free;
+
+static hipError_t aux_take(int dev, AuxStream &out)
+{
+    {
+        std::lock_guard<std::mutex> lk(g_aux_mu);
+        for (size_t i = 0; i < g_aux_free.size(); ++i)
+            if (g_aux_free[i].dev == dev) {
+                out = g_aux_free[i];
+                g_aux_free.erase(g_aux_free.begin() + (long)i);
+                return hipSuccess;
+            }
+    }
+    AuxStream a;
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(&a.e0, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(&a.e1, hipEventDisableTiming)) != hipSuccess) return e;
+    a.dev = dev;
+    out = a;
+    return hipSuccess;
+}
+
+static void aux_give(const AuxStream &a)
+{
+    std::lock_guard<std::mutex> lk(g_aux_mu);
+    g_aux_free.push_back(a);
+}
+
+void otc_rt::aux_release_all()
+{
+    std::lock_guard<std::mutex> lk(g_aux_mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (AuxStream &a : g_aux_free) {
+        (void)hipSetDevice(a.dev);
+        if (a.s) (void)hipStreamSynchronize(a.s);
+        if (a.e0) (void)hipEventDestroy(a.e0);
+        if (a.e1) (void)hipEventDestroy(a.e1);
+        if (a.s) (void)hipStreamDestroy(a.s);
+    }
+    g_aux_free.clear();
+    (void)hipSetDevice(cur);
+}
+
+static hipError_t hybrid_ctr_on(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
+                                hipStream_t st, AuxStream &a);
 
 hipError_t hybrid_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
                       hipStream_t st)
@@ -215,13 +259,17 @@ hipError_t hybrid_ctr(const void *in, void *out, size_t nbytes, const otc_aes_ke
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    AuxStream &a = g_aux[dev & 15];
-    if (a.dev != dev) {
-        if ((e = hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking)) != hipSuccess) return e;
-        if ((e = hipEventCreateWithFlags(&a.e0, hipEventDisableTiming)) != hipSuccess) return e;
-        if ((e = hipEventCreateWithFlags(&a.e1, hipEventDisableTiming)) != hipSuccess) return e;
-        a.dev = dev;
-    }
+    AuxStream a;
+    if ((e = aux_take(dev, a)) != hipSuccess) return e;
+    e = hybrid_ctr_on(in, out, nbytes, K, c, wrap64, st, a);
+    aux_give(a); /* reusable as soon as the work is enqueued: stream order */
+    return e;
+}
+
+static hipError_t hybrid_ctr_on(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
+                                hipStream_t st, AuxStream &a)
+{
+    hipError_t e;
     double frac = 0.6;
     if (const char *f = getenv("OTC_HYBRID_TT")) frac = atof(f);
     const uint64_t nblk = nbytes / 16;
@@ -240,9 +288,7 @@ hipError_t hybrid_ctr(const void *in, void *out, size_t nbytes, const otc_aes_ke
     if (tt_bytes) {
         /* the T-table variant for co-residency is chosen by OTC_TT_VARIANT
          * (B=2 keeps it at <= 64 VGPRs so a 256-VGPR bitsliced wave fits) */
-        otc_impl::tt_set_wg_per_cu(1);
-        e = otc_impl::tt_ctr(in, out, tt_bytes, K, c, wrap64, st);
-        otc_impl::tt_set_wg_per_cu(2);
+        e = otc_impl::tt_ctr(in, out, tt_bytes, K, c, wrap64, st, 1);
         if (e != hipSuccess) return e;
     }
     if (nbytes > tt_bytes) {
@@ -630,566 +676,6 @@ extern "C" void *otc_host_alloc_pinned(size_t nbytes)
 extern "C" void otc_host_free_pinned(void *p)
 {
     if (p) (void)hipHostFree(p);
-}
-
-/* ---- L3 streaming engine ------------------------------------------------ */
-struct otc_engine {
-    int device = 0;
-    size_t chunk = 0;
-    int depth = 0;                  /* ring slots */
-    std::vector<void *> d_in, d_out; /* device ring */
-    std::vector<void *> h_in, h_out; /* pinned staging ring */
-    hipStream_t s_h2d = nullptr, s_k = nullptr, s_d2h = nullptr;
-    std::vector<hipEvent_t> ev_h2d, ev_k, ev_d2h, ev_k0;
-};
-
-extern "C" otc_engine *otc_engine_create(int device, size_t chunk_bytes, int depth)
-{
-    if (chunk_bytes == 0) chunk_bytes = 256ull << 20;
-    chunk_bytes = (chunk_bytes + 15) & ~(size_t)15;
-    if (depth < 2) depth = 3;
-    otc_engine *e = new otc_engine();
-    e->device = device;
-    e->chunk = chunk_bytes;
-    e->depth = depth;
-    if (hipSetDevice(device) != hipSuccess) { set_err(OTC_ERR_HIP, "hipSetDevice"); delete e; return nullptr; }
-    bool ok = hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&e->s_k, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&e->s_d2h, hipStreamNonBlocking) == hipSuccess;
-    e->d_in.assign(depth, nullptr);
-    e->d_out.assign(depth, nullptr);
-    e->h_in.assign(depth, nullptr);
-    e->h_out.assign(depth, nullptr);
-    e->ev_h2d.assign(depth, nullptr);
-    e->ev_k.assign(depth, nullptr);
-    e->ev_d2h.assign(depth, nullptr);
-    e->ev_k0.assign(depth, nullptr);
-    /* pinned staging (h_in/h_out) is allocated lazily, only for pageable
-     * host buffers */
-    for (int i = 0; ok && i < depth; ++i) {
-        ok = hipMalloc(&e->d_in[i], chunk_bytes) == hipSuccess && hipMalloc(&e->d_out[i], chunk_bytes) == hipSuccess &&
-             hipEventCreateWithFlags(&e->ev_h2d[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreate(&e->ev_k[i]) == hipSuccess &&
-             hipEventCreateWithFlags(&e->ev_d2h[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreate(&e->ev_k0[i]) == hipSuccess;
-    }
-    if (!ok) {
-        set_err(OTC_ERR_NOMEM, "engine allocation failed");
-        otc_engine_destroy(e);
-        return nullptr;
-    }
-    return e;
-}
-
-extern "C" void otc_engine_destroy(otc_engine *e)
-{
-    if (!e) return;
-    (void)hipSetDevice(e->device);
-    if (e->s_k) (void)hipStreamSynchronize(e->s_k);
-    if (e->s_h2d) (void)hipStreamSynchronize(e->s_h2d);
-    if (e->s_d2h) (void)hipStreamSynchronize(e->s_d2h);
-    for (int i = 0; i < e->depth; ++i) {
-        if (e->d_in[i]) (void)hipFree(e->d_in[i]);
-        if (e->d_out[i]) (void)hipFree(e->d_out[i]);
-        if (e->h_in[i]) (void)hipHostFree(e->h_in[i]);
-        if (e->h_out[i]) (void)hipHostFree(e->h_out[i]);
-        if (e->ev_h2d[i]) (void)hipEventDestroy(e->ev_h2d[i]);
-        if (e->ev_k[i]) (void)hipEventDestroy(e->ev_k[i]);
-        if (e->ev_d2h[i]) (void)hipEventDestroy(e->ev_d2h[i]);
-        if (e->ev_k0[i]) (void)hipEventDestroy(e->ev_k0[i]);
-    }
-    if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
-    if (e->s_k) (void)hipStreamDestroy(e->s_k);
-    if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
-    delete e;
-}
-
-static bool is_pinned(const void *p)
-{
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return a.type == hipMemoryTypeHost;
-}
-
-extern "C" int otc_ptr_kind(const void *p)
-{
-    if (!p) return OTC_PTR_HOST;
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return OTC_PTR_HOST;
-    }
-    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) return OTC_PTR_DEVICE;
-    if (a.type == hipMemoryTypeHost) return OTC_PTR_PINNED;
-    return OTC_PTR_HOST;
-}
-
-/* Launch the cipher on one device chunk. `blk0` = block offset of the chunk
- * inside the whole stream; `prev` = for CBC-dec, the 16-byte ciphertext block
- * preceding the chunk (the halo), as counter-style numeric IV. */
-/* Up-front validation of a host-streamed job (engine and multi-GPU), so a bad
- * call fails before any allocation or copy is issued. */
-static int check_stream_args(int mode, const void *host_in, const void *host_out, size_t nbytes,
-                             const otc_aes_key *k, const uint8_t ivc[16])
-{
-    if (mode != OTC_MODE_ECB && mode != OTC_MODE_CTR && mode != OTC_MODE_CBC_DEC)
-        return set_err(OTC_ERR_ARG, "unsupported streaming mode");
-    if (mode != OTC_MODE_CTR && nbytes % 16) return set_err(OTC_ERR_ARG, "length must be a multiple of 16");
-    if (nbytes && (!host_in || !host_out)) return set_err(OTC_ERR_ARG, "null host buffer");
-    if (!k) return set_err(OTC_ERR_ARG, "null key");
-    if (mode == OTC_MODE_CTR || mode == OTC_MODE_CBC_DEC) {
-        if (!ivc) return set_err(OTC_ERR_ARG, "null iv/counter");
-        if (int r = check_key(k, mode == OTC_MODE_CTR ? OTC_DIR_ENCRYPT : OTC_DIR_DECRYPT)) return r;
-    } else if (int r = check_key(k, k->dir)) {
-        return r;
-    }
-    if (host_in != host_out && nbytes) {
-        const uintptr_t a = (uintptr_t)host_in, b = (uintptr_t)host_out;
-        if (a < b + nbytes && b < a + nbytes) return set_err(OTC_ERR_ARG, "input and output overlap partially");
-    }
-    return OTC_OK;
-}
-
-static int run_chunk(int mode, const void *din, void *dout, size_t n, const otc_aes_key *k, const uint8_t ivc[16],
-                     uint64_t blk0, const uint8_t *halo, int impl, hipStream_t st)
-{
-    switch (mode) {
-    case OTC_MODE_CTR: return otc_aes_ctr(din, dout, n, k, ivc, blk0, impl, st);
-    case OTC_MODE_ECB: return otc_aes_ecb(din, dout, n, k, impl, st);
-    case OTC_MODE_CBC_DEC: return otc_aes_cbc_decrypt(din, dout, n, k, halo ? halo : ivc, st);
-    default: return set_err(OTC_ERR_ARG, "unsupported engine mode");
-    }
-}
-
-extern "C" int otc_engine_run(otc_engine *e, int mode, const void *host_in, void *host_out, size_t nbytes,
-                              const otc_aes_key *k, const uint8_t ivc[16], uint64_t block_offset, int impl,
-                              otc_stream_stats *stats)
-{
-    Range rg("otc_engine_run");
-    if (!e) return set_err(OTC_ERR_ARG, "null engine");
-    if (int r = check_stream_args(mode, host_in, host_out, nbytes, k, ivc)) return r;
-    if (mode == OTC_MODE_CBC_DEC && block_offset) return set_err(OTC_ERR_ARG, "CBC: pass the halo as iv instead");
-    HIPCHK(hipSetDevice(e->device));
-    auto t0 = std::chrono::steady_clock::now();
-    const bool pin_in = is_pinned(host_in), pin_out = is_pinned(host_out);
-    for (int i = 0; i < e->depth; ++i) {
-        if (!pin_in && !e->h_in[i]) HIPCHK(hipHostMalloc(&e->h_in[i], e->chunk, hipHostMallocDefault));
-        if (!pin_out && !e->h_out[i]) HIPCHK(hipHostMalloc(&e->h_out[i], e->chunk, hipHostMallocDefault));
-    }
-    const size_t C = e->chunk;
-    const size_t nchunks = (nbytes + C - 1) / C;
-    const uint8_t *hin = (const uint8_t *)host_in;
-    uint8_t *hout = (uint8_t *)host_out;
-    double kms = 0.0;
-    std::vector<int> slot_used(e->depth, 0);
-
-    for (size_t c = 0; c < nchunks; ++c) {
-        const int s = (int)(c % e->depth);
-        const size_t off = c * C;
-        const size_t n = std::min(C, nbytes - off);
-        /* slot reuse: wait until the D2H that last used this slot finished */
-        if (slot_used[s]) {
-            HIPCHK(hipEventSynchronize(e->ev_d2h[s]));
-            float ms = 0.f;
-            if (hipEventElapsedTime(&ms, e->ev_k0[s], e->ev_k[s]) == hipSuccess) kms += ms;
-            if (!pin_out) {
-                const size_t poff = (c - e->depth) * C;
-                memcpy(hout + poff, e->h_out[s], std::min(C, nbytes - poff));
-            }
-        }
-        const void *src = hin + off;
-        if (!pin_in) {
-            memcpy(e->h_in[s], hin + off, n);
-            src = e->h_in[s];
-        }
-        HIPCHK(hipMemcpyAsync(e->d_in[s], src, n, hipMemcpyHostToDevice, e->s_h2d));
-        HIPCHK(hipEventRecord(e->ev_h2d[s], e->s_h2d));
-        HIPCHK(hipStreamWaitEvent(e->s_k, e->ev_h2d[s], 0));
-        HIPCHK(hipEventRecord(e->ev_k0[s], e->s_k));
-        uint8_t halo[16];
-        const uint8_t *hp = nullptr;
-        if (mode == OTC_MODE_CBC_DEC && off > 0) {
-            memcpy(halo, hin + off - 16, 16); /* previous ciphertext block */
-            hp = halo;
-        }
-        int r = run_chunk(mode, e->d_in[s], e->d_out[s], n, k, ivc, block_offset + off / 16, hp, impl, e->s_k);
-        if (r) return r;
-        HIPCHK(hipEventRecord(e->ev_k[s], e->s_k));
-        HIPCHK(hipStreamWaitEvent(e->s_d2h, e->ev_k[s], 0));
-        void *dst = pin_out ? (void *)(hout + off) : e->h_out[s];
-        HIPCHK(hipMemcpyAsync(dst, e->d_out[s], n, hipMemcpyDeviceToHost, e->s_d2h));
-        HIPCHK(hipEventRecord(e->ev_d2h[s], e->s_d2h));
-        slot_used[s] = 1;
-    }
-    /* drain */
-    for (size_t c = (nchunks > (size_t)e->depth ? nchunks - e->depth : 0); c < nchunks; ++c) {
-        const int s = (int)(c % e->depth);
-        HIPCHK(hipEventSynchronize(e->ev_d2h[s]));
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, e->ev_k0[s], e->ev_k[s]) == hipSuccess) kms += ms;
-        if (!pin_out) {
-            const size_t off = c * C;
-            memcpy(hout + off, e->h_out[s], std::min(C, nbytes - off));
-        }
-    }
-    auto t1 = std::chrono::steady_clock::now();
-    if (stats) {
-        stats->total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-        stats->kernel_ms = kms;
-        stats->h2d_ms = stats->d2h_ms = 0.0;
-        stats->bytes = nbytes;
-        stats->chunks = (int)nchunks;
-    }
-    return OTC_OK;
-}
-
-/* ---- L4 multi-GPU (single process) -------------------------------------- */
-/* ---- RCCL root scatter / gather (otc_multi_run strategy 1) -----------------
- * Root GPU 0 ingests the host stream, ncclScatter deals equal S-byte pieces to
- * every GPU over xGMI, each GPU runs the cipher, ncclGather collects the
- * results at the root, which drains them to the host.  Two root buffer sets
- * are used in ping-pong: H2D of round r+1 (copy stream) and D2H of round r-1
- * (copy stream) overlap the scatter/compute/gather of round r, ordered by
- * events.  ncclScatter needs equal counts, so the last round is zero padded.
- *
- * Failure detection: waits poll hipStreamQuery and ncclCommGetAsyncError with a
- * watchdog (OTC_RCCL_TIMEOUT_S, default 600 s); on an async error or timeout
- * every communicator is aborted (ncclCommAbort) instead of destroyed, so a
- * hung peer cannot hang the caller.  All resources are owned by RcclJob and
- * released on every exit path. */
-struct RcclJob {
-    int n = 0;
-    size_t S = 0;                         /* per-GPU bytes per round */
-    std::vector<ncclComm_t> comms;
-    std::vector<hipStream_t> st;          /* per GPU: scatter, cipher, gather */
-    std::vector<void *> dsh, dsh_out;     /* per GPU S-byte piece (in / out) */
-    hipStream_t h2d = nullptr, d2h = nullptr;  /* root copy streams */
-    void *root_in[2] = {nullptr, nullptr}, *root_out[2] = {nullptr, nullptr};
-    hipEvent_t ev_in[2] = {}, ev_scattered[2] = {}, ev_gathered[2] = {}, ev_drained[2] = {};
-    bool failed = false;
-
-    ~RcclJob()
-    {
-        for (int g = 0; g < n; ++g) {
-            (void)hipSetDevice(g);
-            if (!failed && st[g]) (void)hipStreamSynchronize(st[g]);
-        }
-        (void)hipSetDevice(0);
-        if (!failed) {
-            if (h2d) (void)hipStreamSynchronize(h2d);
-            if (d2h) (void)hipStreamSynchronize(d2h);
-        }
-        for (int g = 0; g < n; ++g) {
-            if (comms[g]) {
-                if (failed) ncclCommAbort(comms[g]);
-                else ncclCommDestroy(comms[g]);
-            }
-        }
-        for (int g = 0; g < n; ++g) {
-            (void)hipSetDevice(g);
-            if (dsh[g]) (void)hipFree(dsh[g]);
-            if (dsh_out[g]) (void)hipFree(dsh_out[g]);
-            if (st[g]) (void)hipStreamDestroy(st[g]);
-        }
-        (void)hipSetDevice(0);
-        for (int i = 0; i < 2; ++i) {
-            if (root_in[i]) (void)hipFree(root_in[i]);
-            if (root_out[i]) (void)hipFree(root_out[i]);
-            for (hipEvent_t ev : {ev_in[i], ev_scattered[i], ev_gathered[i], ev_drained[i]})
-                if (ev) (void)hipEventDestroy(ev);
-        }
-        if (h2d) (void)hipStreamDestroy(h2d);
-        if (d2h) (void)hipStreamDestroy(d2h);
-    }
-
-    /* wait for `s` while watching every communicator */
-    int wait(hipStream_t s, double timeout_s)
-    {
-        auto t0 = std::chrono::steady_clock::now();
-        for (;;) {
-            hipError_t q = hipStreamQuery(s);
-            if (q == hipSuccess) return OTC_OK;
-            if (q != hipErrorNotReady) {
-                failed = true;
-                return hip_fail(q, "hipStreamQuery (RCCL job)");
-            }
-            for (int g = 0; g < n; ++g) {
-                ncclResult_t ae = ncclSuccess;
-                if (ncclCommGetAsyncError(comms[g], &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
-                    failed = true;
-                    return set_err(OTC_ERR_RCCL, std::string("RCCL async error on GPU ") + std::to_string(g) + ": " +
-                                                     ncclGetErrorString(ae));
-                }
-            }
-            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
-                failed = true;
-                return set_err(OTC_ERR_RCCL, "RCCL collective timed out (OTC_RCCL_TIMEOUT_S)");
-            }
-            std::this_thread::sleep_for(std::chrono::microseconds(50));
-        }
-    }
-};
-
-static int rccl_job_init(RcclJob &J, int ngpus, size_t S)
-{
-    J.n = ngpus;
-    J.S = S;
-    J.comms.assign(ngpus, nullptr);
-    J.st.assign(ngpus, nullptr);
-    J.dsh.assign(ngpus, nullptr);
-    J.dsh_out.assign(ngpus, nullptr);
-    std::vector<int> devs(ngpus);
-    for (int g = 0; g < ngpus; ++g) devs[g] = g;
-    RCCLCHK(ncclCommInitAll(J.comms.data(), ngpus, devs.data()));
-    const size_t round = S * (size_t)ngpus;
-    for (int g = 0; g < ngpus; ++g) {
-        HIPCHK(hipSetDevice(g));
-        HIPCHK(hipStreamCreateWithFlags(&J.st[g], hipStreamNonBlocking));
-        HIPCHK(hipMalloc(&J.dsh[g], S));
-        HIPCHK(hipMalloc(&J.dsh_out[g], S));
-    }
-    HIPCHK(hipSetDevice(0));
-    HIPCHK(hipStreamCreateWithFlags(&J.h2d, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&J.d2h, hipStreamNonBlocking));
-    for (int i = 0; i < 2; ++i) {
-        HIPCHK(hipMalloc(&J.root_in[i], round));
-        HIPCHK(hipMalloc(&J.root_out[i], round));
-        for (hipEvent_t *ev : {&J.ev_in[i], &J.ev_scattered[i], &J.ev_gathered[i], &J.ev_drained[i]})
-            HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
-    }
-    return OTC_OK;
-}
-
-/* The communicators, streams and buffers of the last job are cached across
- * calls (ncclCommInitAll + allocation cost ~0.4 s, more than streaming 8 GiB);
- * a different GPU count or round size rebuilds them, a failure aborts them,
- * otc_multi_release() frees them.  Never torn down by a static destructor:
- * at process exit the HIP runtime may already be gone. */
-std::mutex g_rccl_mu;
-RcclJob *g_rccl = nullptr;
-
-/* strategy 0 (direct ingest): one cached pipeline engine per GPU */
-std::mutex g_direct_mu;
-std::vector<otc_engine *> g_direct;
-
-static int rccl_job_run(RcclJob &J, int mode, const uint8_t *hin, uint8_t *hout, size_t nbytes,
-                        const otc_aes_key *k, const uint8_t ivc[16], int impl, double timeout_s);
-
-static int rccl_scatter_gather(int ngpus, int mode, const uint8_t *hin, uint8_t *hout, size_t nbytes,
-                               const otc_aes_key *k, const uint8_t ivc[16], int impl, size_t chunk_bytes)
-{
-    const char *to = getenv("OTC_RCCL_TIMEOUT_S");
-    const double timeout_s = to ? atof(to) : 600.0;
-    size_t S = chunk_bytes ? chunk_bytes : (size_t)64 << 20; /* per-GPU bytes per round */
-    S = (S + 15) & ~(size_t)15;
-    std::lock_guard<std::mutex> lk(g_rccl_mu);
-    if (g_rccl && (g_rccl->n != ngpus || g_rccl->S != S)) {
-        delete g_rccl;
-        g_rccl = nullptr;
-    }
-    if (!g_rccl) {
-        RcclJob *J = new RcclJob;
-        if (int r = rccl_job_init(*J, ngpus, S)) {
-            delete J;
-            return r;
-        }
-        g_rccl = J;
-    }
-    int rc = rccl_job_run(*g_rccl, mode, hin, hout, nbytes, k, ivc, impl, timeout_s);
-    if (rc) { /* unknown state: abort the communicators, rebuild next time */
-        g_rccl->failed = true;
-        delete g_rccl;
-        g_rccl = nullptr;
-    }
-    return rc;
-}
-
-static int rccl_job_run(RcclJob &J, int mode, const uint8_t *hin, uint8_t *hout, size_t nbytes,
-                        const otc_aes_key *k, const uint8_t ivc[16], int impl, double timeout_s)
-{
-    const int ngpus = J.n;
-    const size_t S = J.S, round = S * (size_t)ngpus;
-    const size_t nrounds = (nbytes + round - 1) / round;
-    for (size_t r = 0; r < nrounds; ++r) {
-        const int b = (int)(r & 1);
-        const size_t off = r * round, n = std::min(round, nbytes - off);
-        HIPCHK(hipSetDevice(0));
-        /* root_in[b] is free once round r-2's scatter has read it */
-        if (r >= 2) HIPCHK(hipStreamWaitEvent(J.h2d, J.ev_scattered[b], 0));
-        if (n < round) HIPCHK(hipMemsetAsync(J.root_in[b], 0, round, J.h2d));
-        HIPCHK(hipMemcpyAsync(J.root_in[b], hin + off, n, hipMemcpyHostToDevice, J.h2d));
-        HIPCHK(hipEventRecord(J.ev_in[b], J.h2d));
-        HIPCHK(hipStreamWaitEvent(J.st[0], J.ev_in[b], 0));
-        RCCLCHK(ncclGroupStart());
-        for (int g = 0; g < ngpus; ++g)
-            RCCLCHK(ncclScatter(J.root_in[b], J.dsh[g], S, ncclUint8, 0, J.comms[g], J.st[g]));
-        RCCLCHK(ncclGroupEnd());
-        HIPCHK(hipSetDevice(0));
-        HIPCHK(hipEventRecord(J.ev_scattered[b], J.st[0]));
-        for (int g = 0; g < ngpus; ++g) {
-            const size_t goff = off + (size_t)g * S;
-            if (goff >= nbytes) continue;
-            HIPCHK(hipSetDevice(g));
-            const size_t gn = std::min(S, nbytes - goff);
-            uint8_t halo[16];
-            const uint8_t *hp = nullptr;
-            if (mode == OTC_MODE_CBC_DEC && goff > 0) {
-                memcpy(halo, hin + goff - 16, 16);
-                hp = halo;
-            }
-            if (int rr = run_chunk(mode, J.dsh[g], J.dsh_out[g], gn, k, ivc, goff / 16, hp, impl, J.st[g])) {
-                J.failed = true;
-                return rr;
-            }
-        }
-        /* root_out[b] is free once round r-2's D2H has drained it */
-        HIPCHK(hipSetDevice(0));
-        if (r >= 2) HIPCHK(hipStreamWaitEvent(J.st[0], J.ev_drained[b], 0));
-        RCCLCHK(ncclGroupStart());
-        for (int g = 0; g < ngpus; ++g)
-            RCCLCHK(ncclGather(J.dsh_out[g], J.root_out[b], S, ncclUint8, 0, J.comms[g], J.st[g]));
-        RCCLCHK(ncclGroupEnd());
-        HIPCHK(hipSetDevice(0));
-        HIPCHK(hipEventRecord(J.ev_gathered[b], J.st[0]));
-        HIPCHK(hipStreamWaitEvent(J.d2h, J.ev_gathered[b], 0));
-        HIPCHK(hipMemcpyAsync(hout + off, J.root_out[b], n, hipMemcpyDeviceToHost, J.d2h));
-        HIPCHK(hipEventRecord(J.ev_drained[b], J.d2h));
-        /* every buffer reuse is ordered by the events above, so the host only
-         * enqueues; it blocks in the copies when the host buffers are pageable
-         * (pin them -- otc_host_register -- for H2D/D2H overlap) */
-    }
-    HIPCHK(hipSetDevice(0));
-    if (int w = J.wait(J.st[0], timeout_s)) return w;
-    if (int w = J.wait(J.d2h, timeout_s)) return w;
-    return OTC_OK;
-}
-
-extern "C" void otc_multi_release(void)
-{
-    {
-        std::lock_guard<std::mutex> lk(g_rccl_mu);
-        delete g_rccl;
-        g_rccl = nullptr;
-    }
-    std::lock_guard<std::mutex> lk(g_direct_mu);
-    for (otc_engine *&e : g_direct) {
-        otc_engine_destroy(e);
-        e = nullptr;
-    }
-}
-
-extern "C" int otc_multi_run(int ngpus, int strategy, int mode, const void *host_in, void *host_out, size_t nbytes,
-                             const otc_aes_key *k, const uint8_t ivc[16], int impl, size_t chunk_bytes,
-                             otc_multi_stats *stats)
-{
-    Range rg("otc_multi_run");
-    if (int r = check_stream_args(mode, host_in, host_out, nbytes, k, ivc)) return r;
-    int ndev = otc_device_count();
-    if (ngpus < 1 || ngpus > ndev) return set_err(OTC_ERR_ARG, "ngpus out of range");
-    const size_t nblk = (nbytes + 15) / 16;
-    /* planner: contiguous block-aligned shards, remainder spread over the
-     * first shards (nothing dropped, unlike reference test.c:50) */
-    std::vector<size_t> boff(ngpus + 1, 0);
-    for (int g = 0; g < ngpus; ++g) boff[g + 1] = boff[g] + nblk / ngpus + ((size_t)g < nblk % ngpus ? 1 : 0);
-    auto t0 = std::chrono::steady_clock::now();
-    int rc = OTC_OK;
-
-    if (strategy == 0) {
-        /* one host thread per GPU, each driving that GPU's cached pipeline
-         * engine (pinned ring + 3 streams: created on first use, reused by
-         * later calls with the same chunk size, freed by otc_multi_release).
-         * Error messages are thread_local: a worker's is carried back so
-         * otc_last_error() on the calling thread reports it. */
-        std::lock_guard<std::mutex> lk(g_direct_mu);
-        const size_t C = chunk_bytes ? ((chunk_bytes + 15) & ~(size_t)15) : (256ull << 20);
-        if (g_direct.size() < (size_t)ngpus) g_direct.resize(ngpus, nullptr);
-        std::vector<std::thread> th;
-        std::vector<int> res(ngpus, 0);
-        std::vector<std::string> msg(ngpus);
-        for (int g = 0; g < ngpus; ++g) {
-            th.emplace_back([&, g]() {
-                const size_t b0 = std::min(boff[g] * 16, nbytes), b1 = std::min(boff[g + 1] * 16, nbytes);
-                if (b1 <= b0) return;
-                otc_engine *&e = g_direct[g];
-                if (e && e->chunk != C) {
-                    otc_engine_destroy(e);
-                    e = nullptr;
-                }
-                if (!e) e = otc_engine_create(g, C, 3);
-                if (!e) {
-                    res[g] = OTC_ERR_NOMEM;
-                    msg[g] = g_err;
-                    return;
-                }
-                uint8_t iv_local[16];
-                const uint8_t *ivp = ivc;
-                uint64_t bo = 0;
-                if (mode == OTC_MODE_CBC_DEC) {
-                    if (b0 > 0) { memcpy(iv_local, (const uint8_t *)host_in + b0 - 16, 16); ivp = iv_local; }
-                } else if (mode == OTC_MODE_CTR) {
-                    bo = b0 / 16;
-                }
-                res[g] = otc_engine_run(e, mode, (const uint8_t *)host_in + b0, (uint8_t *)host_out + b0, b1 - b0, k,
-                                        ivp, bo, impl, nullptr);
-                if (res[g]) {
-                    msg[g] = g_err;
-                    otc_engine_destroy(e); /* unknown state: rebuild next time */
-                    e = nullptr;
-                }
-            });
-        }
-        for (auto &t : th) t.join();
-        for (int g = 0; g < ngpus; ++g)
-            if (res[g]) {
-                rc = res[g];
-                set_err(rc, "GPU " + std::to_string(g) + ": " + msg[g]);
-            }
-    } else {
-        rc = rccl_scatter_gather(ngpus, mode, (const uint8_t *)host_in, (uint8_t *)host_out, nbytes, k, ivc, impl,
-                                 chunk_bytes);
-    }
-    auto t1 = std::chrono::steady_clock::now();
-    if (stats) {
-        stats->total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-        stats->gbps = stats->total_ms > 0 ? (double)nbytes / (stats->total_ms * 1e6) : 0.0;
-        stats->ngpus = ngpus;
-        stats->strategy = strategy;
-    }
-    return rc;
-}
-
-extern "C" int otc_multi_ctr_resident(int ngpus, void *const *dev_bufs, size_t shard_bytes, const otc_aes_key *k,
-                                      const uint8_t ctr0[16], int impl, double *elapsed_ms)
-{
-    Range rg("otc_multi_ctr_resident");
-    if (ngpus < 1 || ngpus > otc_device_count()) return set_err(OTC_ERR_ARG, "ngpus out of range");
-    if (shard_bytes % 16) return set_err(OTC_ERR_ARG, "shard must be a multiple of 16");
-    std::vector<hipStream_t> st(ngpus);
-    for (int g = 0; g < ngpus; ++g) {
-        HIPCHK(hipSetDevice(g));
-        HIPCHK(hipStreamCreateWithFlags(&st[g], hipStreamNonBlocking));
-        HIPCHK(hipDeviceSynchronize());
-    }
-    auto t0 = std::chrono::steady_clock::now();
-    for (int g = 0; g < ngpus; ++g) {
-        HIPCHK(hipSetDevice(g));
-        int r = otc_aes_ctr(dev_bufs[g], dev_bufs[g], shard_bytes, k, ctr0, (uint64_t)g * (shard_bytes / 16), impl, st[g]);
-        if (r) return r;
-    }
-    for (int g = 0; g < ngpus; ++g) {
-        HIPCHK(hipSetDevice(g));
-        HIPCHK(hipStreamSynchronize(st[g]));
-    }
-    auto t1 = std::chrono::steady_clock::now();
-    for (int g = 0; g < ngpus; ++g) {
-        (void)hipSetDevice(g);
-        (void)hipStreamDestroy(st[g]);
-    }
-    if (elapsed_ms) *elapsed_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    return OTC_OK;
 }
 
 extern "C" const char *otc_build_info(void)

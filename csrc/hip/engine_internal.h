@@ -1,0 +1,57 @@
+/*
+ * engine_internal.h -- helpers shared by the host runtime translation units
+ * (engine.cpp: device ops / keys / info; pipeline.cpp: host streaming engine
+ * and multi-GPU jobs).  Not part of the public C API (otc.h).
+ */
+#ifndef OTC_ENGINE_INTERNAL_H
+#define OTC_ENGINE_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include <string>
+
+#include "otc.h"
+#include "otc_device.h"
+
+namespace otc_rt {
+
+using otc_dev::Ctr128;
+
+/* error message of the last failing call on this thread (otc_last_error) */
+int set_err(int code, const std::string &msg);
+std::string last_err();
+int hip_fail(hipError_t e, const char *what);
+
+Ctr128 ctr_from_bytes(const uint8_t c[16]);
+Ctr128 ctr_add(Ctr128 c, uint64_t n, bool wrap64);
+int check_key(const otc_aes_key *k, int dir);
+
+/* roctx range for rocprofv3 --marker-trace (a no-op unless a tool is
+ * attached): every public entry point is one named range. */
+struct Range {
+    explicit Range(const char *name) { roctxRangePushA(name); }
+    ~Range() { roctxRangePop(); }
+    Range(const Range &) = delete;
+    Range &operator=(const Range &) = delete;
+};
+
+/* releases the hybrid-CTR auxiliary stream pool (engine.cpp) */
+void aux_release_all();
+
+} // namespace otc_rt
+
+#define HIPCHK(expr)                                                  \
+    do {                                                              \
+        hipError_t _e = (expr);                                       \
+        if (_e != hipSuccess) return otc_rt::hip_fail(_e, #expr);     \
+    } while (0)
+
+#define RCCLCHK(expr)                                                                               \
+    do {                                                                                            \
+        ncclResult_t _r = (expr);                                                                   \
+        if (_r != ncclSuccess)                                                                      \
+            return otc_rt::set_err(OTC_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+    } while (0)
+
+#endif

@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "otc.h"
 
 namespace otc_dev {
@@ -99,6 +101,23 @@ __device__ __forceinline__ void ctr_words(const Ctr128 &c, uint64_t idx, bool wr
     w1 = bswap32((uint32_t)hi);
     w2 = bswap32((uint32_t)(lo >> 32));
     w3 = bswap32((uint32_t)lo);
+}
+
+/* Host: CU count of the calling thread's current device, cached per device.
+ * Thread-safe (the multi-GPU paths launch from one host thread per GPU): the
+ * attribute is immutable, so a relaxed atomic cache is enough. */
+inline int device_cus()
+{
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::atomic<int> &slot = cache[(unsigned)dev & 63u];
+    int v = slot.load(std::memory_order_relaxed);
+    if (v <= 0) {
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        slot.store(v, std::memory_order_relaxed);
+    }
+    return v;
 }
 
 } // namespace otc_dev

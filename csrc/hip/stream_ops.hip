@@ -16,6 +16,8 @@
  * 16 KiB per wave; one wave per workgroup, up to 10 workgroups per CU.
  */
 #include <hip/hip_runtime.h>
+
+#include "otc_device.h"
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -456,17 +458,10 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     rc4_prga<MODE, AL>(S, lane4, i, j, len, src, out, base, live);
 }
 
-int g_cus_s = 0;
 int grid_stream(uint64_t items, int per_cu)
 {
-    if (g_cus_s <= 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&g_cus_s, hipDeviceAttributeMultiprocessorCount, dev);
-        if (g_cus_s <= 0) g_cus_s = 256;
-    }
     uint64_t need = (items + 255) / 256;
-    uint64_t cap = (uint64_t)g_cus_s * per_cu;
+    uint64_t cap = (uint64_t)otc_dev::device_cus() * per_cu;
     if (need < 1) need = 1;
     return (int)(need < cap ? need : cap);
 }
@@ -512,15 +507,19 @@ hipError_t k_clock(uint64_t *out, uint64_t delay_ticks, uint64_t ticks, hipStrea
 
 hipError_t k_xor(const void *a, const void *b, void *out, size_t n, hipStream_t st)
 {
-    /* OTC_XOR_VARIANT="U,per_cu,nt" (A/B only) */
-    static int U = 1, per_cu = 8, nt = 0;
-    static bool init = false;
-    if (!init) {
-        if (const char *e = getenv("OTC_XOR_VARIANT")) sscanf(e, "%d,%d,%d", &U, &per_cu, &nt);
-        if (U != 1 && U != 2 && U != 4 && U != 8) U = 1;
-        if (per_cu < 1 || per_cu > 64) per_cu = 8;
-        init = true;
-    }
+    /* OTC_XOR_VARIANT="U,per_cu,nt" (A/B only); read once, thread-safe
+     * (function-local static initialisation) */
+    struct Cfg {
+        int U = 1, per_cu = 8, nt = 0;
+    };
+    static const Cfg cfg = [] {
+        Cfg c;
+        if (const char *e = getenv("OTC_XOR_VARIANT")) sscanf(e, "%d,%d,%d", &c.U, &c.per_cu, &c.nt);
+        if (c.U != 1 && c.U != 2 && c.U != 4 && c.U != 8) c.U = 1;
+        if (c.per_cu < 1 || c.per_cu > 64) c.per_cu = 8;
+        return c;
+    }();
+    const int U = cfg.U, per_cu = cfg.per_cu, nt = cfg.nt;
     auto kern = nt ? (U == 1   ? k_xor_kernel<1, true>
                       : U == 2 ? k_xor_kernel<2, true>
                       : U == 4 ? k_xor_kernel<4, true>
@@ -582,8 +581,7 @@ hipError_t k_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t 
     static const int wg_env = getenv("OTC_RC4_WG_PER_CU") ? atoi(getenv("OTC_RC4_WG_PER_CU")) : -1;
     int wg_cap = wg_env;
     if (wg_env < 0) {
-        (void)grid_stream(1, 1); /* initialises the CU count */
-        const uint64_t cus = (uint64_t)g_cus_s;
+        const uint64_t cus = (uint64_t)otc_dev::device_cus();
         wg_cap = (wgs > 9 * cus && wgs <= 10 * cus) ? 6 : 0;
     }
     /* OTC_RC4_KSA16=0: generic KSA for every key length (A/B only) */

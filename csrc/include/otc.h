@@ -209,16 +209,26 @@ void otc_engine_destroy(otc_engine *e);
 #define OTC_MODE_XOR 3
 
 typedef struct {
-    double total_ms;    /* wall time of the whole call */
-    double kernel_ms;   /* sum of kernel times (hipEvent) */
-    double h2d_ms, d2h_ms;
+    double total_ms;      /* wall time of the whole call */
+    double kernel_ms;     /* sum of kernel times (hipEvent, kernel stream) */
+    double h2d_ms, d2h_ms; /* sum of copy times (hipEvent, copy streams) */
+    double host_stage_ms; /* host memcpy into / out of the pinned ring (pageable callers) */
     size_t bytes;
     int chunks;
+    int numa_node;        /* node of the pinned ring (-1: unknown / OTC_NUMA=0) */
 } otc_stream_stats;
 
 int otc_engine_run(otc_engine *e, int mode, const void *host_in, void *host_out, size_t nbytes,
                    const otc_aes_key *k, const uint8_t iv_or_ctr[16], uint64_t block_offset,
                    int impl, otc_stream_stats *stats);
+
+/* NUMA placement (csrc/cpu/numa.c): the GPU's node from sysfs (-1 unknown);
+ * the engine allocates its pinned ring there.  otc_engine_staging returns the
+ * ring's input slot (NULL until a pageable run allocated it) so tests can
+ * check where its pages live (otc_numa_node_of_addr in otc_numa.h). */
+int otc_device_numa_node(int dev);
+int otc_engine_numa_node(const otc_engine *e);
+const void *otc_engine_staging(const otc_engine *e, int slot);
 
 /* Where a pointer lives: pageable host memory, pinned host memory, or device
  * memory (decides between the kernels and the host pipeline). */
@@ -235,7 +245,9 @@ void *otc_host_alloc_pinned(size_t nbytes);
 void otc_host_free_pinned(void *p);
 
 /* ---- L4 multi-GPU (single process, RCCL over xGMI) -----------------------
- * Shard one host-resident CTR/ECB/CBC-dec stream over `ngpus` devices.
+ * Shard one host-resident CTR/ECB/CBC-dec stream over `ngpus` devices
+ * (strategy 0 with OTC_SHARE_GPUS=1: `ngpus` logical shards mapped onto the
+ * visible devices round-robin, to rehearse N shards on fewer GPUs).
  * strategy 0 = direct ingest (each GPU streams its own shard from pinned host
  * memory, engine pipeline per GPU, one host thread per GPU);
  * strategy 1 = RCCL root scatter/gather (root H2D, ncclScatter over xGMI,
@@ -248,6 +260,7 @@ typedef struct {
     double gbps;
     int ngpus;
     int strategy;
+    int numa_nodes_used; /* strategy 0: distinct NUMA nodes the shard threads ran on */
 } otc_multi_stats;
 
 int otc_multi_run(int ngpus, int strategy, int mode, const void *host_in, void *host_out,
@@ -255,8 +268,10 @@ int otc_multi_run(int ngpus, int strategy, int mode, const void *host_in, void *
                   size_t chunk_bytes, otc_multi_stats *stats);
 
 /* Free the RCCL communicators / buffers that strategy 1 caches between calls
- * (rebuilt on demand). */
+ * and the per-shard engines of strategy 0 (rebuilt on demand). */
 void otc_multi_release(void);
+/* otc_multi_release + the pooled auxiliary streams of the hybrid CTR path. */
+void otc_release_resources(void);
 
 /* Device-resident multi-GPU CTR: buffers dev_bufs[g] (already on GPU g) hold
  * shard g of `shard_bytes`; all GPUs encrypt in place concurrently with the

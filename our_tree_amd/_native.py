@@ -75,8 +75,10 @@ class StreamStats(ctypes.Structure):
         ("kernel_ms", ctypes.c_double),
         ("h2d_ms", ctypes.c_double),
         ("d2h_ms", ctypes.c_double),
+        ("host_stage_ms", ctypes.c_double),
         ("bytes", ctypes.c_size_t),
         ("chunks", ctypes.c_int),
+        ("numa_node", ctypes.c_int),
     ]
 
 
@@ -86,6 +88,7 @@ class MultiStats(ctypes.Structure):
         ("gbps", ctypes.c_double),
         ("ngpus", ctypes.c_int),
         ("strategy", ctypes.c_int),
+        ("numa_nodes_used", ctypes.c_int),
     ]
 
 
@@ -120,6 +123,14 @@ def _declare_cpu(lib):
         "AES_CTR_encrypt": (None, [c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int]),
         "AES_CTR_encrypt_at": (None, [c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int, ctypes.c_ulonglong]),
         "otc_bitslice_selftest": (c_int, [c_int]),
+        "otc_parse_cpulist": (c_int, [ctypes.c_char_p, c_u8p, c_int]),
+        "otc_numa_node_of_pci": (c_int, [ctypes.c_char_p, ctypes.c_char_p]),
+        "otc_numa_node_cpus": (c_int, [ctypes.c_char_p, c_int, c_u8p, c_int]),
+        "otc_numa_num_nodes": (c_int, [ctypes.c_char_p]),
+        "otc_numa_bind_thread": (c_int, [c_int]),
+        "otc_numa_alloc": (c_vp, [c_sz, c_int]),
+        "otc_numa_free": (None, [c_vp, c_sz]),
+        "otc_numa_node_of_addr": (c_int, [c_vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -151,6 +162,10 @@ def _declare_gpu(lib):
         "otc_AES_ECB_decrypt": (c_int, [c_vp, c_vp, ctypes.c_ulong, c_u8p, c_int, c_vp]),
         "otc_AES_CTR_encrypt": (c_int, [c_vp, c_vp, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int, c_vp]),
         "otc_multi_release": (None, []),
+        "otc_release_resources": (None, []),
+        "otc_device_numa_node": (c_int, [c_int]),
+        "otc_engine_numa_node": (c_int, [c_vp]),
+        "otc_engine_staging": (c_vp, [c_vp, c_int]),
         "otc_device_count": (c_int, []),
         "otc_device_cus": (c_int, [c_int]),
         "otc_device_clock_khz": (c_int, [c_int]),

@@ -78,8 +78,21 @@ class StreamEngine:
         rc = self._lib.otc_engine_run(self._h, MODES[mode], _ptr(host_in), _ptr(host_out), n, ctypes.byref(k), ivb,
                                       block_offset, {"auto": 0, "ttable": 1, "bitslice": 2}[impl], ctypes.byref(st))
         _native.check(rc, "otc_engine_run")
-        return {"total_ms": st.total_ms, "kernel_ms": st.kernel_ms, "bytes": st.bytes, "chunks": st.chunks,
-                "gbps": st.bytes / (st.total_ms * 1e6) if st.total_ms else 0.0}
+        return {"total_ms": st.total_ms, "kernel_ms": st.kernel_ms, "h2d_ms": st.h2d_ms, "d2h_ms": st.d2h_ms,
+                "host_stage_ms": st.host_stage_ms, "bytes": st.bytes, "chunks": st.chunks,
+                "numa_node": st.numa_node, "gbps": st.bytes / (st.total_ms * 1e6) if st.total_ms else 0.0,
+                # per-direction PCIe rates over the time the copies were in flight
+                "h2d_gbps": st.bytes / (st.h2d_ms * 1e6) if st.h2d_ms else 0.0,
+                "d2h_gbps": st.bytes / (st.d2h_ms * 1e6) if st.d2h_ms else 0.0}
+
+    @property
+    def numa_node(self) -> int:
+        """NUMA node of this engine's pinned staging ring (-1: unknown)."""
+        return self._lib.otc_engine_numa_node(self._h)
+
+    def staging_ptr(self, slot: int = 0) -> int:
+        """Address of staging slot ``slot`` (0 until a pageable run allocated it)."""
+        return self._lib.otc_engine_staging(self._h, slot) or 0
 
 
 def multi_gpu_run(mode: str, host_in, host_out, key: bytes, iv_or_counter: bytes = bytes(16), ngpus: int = 1,
@@ -93,7 +106,26 @@ def multi_gpu_run(mode: str, host_in, host_out, key: bytes, iv_or_counter: bytes
                            ctypes.byref(k), ivb, {"auto": 0, "ttable": 1, "bitslice": 2}[impl], chunk_bytes,
                            ctypes.byref(st))
     _native.check(rc, "otc_multi_run")
-    return {"total_ms": st.total_ms, "gbps": st.gbps, "ngpus": st.ngpus, "strategy": strategy}
+    return {"total_ms": st.total_ms, "gbps": st.gbps, "ngpus": st.ngpus, "strategy": strategy,
+            "numa_nodes_used": st.numa_nodes_used}
+
+
+def multi_ctr_resident(bufs, key: bytes, counter: bytes, impl: str = "auto") -> float:
+    """In-place CTR over device-resident shards ``bufs[g]`` (on GPU g, equal
+    sizes, shard g at counter offset g * shard_blocks), all GPUs concurrently
+    from one host thread (otc_multi_ctr_resident).  Returns elapsed ms."""
+    lib = _native.require_gpu_lib()
+    n = bufs[0].numel()
+    if any(b.numel() != n or not b.is_cuda or b.device.index != g for g, b in enumerate(bufs)):
+        raise ValueError("bufs[g] must be equal-size tensors on cuda:g")
+    ptrs = (ctypes.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
+    k = expand_key(key)
+    ms = ctypes.c_double()
+    ivb = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(counter))
+    rc = lib.otc_multi_ctr_resident(len(bufs), ptrs, n, ctypes.byref(k), ivb,
+                                    {"auto": 0, "ttable": 1, "bitslice": 2}[impl], ctypes.byref(ms))
+    _native.check(rc, "otc_multi_ctr_resident")
+    return ms.value
 
 
 class _PinnedOwner:

@@ -133,3 +133,89 @@ def test_cli_gpu_selftest_and_file_job(gpu, tmp_path):
         assert main(["crypt", str(s), str(d), "--key", "22" * 16, "--iv", "ff" * 16, "--chunk", "64K"]) == 0
     assert mid.read_bytes() == cpu_ref.ctr(b"\x22" * 16, b"\xff" * 16, data)
     assert back.read_bytes() == data
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_engine_cbc_dec_in_place(gpu, pinned):
+    """host_in == host_out over many chunks: every chunk's halo (previous
+    ciphertext block) is captured before any D2H can overwrite it."""
+    n = (3 << 20) + 16 * 77
+    key, iv = os.urandom(16), os.urandom(16)
+    data = rnd_np(n, 5)
+    if pinned:
+        x = pstream.pinned_empty(n)
+        x[:] = data
+    else:
+        x = data.copy()
+    with pstream.StreamEngine(0, chunk_bytes=256 << 10, depth=3) as eng:
+        eng.run("cbc-dec", x, x, key, iv)
+    assert x.tobytes() == cpu_ref.cbc(key, iv, data.tobytes(), decrypt=True)
+
+
+def test_engine_stats_breakdown_and_numa(gpu):
+    """otc_stream_stats: kernel / H2D / D2H / host staging times from events,
+    and the pinned ring placed on the GPU's NUMA node."""
+    from our_tree_amd import _native
+
+    lib = _native.require_gpu_lib()
+    n = 8 << 20
+    x, y = rnd_np(n, 6), np.zeros(n, np.uint8)
+    key, ctr = os.urandom(16), os.urandom(16)
+    with pstream.StreamEngine(0, chunk_bytes=1 << 20, depth=3) as eng:
+        st = eng.run("ctr", x, y, key, ctr)
+        assert y.tobytes() == cpu_ref.ctr(key, ctr, x.tobytes())
+        assert st["kernel_ms"] > 0 and st["h2d_ms"] > 0 and st["d2h_ms"] > 0 and st["host_stage_ms"] > 0
+        assert st["h2d_gbps"] > 1 and st["d2h_gbps"] > 1
+        node = eng.numa_node
+        assert node == lib.otc_device_numa_node(0) == st["numa_node"]
+        if node >= 0:
+            assert lib.otc_numa_node_of_addr(eng.staging_ptr(0)) == node
+
+
+@pytest.mark.parametrize("nshards", [2, 4, 8])
+@pytest.mark.parametrize("mode", ["ctr", "cbc-dec"])
+def test_multi_direct_logical_shards(gpu, nshards, mode, monkeypatch):
+    """otc_multi_run(direct) with N logical shards mapped onto the visible
+    GPU(s) (OTC_SHARE_GPUS=1): N host threads, N engines, in place for CBC."""
+    monkeypatch.setenv("OTC_SHARE_GPUS", "1")
+    n = (1 << 20) * 3 + 16 * 13 + (7 if mode == "ctr" else 0)
+    key, iv = os.urandom(32), os.urandom(16)
+    x = rnd_np(n, 7 + nshards)
+    ref = cpu_ref.ctr(key, iv, x.tobytes()) if mode == "ctr" else cpu_ref.cbc(key, iv, x.tobytes(), decrypt=True)
+    y = x.copy() if mode == "cbc-dec" else np.zeros(n, np.uint8)
+    src = y if mode == "cbc-dec" else x
+    st = pstream.multi_gpu_run(mode, src, y, key, iv, ngpus=nshards, strategy="direct", chunk_bytes=256 << 10)
+    assert y.tobytes() == ref
+    assert st["ngpus"] == nshards and st["numa_nodes_used"] >= 0
+
+
+def test_multi_direct_refuses_oversubscription_without_share(gpu, monkeypatch):
+    monkeypatch.delenv("OTC_SHARE_GPUS", raising=False)
+    n = 1 << 16
+    x, y = rnd_np(n, 8), np.zeros(n, np.uint8)
+    with pytest.raises(RuntimeError, match="ngpus out of range"):
+        pstream.multi_gpu_run("ctr", x, y, os.urandom(16), os.urandom(16), ngpus=torch.cuda.device_count() + 1)
+
+
+def test_multi_rccl_cbc_dec_in_place_many_rounds(gpu):
+    """RCCL scatter/gather job, double-buffered pieces, in-place CBC-dec across
+    >2 rounds (buffer reuse two rounds later ordered by events)."""
+    ngpus = torch.cuda.device_count()
+    n = (5 << 20) + 16 * 3
+    key, iv = os.urandom(16), os.urandom(16)
+    data = rnd_np(n, 9)
+    x = data.copy()
+    pstream.multi_gpu_run("cbc-dec", x, x, key, iv, ngpus=ngpus, strategy="rccl", chunk_bytes=512 << 10)
+    assert x.tobytes() == cpu_ref.cbc(key, iv, data.tobytes(), decrypt=True)
+
+
+def test_multi_ctr_resident(gpu):
+    ngpus = torch.cuda.device_count()
+    key, ctr = os.urandom(16), (2**64 - 3).to_bytes(16, "big")
+    per = 16 * 4099
+    bufs = [torch.randint(0, 256, (per,), dtype=torch.uint8, device=f"cuda:{g}") for g in range(ngpus)]
+    src = b"".join(b.cpu().numpy().tobytes() for b in bufs)
+    ms = pstream.multi_ctr_resident(bufs, key, ctr)
+    assert ms > 0
+    got = b"".join(b.cpu().numpy().tobytes() for b in bufs)
+    assert got == cpu_ref.ctr(key, ctr, src)
