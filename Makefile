@@ -43,8 +43,8 @@ HIP_OBJ := $(patsubst csrc/hip/%.hip,$(OBJ)/hip/%.o,$(HIP_SRC)) $(OBJ)/hip/engin
 BINS := bin/test bin/aes_test bin/aes_ecb_e bin/aes_ecb_d bin/otbench bin/bc_test
 
 .PHONY: all cpu clean
-all: $(LIBDIR)/libotc.so $(LIBDIR)/libotc_cpu.so $(BINS) bin/test_cpu bin/aes_test_cpu
-cpu: $(LIBDIR)/libotc_cpu.so bin/test_cpu bin/aes_test_cpu
+all: $(LIBDIR)/libotc.so $(LIBDIR)/libotc_cpu.so $(BINS) bin/test_cpu bin/aes_test_cpu ref-o0
+cpu: $(LIBDIR)/libotc_cpu.so bin/test_cpu bin/aes_test_cpu ref-o0
 
 $(OBJ)/cpu/aesni.o: csrc/cpu/aesni.c csrc/include/aesni.h
 	@mkdir -p $(dir $@)
@@ -112,8 +112,39 @@ bin/bc_test: csrc/cli/bc_test.cpp csrc/include/otc_cipher.hpp $(LIBDIR)/libotc.s
 	@mkdir -p bin
 	$(CXX) -O2 -std=c++17 -Wall $(INC) $< -o $@ -L$(LIBDIR) -lotc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 
+# --- reference-methodology CPU baseline --------------------------------------
+# The reference's published CPU numbers were built at -O0 (reference
+# Makefile:13 "gcc -g -Wall -pedantic -O0 -std=gnu99", aes-modes/Makefile:15
+# "clang -O0 -msse4.1 -maes").  bin/test_o0 and bin/aes_test_o0 are the same
+# harnesses and oracle built the same way, for apples-to-apples rows against
+# the results.* logs (the -O2 builds above are the real CPU baseline).
+O0FLAGS := -g -Wall -pedantic -O0 -std=gnu99
+O0_OBJ  := $(patsubst csrc/cpu/%.c,$(OBJ)/o0/%.o,$(CPU_SRC)) $(OBJ)/o0/bs_selftest.o
+.PHONY: ref-o0
+ref-o0: bin/test_o0 bin/aes_test_o0
+
+$(OBJ)/o0/aesni.o: csrc/cpu/aesni.c csrc/include/aesni.h
+	@mkdir -p $(dir $@)
+	$(CC) $(O0FLAGS) -maes -msse4.1 -mssse3 $(INC) -c $< -o $@
+
+$(OBJ)/o0/%.o: csrc/cpu/%.c $(wildcard csrc/include/*.h)
+	@mkdir -p $(dir $@)
+	$(CC) $(O0FLAGS) $(INC) -c $< -o $@
+
+$(OBJ)/o0/bs_selftest.o: csrc/cpu/bs_selftest.cpp csrc/include/otc_bitslice.h
+	@mkdir -p $(dir $@)
+	$(CXX) -g -O0 -std=c++17 $(INC) -c $< -o $@
+
+bin/test_o0: csrc/cli/rc4_test.c $(O0_OBJ)
+	@mkdir -p bin
+	$(CXX) -O0 -g $(INC) -x c -std=gnu99 $< -x none $(O0_OBJ) -o $@ -lpthread
+
+bin/aes_test_o0: csrc/cli/aes_test.c $(O0_OBJ)
+	@mkdir -p bin
+	$(CXX) -O0 -g $(INC) -x c -std=gnu99 $< -x none $(O0_OBJ) -o $@ -lpthread
+
 clean:
-	rm -rf build $(LIBDIR)/*.so $(BINS) bin/test_cpu bin/aes_test_cpu
+	rm -rf build $(LIBDIR)/*.so $(BINS) bin/test_cpu bin/aes_test_cpu bin/test_o0 bin/aes_test_o0
 
 # Host sanitizers over the threaded CPU paths (also tests/test_sanitizers_cpu.py)
 SAN_SRC := csrc/cpu/aes.c csrc/cpu/arc4.c csrc/cli/san_driver.c

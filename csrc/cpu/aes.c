@@ -404,9 +404,10 @@ int aes_ecb_bulk(const aes_context *ctx, int mode, const unsigned char *input,
 }
 
 /* ---------------------------------------------------------------------------
- * Self test: FIPS-197 appendix C, SP 800-38A F.1/F.2/F.3/F.5, RFC 3686 #1-#3
- * (standard published vectors; the reference's Monte-Carlo vectors are not
- * reused).
+ * Self test: FIPS-197 appendix C, SP 800-38A F.1/F.2/F.3/F.5, RFC 3686 #1-#3,
+ * and the 10,000-iteration Monte-Carlo ECB/CBC chains of the NIST
+ * rijndael-vals set that the reference's self-test runs
+ * (/root/reference/aes-modes/aes.c:912-950 vectors, loop :1084-1200).
  * ------------------------------------------------------------------------- */
 static int hexval(char c)
 {
@@ -476,6 +477,58 @@ static int report(int verbose, const char *name, int ok)
 {
     if (verbose) printf("  %s: %s\n", name, ok ? "passed" : "failed");
     return ok ? 0 : 1;
+}
+
+/* Monte-Carlo results after 10,000 chained operations from an all-zero key
+ * (128/192/256), block and IV (NIST rijndael-vals) */
+static const char *MC_ECB_ENC[3] = {"c34c052cc0da8d73451afe5f03be297f", "f3f6752ae8d7831138f041560631b114",
+                                    "8b79eecc93a0ee5dff30b4ea21636da4"};
+static const char *MC_ECB_DEC[3] = {"44416ac2d1f53c583303917e6be9ebe0", "48e31e9e256718f29229319c19f15ba4",
+                                    "058ccffdbbcb382d1f6f56585d8a4ade"};
+static const char *MC_CBC_ENC[3] = {"8a05fc5e095af4848a08d328d3688e3d", "7bd966d53ad8c1bb85d2adfae87bb104",
+                                    "fe3c53653e2f45b56fcd88b2cc898ff0"};
+static const char *MC_CBC_DEC[3] = {"faca37e0b0c85373df706e73f7c9af86", "5df678dd17ba4e75b61768c6adef7c7b",
+                                    "4804e1818fe6297519a3e88c57310413"};
+
+int aes_monte_carlo(int mode, int bits, unsigned char result[16])
+{
+    unsigned char key[32] = {0}, buf[16] = {0}, iv[16] = {0}, prv[16] = {0};
+    aes_context ctx;
+    const int dec = (mode == AES_MC_ECB_DEC || mode == AES_MC_CBC_DEC);
+    int r = dec ? aes_setkey_dec(&ctx, key, (unsigned)bits) : aes_setkey_enc(&ctx, key, (unsigned)bits);
+    if (r) return r;
+    for (int j = 0; j < 10000; ++j) {
+        switch (mode) {
+        case AES_MC_ECB_ENC: aes_crypt_ecb(&ctx, AES_ENCRYPT, buf, buf); break;
+        case AES_MC_ECB_DEC: aes_crypt_ecb(&ctx, AES_DECRYPT, buf, buf); break;
+        case AES_MC_CBC_DEC: aes_crypt_cbc(&ctx, AES_DECRYPT, 16, iv, buf, buf); break;
+        case AES_MC_CBC_ENC: { /* the ciphertext becomes the next IV (in iv) and the
+                                  previous ciphertext the next plaintext */
+            unsigned char tmp[16];
+            aes_crypt_cbc(&ctx, AES_ENCRYPT, 16, iv, buf, buf);
+            memcpy(tmp, prv, 16);
+            memcpy(prv, buf, 16);
+            memcpy(buf, tmp, 16);
+            break;
+        }
+        default: return POLARSSL_ERR_AES_INVALID_INPUT_LENGTH;
+        }
+    }
+    memcpy(result, mode == AES_MC_CBC_ENC ? prv : buf, 16);
+    return 0;
+}
+
+const char *aes_monte_carlo_expected(int mode, int bits)
+{
+    const int k = (bits - 128) / 64;
+    if (k < 0 || k > 2 || bits % 64) return NULL;
+    switch (mode) {
+    case AES_MC_ECB_ENC: return MC_ECB_ENC[k];
+    case AES_MC_ECB_DEC: return MC_ECB_DEC[k];
+    case AES_MC_CBC_ENC: return MC_CBC_ENC[k];
+    case AES_MC_CBC_DEC: return MC_CBC_DEC[k];
+    default: return NULL;
+    }
 }
 
 int aes_self_test(int verbose)
@@ -569,7 +622,16 @@ int aes_self_test(int verbose)
         snprintf(name, sizeof name, "RFC 3686 AES-CTR test vector #%d", v + 1);
         fails += report(verbose, name, memcmp(out, ref, n) == 0);
     }
-    /* restore SP plaintext for callers that inspect nothing -- no state kept */
+    static const char *mc_name[4] = {"ECB", "ECB", "CBC", "CBC"};
+    for (int mode = 0; mode < 4; ++mode)
+        for (int k = 0; k < 3; ++k) {
+            const int bits = 128 + 64 * k;
+            unsigned char got[16];
+            unhex(aes_monte_carlo_expected(mode, bits), ref);
+            snprintf(name, sizeof name, "AES-%s-%d (%s) Monte-Carlo x10000", mc_name[mode], bits,
+                     (mode & 1) ? "dec" : "enc");
+            fails += report(verbose, name, aes_monte_carlo(mode, bits, got) == 0 && memcmp(got, ref, 16) == 0);
+        }
     if (verbose) printf("\n");
     return fails ? 1 : 0;
 }

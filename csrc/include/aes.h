@@ -71,6 +71,17 @@ int aes_ctr_bulk(const aes_context *ctx, const unsigned char nonce_counter[16],
 int aes_ecb_bulk(const aes_context *ctx, int mode, const unsigned char *input,
                  unsigned char *output, size_t length, int nthreads);
 
+/* Monte-Carlo known-answer chains of the reference self-test
+ * (aes-modes/aes.c:1084-1200): 10,000 chained operations from an all-zero
+ * key / block / IV.  aes_monte_carlo writes the final block (CBC-enc: the last
+ * ciphertext); aes_monte_carlo_expected returns the published value (hex). */
+#define AES_MC_ECB_ENC 0
+#define AES_MC_ECB_DEC 1
+#define AES_MC_CBC_ENC 2
+#define AES_MC_CBC_DEC 3
+int aes_monte_carlo(int mode, int bits, unsigned char result[16]);
+const char *aes_monte_carlo_expected(int mode, int bits);
+
 /* 128-bit big-endian counter add: ctr += blocks. */
 void aes_ctr128_add(unsigned char ctr[16], uint64_t blocks);
 

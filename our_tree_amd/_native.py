@@ -123,6 +123,8 @@ def _declare_cpu(lib):
         "AES_CTR_encrypt": (None, [c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int]),
         "AES_CTR_encrypt_at": (None, [c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int, ctypes.c_ulonglong]),
         "otc_bitslice_selftest": (c_int, [c_int]),
+        "aes_monte_carlo": (c_int, [c_int, c_int, c_u8p]),
+        "aes_monte_carlo_expected": (ctypes.c_char_p, [c_int, c_int]),
         "otc_parse_cpulist": (c_int, [ctypes.c_char_p, c_u8p, c_int]),
         "otc_numa_node_of_pci": (c_int, [ctypes.c_char_p, ctypes.c_char_p]),
         "otc_numa_node_cpus": (c_int, [ctypes.c_char_p, c_int, c_u8p, c_int]),

@@ -176,7 +176,8 @@ def test_xor_and_arc4(gpu):
 
 @pytest.mark.parametrize("keylen,length,drop", [(16, 4096, 0), (5, 1000, 3), (256, 37, 768), (16, 1, 0), (16, 2, 0),
                                                 (7, 3, 0), (16, 18, 0), (1, 19, 1), (16, 35, 0), (3, 8197, 0),
-                                                (32, 100, 0), (8, 64, 16), (2, 40, 32), (32, 33, 768)])
+                                                (32, 100, 0), (8, 64, 16), (2, 40, 32), (32, 33, 768),
+                                                (1, 64, 0), (4, 100, 256), (16, 50, 4096)])
 def test_rc4_multi(gpu, keylen, length, drop):
     """every stream vs the oracle: lengths around the 16-byte blocks and the
     two-iteration write delay of the pipelined PRGA; short keys make the

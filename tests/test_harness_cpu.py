@@ -68,3 +68,71 @@ def test_format_roundtrip():
     recs = results.parse(txt)
     assert recs[0]["keygen_us"] == 55 and recs[0]["us"] == [1, 2, 3]
     assert recs[1]["label"] == "HIP CTR" and recs[2]["average_us"] == 15
+
+
+@pytest.mark.parametrize("exe,args,pat", [
+    ("test_o0", ["--sizes", "65536", "--threads", "1,2", "--iters", "2"], r"^RC4, 65536, 2, \n"),
+    ("aes_test_o0", ["--suite", "plain-ecb,aesni-ctr", "--sizes", "65536", "--threads", "1", "--iters", "2"],
+     r"^Plain ECB, 65536, 1, (\d+, ){2}\n"),
+])
+def test_reference_methodology_o0_build(cpu_bins, exe, args, pat):
+    """bin/*_o0: the harnesses built like the reference (gcc -O0 -g -Wall
+    -pedantic -std=gnu99, reference Makefile:13) print the same formats."""
+    out = subprocess.run([os.path.join(cpu_bins, exe)] + args, capture_output=True, text=True, check=True).stdout
+    assert re.search(pat, out, re.M), out
+    assert results.parse(out)
+
+
+def test_o0_build_is_unoptimised():
+    """The -O0 objects really are unoptimised (DWARF producer records -O0)."""
+    import glob
+
+    objs = glob.glob(os.path.join(ROOT, "build", "obj", "o0", "*.o"))
+    assert objs, "make ref-o0 produced no objects"
+    r = subprocess.run(["readelf", "--debug-dump=info", os.path.join(ROOT, "build", "obj", "o0", "aes.o")],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip("readelf unavailable")
+    assert "-O0" in r.stdout
+
+
+def test_gpu_cli_usage_errors():
+    """aes_ecb_d argument errors print the reference's strings
+    (main_ecb_d.cu:11-26) before touching the GPU."""
+    exe = os.path.join(ROOT, "bin", "aes_ecb_d")
+    if not os.path.exists(exe):
+        pytest.skip("bin/aes_ecb_d not built (needs hipcc)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and r.stdout == "USAGE: aes_ecb_d KEY PLAINTEXT [PLAINTEXT...]\n"
+    r = subprocess.run([exe, "0011", "00" * 16], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and r.stdout == "Invalid AES key size.\n"
+    r = subprocess.run([exe, "00" * 16, "00" * 10], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and r.stdout == "Plaintext size must be a multiple of AES block size.\n"
+
+
+@pytest.mark.gpu
+def test_gpu_cli_ecb_d_fips197(gpu):
+    """aes_ecb_d KEYHEX CTHEX decrypts FIPS-197 C.1/C.3 on the GPU and prints
+    upper-case hex (reference main_ecb_d.cu:33-37, printHexArray :62-67)."""
+    exe = os.path.join(ROOT, "bin", "aes_ecb_d")
+    for key, ct in (("000102030405060708090a0b0c0d0e0f", "69c4e0d86a7b0430d8cdb78070b4c55a"),
+                    ("000102030405060708090a0b0c0d0e0f101112131415161718191a1b1c1d1e1f",
+                     "8ea2b7ca516745bfeafc49904b496089")):
+        r = subprocess.run([exe, key, ct * 2], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert r.stdout == "00112233445566778899AABBCCDDEEFF" * 2 + "\n"
+
+
+@pytest.mark.gpu
+def test_gpu_cli_ecb_e_format(gpu):
+    """aes_ecb_e prints the reference's `AES ECB test, <bytes>: <us>, ...
+    Average <us>` lines for its 4 sizes (main_ecb_e.cu:54-73)."""
+    exe = os.path.join(ROOT, "bin", "aes_ecb_e")
+    r = subprocess.run([exe, "--iters", "2"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().splitlines()
+    sizes = [int(m.group(1)) for m in (re.match(r"^AES ECB test, (\d+): (\d+, ){2} Average \d+$", ln)
+                                       for ln in lines) if m]
+    assert sizes == [1048576, 10485760, 104857600, 1048576000], r.stdout
+    recs = results.parse(r.stdout)
+    assert [x["bytes"] for x in recs] == sizes and all(len(x["us"]) == 2 for x in recs)
