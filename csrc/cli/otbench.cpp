@@ -3,7 +3,7 @@
  * gfx950 kernels (the profiling target for rocprofv3).  Prints one JSON line
  * per configuration.
  *
- *   otbench --mode ctr|ecb|ecb-dec|cbc-dec|cbc-enc-seg|cfb-dec|xor|rc4
+ *   otbench --mode ctr|ecb|ecb-dec|cbc-dec|cbc-enc-seg|cfb-enc-seg|cfb-dec-seg|cfb-dec|xor|rc4
  *           [--bits 128] [--bytes 1G] [--iters 20] [--warmup 3]
  *           [--impl auto|ttable|bitslice] [--inplace] [--verify] [--clock]
  *           [--e2e --chunk 256M]            host-resident, pinned pipeline
@@ -72,6 +72,10 @@ static int run_op(void *p)
     if (c.mode == "cbc-dec") return otc_aes_cbc_decrypt(a->in, a->out, c.bytes, a->k, a->iv, nullptr);
     if (c.mode == "cbc-enc-seg")
         return otc_aes_cbc_encrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
+    if (c.mode == "cfb-enc-seg")
+        return otc_aes_cfb128_encrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
+    if (c.mode == "cfb-dec-seg")
+        return otc_aes_cfb128_decrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
     if (c.mode == "cfb-dec") return otc_aes_cfb128_decrypt(a->in, a->out, c.bytes, a->k, a->iv, nullptr);
     if (c.mode == "xor") return otc_xor(a->in, a->out, a->out, c.bytes, nullptr);
     if (c.mode == "rc4") return otc_rc4_multi(a->keys, (int)c.keylen, c.streams, c.len, c.drop, a->in, a->out, nullptr);
@@ -148,7 +152,7 @@ int main(int argc, char **argv)
     }
     if (c.mode == "rc4") c.bytes = c.streams * c.len;
     if (c.mode != "ctr" && c.mode != "xor" && c.mode != "rc4") c.bytes &= ~(size_t)15;
-    if (c.mode == "cbc-enc-seg") c.bytes = (c.bytes / c.seg) * c.seg;
+    if (c.mode == "cbc-enc-seg" || c.mode == "cfb-enc-seg" || c.mode == "cfb-dec-seg") c.bytes = (c.bytes / c.seg) * c.seg;
 
     uint8_t key[32];
     srand(1337);

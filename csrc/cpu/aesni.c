@@ -158,3 +158,36 @@ void AES_CTR_encrypt(const unsigned char *in, unsigned char *out, const unsigned
 {
     AES_CTR_encrypt_at(in, out, ivec, nonce, length, key, nr, 0);
 }
+
+/* Serial chains (one AES-NI pipe, latency bound): the host path for exact
+ * single-stream CBC / CFB128 encryption, which no amount of GPU parallelism
+ * can speed up (every block needs the previous ciphertext). */
+void AES_CBC_encrypt(const unsigned char *in, unsigned char *out, unsigned char ivec[16], unsigned long length,
+                     const unsigned char *key, int nr)
+{
+    const __m128i *rk = (const __m128i *)key;
+    __m128i c = _mm_loadu_si128((const __m128i *)ivec);
+    for (unsigned long i = 0; i < length / 16; ++i) {
+        c = enc1(_mm_xor_si128(c, _mm_loadu_si128((const __m128i *)in + i)), rk, nr);
+        _mm_storeu_si128((__m128i *)out + i, c);
+    }
+    _mm_storeu_si128((__m128i *)ivec, c);
+}
+
+void AES_CFB128_encrypt(const unsigned char *in, unsigned char *out, unsigned char ivec[16], unsigned long length,
+                        const unsigned char *key, int nr)
+{
+    const __m128i *rk = (const __m128i *)key;
+    __m128i c = _mm_loadu_si128((const __m128i *)ivec);
+    unsigned long nb = length / 16;
+    for (unsigned long i = 0; i < nb; ++i) {
+        c = _mm_xor_si128(enc1(c, rk, nr), _mm_loadu_si128((const __m128i *)in + i));
+        _mm_storeu_si128((__m128i *)out + i, c);
+    }
+    if (length % 16) { /* trailing partial block: keystream bytes of E(c) */
+        unsigned char k[16];
+        _mm_storeu_si128((__m128i *)k, enc1(c, rk, nr));
+        for (unsigned long b = 0; b < length % 16; ++b) out[16 * nb + b] = (unsigned char)(in[16 * nb + b] ^ k[b]);
+    }
+    _mm_storeu_si128((__m128i *)ivec, c);
+}

@@ -344,7 +344,7 @@ __device__ __forceinline__ void st16s(uint8_t *p, uint64_t blk, uint4 v)
     __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p + 16 * blk));
 }
 
-enum : int { E_ECB = 0, E_CTR = 1, E_CFB_DEC = 2 };
+enum : int { E_ECB = 0, E_CTR = 1, E_CFB_DEC = 2, E_CFB_DEC_SEG = 3 };
 enum : int { D_ECB = 0, D_CBC = 1, D_CBC_SEG = 2 };
 
 struct EncParams {
@@ -353,8 +353,11 @@ struct EncParams {
     uint64_t nfull;   /* full 16-byte blocks */
     uint32_t tail;    /* bytes of a trailing partial block (CTR) */
     uint32_t wrap64;  /* CTR: 64-bit (RFC 3686) increment */
-    Ctr128 ctr;
+    Ctr128 ctr;       /* CTR: counter; CFB_DEC_SEG: IV of segment 0 (IV_s = ctr + s) */
     uint32_t iv[4];   /* CFB: IV as LE words */
+    uint64_t seg_blocks; /* CFB_DEC_SEG: blocks per segment */
+    uint32_t seg_shift;  /* CFB_DEC_SEG: log2(seg_blocks), or 64 if not a power of two */
+    uint32_t pad2;
 };
 
 struct DecParams {
@@ -398,11 +401,20 @@ __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key
             } else if (MODE == E_ECB) {
                 uint4 v = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
                 s[b][0] = v.x; s[b][1] = v.y; s[b][2] = v.z; s[b][3] = v.w;
-            } else { /* CFB decrypt: cipher input is the previous ciphertext */
+            } else if (MODE == E_CFB_DEC) { /* cipher input is the previous ciphertext */
                 x[b] = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
                 uint4 v = (i == 0) ? make_uint4(P.iv[0], P.iv[1], P.iv[2], P.iv[3])
                                    : (ok ? ld16(P.in, i - 1) : make_uint4(0, 0, 0, 0));
                 s[b][0] = v.x; s[b][1] = v.y; s[b][2] = v.z; s[b][3] = v.w;
+            } else { /* CFB decrypt of independent segments: IV_s at segment starts */
+                x[b] = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
+                const uint64_t sg = P.seg_shift < 64 ? (i >> P.seg_shift) : i / P.seg_blocks;
+                if (i == sg * P.seg_blocks) {
+                    ctr_words(P.ctr, sg, false, s[b][0], s[b][1], s[b][2], s[b][3]);
+                } else {
+                    uint4 v = ok ? ld16(P.in, i - 1) : make_uint4(0, 0, 0, 0);
+                    s[b][0] = v.x; s[b][1] = v.y; s[b][2] = v.z; s[b][3] = v.w;
+                }
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) s[b][j] ^= K.rk[j];
@@ -610,9 +622,13 @@ __global__ __launch_bounds__(THREADS) void k_aes_dec_tt(DecParams P, otc_aes_key
 }
 
 /* ---------------------------------------------------------------------------
- * CBC encryption over independent contiguous segments: one segment per lane
- * slot, B segments per lane for ILP.  IV_s = iv0 + s.  Next plaintext block
- * is prefetched one step ahead.
+ * CBC / CFB128 encryption over independent contiguous segments: one segment
+ * per lane slot, B segments per lane for ILP.  IV_s = iv0 + s.  Next
+ * plaintext block is prefetched one step ahead.  Both modes are serial chains
+ * (reference aes-modes/aes.c:801-812 CBC, :822-862 CFB); per block
+ *   CBC:  c = E(p ^ c)          out = c
+ *   CFB:  c = p ^ E(c)          out = c
+ * so one kernel body serves both (template flag CFB).
  * ------------------------------------------------------------------------- */
 struct CbcSegParams {
     const uint8_t *in;
@@ -622,7 +638,29 @@ struct CbcSegParams {
     Ctr128 iv0;
 };
 
-template <int NR, int B, int THREADS>
+/* chain step on B lanes: s = cipher input ^ rk0 from the chain value c and
+ * the plaintext p; after the rounds, chain_out gives the new c (= output) */
+template <bool CFB>
+__device__ __forceinline__ void chain_in(const uint4 &p, const uint32_t (&c)[4], const otc_aes_key &K, uint32_t (&s)[4])
+{
+    if (CFB) {
+        s[0] = c[0] ^ K.rk[0]; s[1] = c[1] ^ K.rk[1]; s[2] = c[2] ^ K.rk[2]; s[3] = c[3] ^ K.rk[3];
+    } else {
+        s[0] = p.x ^ c[0] ^ K.rk[0]; s[1] = p.y ^ c[1] ^ K.rk[1]; s[2] = p.z ^ c[2] ^ K.rk[2];
+        s[3] = p.w ^ c[3] ^ K.rk[3];
+    }
+}
+template <bool CFB>
+__device__ __forceinline__ void chain_out(const uint4 &p, const uint32_t (&s)[4], uint32_t (&c)[4])
+{
+    if (CFB) {
+        c[0] = s[0] ^ p.x; c[1] = s[1] ^ p.y; c[2] = s[2] ^ p.z; c[3] = s[3] ^ p.w;
+    } else {
+        c[0] = s[0]; c[1] = s[1]; c[2] = s[2]; c[3] = s[3];
+    }
+}
+
+template <int NR, int B, int THREADS, bool CFB = false>
 __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg(CbcSegParams P, otc_aes_key K)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
@@ -652,22 +690,19 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg(CbcSegParams P, otc
         }
         for (uint64_t j = 0; j < P.seg_blocks; ++j) {
             uint32_t s[B][4];
+            uint4 p[B];
 #pragma unroll
             for (int b = 0; b < B; ++b) {
-                const uint4 p = nxt[b];
-                s[b][0] = p.x ^ c[b][0] ^ K.rk[0];
-                s[b][1] = p.y ^ c[b][1] ^ K.rk[1];
-                s[b][2] = p.z ^ c[b][2] ^ K.rk[2];
-                s[b][3] = p.w ^ c[b][3] ^ K.rk[3];
+                p[b] = nxt[b];
+                chain_in<CFB>(p[b], c[b], K, s[b]);
                 nxt[b] = (live[b] && j + 1 < P.seg_blocks) ? ld16(P.in, seg[b] * P.seg_blocks + j + 1)
                                                            : make_uint4(0, 0, 0, 0);
             }
             enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
 #pragma unroll
             for (int b = 0; b < B; ++b) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) c[b][q] = s[b][q];
-                if (live[b]) st16(P.out, seg[b] * P.seg_blocks + j, make_uint4(s[b][0], s[b][1], s[b][2], s[b][3]));
+                chain_out<CFB>(p[b], s[b], c[b]);
+                if (live[b]) st16(P.out, seg[b] * P.seg_blocks + j, make_uint4(c[b][0], c[b][1], c[b][2], c[b][3]));
             }
         }
     }
@@ -681,7 +716,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg(CbcSegParams P, otc
  * each 16-byte block re-fetches a whole line.  Group g+1 is prefetched while
  * group g is encrypted; ciphertext overwrites the plaintext registers and is
  * stored as a burst at the end of the group. */
-template <int NR, int B, int THREADS, int G>
+template <int NR, int B, int THREADS, int G, bool CFB = false>
 __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg_g(CbcSegParams P, otc_aes_key K)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
@@ -725,18 +760,12 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg_g(CbcSegParams P, o
             for (int t = 0; t < G; ++t) {
                 uint32_t s[B][4];
 #pragma unroll
-                for (int b = 0; b < B; ++b) {
-                    s[b][0] = cur[b][t].x ^ c[b][0] ^ K.rk[0];
-                    s[b][1] = cur[b][t].y ^ c[b][1] ^ K.rk[1];
-                    s[b][2] = cur[b][t].z ^ c[b][2] ^ K.rk[2];
-                    s[b][3] = cur[b][t].w ^ c[b][3] ^ K.rk[3];
-                }
+                for (int b = 0; b < B; ++b) chain_in<CFB>(cur[b][t], c[b], K, s[b]);
                 enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
 #pragma unroll
                 for (int b = 0; b < B; ++b) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) c[b][q] = s[b][q];
-                    cur[b][t] = make_uint4(s[b][0], s[b][1], s[b][2], s[b][3]);
+                    chain_out<CFB>(cur[b][t], s[b], c[b]);
+                    cur[b][t] = make_uint4(c[b][0], c[b][1], c[b][2], c[b][3]);
                 }
             }
 #pragma unroll
@@ -751,20 +780,17 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg_g(CbcSegParams P, o
         /* remaining sb % G blocks, one at a time */
         for (uint64_t j = ng * G; j < sb; ++j) {
             uint32_t s[B][4];
+            uint4 p[B];
 #pragma unroll
             for (int b = 0; b < B; ++b) {
-                const uint4 p = live[b] ? ld16(P.in, first[b] + j) : make_uint4(0, 0, 0, 0);
-                s[b][0] = p.x ^ c[b][0] ^ K.rk[0];
-                s[b][1] = p.y ^ c[b][1] ^ K.rk[1];
-                s[b][2] = p.z ^ c[b][2] ^ K.rk[2];
-                s[b][3] = p.w ^ c[b][3] ^ K.rk[3];
+                p[b] = live[b] ? ld16(P.in, first[b] + j) : make_uint4(0, 0, 0, 0);
+                chain_in<CFB>(p[b], c[b], K, s[b]);
             }
             enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
 #pragma unroll
             for (int b = 0; b < B; ++b) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) c[b][q] = s[b][q];
-                if (live[b]) st16(P.out, first[b] + j, make_uint4(s[b][0], s[b][1], s[b][2], s[b][3]));
+                chain_out<CFB>(p[b], s[b], c[b]);
+                if (live[b]) st16(P.out, first[b] + j, make_uint4(c[b][0], c[b][1], c[b][2], c[b][3]));
             }
         }
     }
@@ -1070,20 +1096,21 @@ hipError_t launch_dec(const DecParams &P, const otc_aes_key &K, hipStream_t st)
     }
 }
 
-template <int NR>
+template <int NR, bool CFB>
 hipError_t launch_seg_nr(const CbcSegParams &P, const otc_aes_key &K, hipStream_t st)
 {
     int grid = grid_for(P.nseg, (uint64_t)SEG_THREADS * SEG_B, 1);
     /* OTC_CBC_GROUP: blocks per load/store burst (1 = the per-block kernel) */
     static const int grp = getenv("OTC_CBC_GROUP") ? atoi(getenv("OTC_CBC_GROUP")) : 8;
     if (grp == 4 && P.seg_blocks >= 4)
-        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, SEG_B, SEG_THREADS, 4>), dim3(grid), dim3(SEG_THREADS), 0, st, P,
-                           K);
+        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, SEG_B, SEG_THREADS, 4, CFB>), dim3(grid), dim3(SEG_THREADS), 0, st,
+                           P, K);
     else if (grp == 8 && P.seg_blocks >= 8) /* B = 1: two 8-block buffers per segment fit without spills */
-        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, 1, SEG_THREADS, 8>),
+        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, 1, SEG_THREADS, 8, CFB>),
                            dim3(grid_for(P.nseg, (uint64_t)SEG_THREADS, 1)), dim3(SEG_THREADS), 0, st, P, K);
     else
-        hipLaunchKernelGGL((k_aes_cbc_enc_seg<NR, SEG_B, SEG_THREADS>), dim3(grid), dim3(SEG_THREADS), 0, st, P, K);
+        hipLaunchKernelGGL((k_aes_cbc_enc_seg<NR, SEG_B, SEG_THREADS, CFB>), dim3(grid), dim3(SEG_THREADS), 0, st, P,
+                           K);
     return hipGetLastError();
 }
 
@@ -1251,8 +1278,9 @@ hipError_t tt_cbc_decrypt_seg(const void *in, void *out, uint64_t seg_blocks, ui
     return hipGetLastError();
 }
 
-hipError_t tt_cbc_encrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,
-                              const otc_aes_key &K, Ctr128 iv0, hipStream_t st)
+template <bool CFB>
+static hipError_t chain_encrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,
+                                    const otc_aes_key &K, Ctr128 iv0, hipStream_t st)
 {
     CbcSegParams P{};
     P.in = (const uint8_t *)in;
@@ -1261,11 +1289,41 @@ hipError_t tt_cbc_encrypt_seg(const void *in, void *out, uint64_t seg_blocks, ui
     P.nseg = nseg;
     P.iv0 = iv0;
     switch (K.nr) {
-    case 10: return launch_seg_nr<10>(P, K, st);
-    case 12: return launch_seg_nr<12>(P, K, st);
-    case 14: return launch_seg_nr<14>(P, K, st);
+    case 10: return launch_seg_nr<10, CFB>(P, K, st);
+    case 12: return launch_seg_nr<12, CFB>(P, K, st);
+    case 14: return launch_seg_nr<14, CFB>(P, K, st);
     default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t tt_cbc_encrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,
+                              const otc_aes_key &K, Ctr128 iv0, hipStream_t st)
+{
+    return chain_encrypt_seg<false>(in, out, seg_blocks, nseg, K, iv0, st);
+}
+
+hipError_t tt_cfb_encrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,
+                              const otc_aes_key &K, Ctr128 iv0, hipStream_t st)
+{
+    return chain_encrypt_seg<true>(in, out, seg_blocks, nseg, K, iv0, st);
+}
+
+hipError_t tt_cfb_decrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,
+                              const otc_aes_key &K, Ctr128 iv0, hipStream_t st)
+{
+    EncParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = seg_blocks * nseg;
+    P.ctr = iv0;
+    P.seg_blocks = seg_blocks;
+    P.seg_shift = 64;
+    if ((seg_blocks & (seg_blocks - 1)) == 0) {
+        uint32_t sh = 0;
+        while ((1ull << sh) < seg_blocks) ++sh;
+        P.seg_shift = sh;
+    }
+    return launch_enc<E_CFB_DEC_SEG>(P, K, st);
 }
 
 } // namespace otc_impl

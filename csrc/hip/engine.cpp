@@ -46,6 +46,8 @@ hipError_t tt_cfb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, c
 hipError_t tt_cbc_decrypt(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t tt_cbc_decrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t tt_cbc_encrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
+hipError_t tt_cfb_encrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
+hipError_t tt_cfb_decrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
 hipError_t bs_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
 hipError_t tt_ctr_batch(const otc_ctr_msg *, const otc_aes_key *, const uint32_t *, const uint64_t *, uint64_t, int, int,
@@ -422,6 +424,44 @@ extern "C" int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t se
     hipError_t e = otc_impl::tt_cbc_decrypt_seg(in, out, sb, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "cbc_decrypt_segments launch");
     return OTC_OK;
+}
+
+/* CFB128 over independent segments (IV_s = iv0 + s, like the CBC sector
+ * mode): encryption is one serial chain per segment (one lane each, the
+ * sector kernel with the CFB chain step); decryption is fully parallel with
+ * IV_s at every segment start.  Both use the ENCRYPTION key schedule. */
+static int cfb_seg_common(const void *in, void *out, size_t seg_bytes, size_t nseg, const otc_aes_key *k,
+                          const uint8_t iv0[16], void *stream, bool decrypt, const char *what)
+{
+    int r = check_key(k, OTC_DIR_ENCRYPT);
+    if (r) return r;
+    if (seg_bytes % 16) return set_err(OTC_ERR_ARG, "segment length must be a multiple of 16");
+    if (!iv0) return set_err(OTC_ERR_ARG, "null iv");
+    if (nseg && seg_bytes > SIZE_MAX / nseg) return set_err(OTC_ERR_ARG, "size overflow");
+    /* decrypt reads block i-1 of the input while another lane writes block
+     * i-1 of the output: in place only for encryption (lane-private chains) */
+    if ((r = check_bufs(in, out, seg_bytes * nseg, !decrypt, what))) return r;
+    if (nseg == 0 || seg_bytes == 0) return OTC_OK;
+    hipError_t e = decrypt ? otc_impl::tt_cfb_decrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
+                                                          (hipStream_t)stream)
+                           : otc_impl::tt_cfb_encrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
+                                                          (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, what);
+    return OTC_OK;
+}
+
+extern "C" int otc_aes_cfb128_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                               const otc_aes_key *k, const uint8_t iv0[16], void *stream)
+{
+    Range rg("otc_aes_cfb128_encrypt_segments");
+    return cfb_seg_common(in, out, seg_bytes, nseg, k, iv0, stream, false, "cfb128_encrypt_segments");
+}
+
+extern "C" int otc_aes_cfb128_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                               const otc_aes_key *k, const uint8_t iv0[16], void *stream)
+{
+    Range rg("otc_aes_cfb128_decrypt_segments");
+    return cfb_seg_common(in, out, seg_bytes, nseg, k, iv0, stream, true, "cfb128_decrypt_segments");
 }
 
 extern "C" int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,

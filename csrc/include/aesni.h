@@ -42,6 +42,14 @@ void AES_CTR_encrypt_at(const unsigned char *in, unsigned char *out, const unsig
                         const unsigned char *key, int number_of_rounds,
                         unsigned long long block_offset);
 
+/* Serial CBC / CFB128 encryption chains (whole stream, one core): ivec is
+ * updated to the last full ciphertext block, as a resumable IV.  CBC needs a
+ * multiple of 16 bytes; CFB128 encrypts a trailing partial block too. */
+void AES_CBC_encrypt(const unsigned char *in, unsigned char *out, unsigned char ivec[16], unsigned long length,
+                     const unsigned char *key, int number_of_rounds);
+void AES_CFB128_encrypt(const unsigned char *in, unsigned char *out, unsigned char ivec[16], unsigned long length,
+                        const unsigned char *key, int number_of_rounds);
+
 #ifdef __cplusplus
 }
 #endif

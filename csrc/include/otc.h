@@ -101,6 +101,15 @@ int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t seg_bytes, si
                                  const otc_aes_key *k, const uint8_t iv0[16], void *stream);
 
 /* CFB128 decryption (parallel): P_i = C_i ^ E(C_{i-1}); nbytes % 16 == 0. */
+/* CFB128 over nseg independent segments of seg_bytes (multiple of 16) with
+ * IV_s = iv0 + s (128-bit BE add) -- the parallel form of the serial CFB
+ * chain, like otc_aes_cbc_encrypt_segments.  Encryption keys for both
+ * directions.  Encrypt may run in place; decrypt may not. */
+int otc_aes_cfb128_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                    const otc_aes_key *k, const uint8_t iv0[16], void *stream);
+int otc_aes_cfb128_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                    const otc_aes_key *k, const uint8_t iv0[16], void *stream);
+
 int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
                            const uint8_t iv[16], void *stream);
 

@@ -123,6 +123,8 @@ def _declare_cpu(lib):
         "AES_CTR_encrypt": (None, [c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int]),
         "AES_CTR_encrypt_at": (None, [c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int, ctypes.c_ulonglong]),
         "otc_bitslice_selftest": (c_int, [c_int]),
+        "AES_CBC_encrypt": (None, [c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int]),
+        "AES_CFB128_encrypt": (None, [c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int]),
         "aes_monte_carlo": (c_int, [c_int, c_int, c_u8p]),
         "aes_monte_carlo_expected": (ctypes.c_char_p, [c_int, c_int]),
         "otc_parse_cpulist": (c_int, [ctypes.c_char_p, c_u8p, c_int]),
@@ -154,6 +156,8 @@ def _declare_gpu(lib):
         "otc_aes_cbc_encrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cbc_decrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cfb128_decrypt": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_vp]),
+        "otc_aes_cfb128_encrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
+        "otc_aes_cfb128_decrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
         "otc_aes_ctr_batch": (c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_int, c_int, c_vp]),
         "otc_xor": (c_int, [c_vp, c_vp, c_vp, c_sz, c_vp]),
         "otc_rc4_multi": (c_int, [c_vp, c_int, c_sz, c_sz, c_sz, c_vp, c_vp, c_vp]),

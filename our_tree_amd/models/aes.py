@@ -71,15 +71,31 @@ class AES:
             return ops.ctr(data, self._key, counter, out=out, block_offset=block_offset, impl=self.impl)
         return cpu_ref.ctr(self._key, counter, data, block_offset)
 
-    def cbc_encrypt(self, data, iv: bytes, segment_bytes: int | None = None, out=None):
+    # exact single-stream CBC / CFB encryption is one serial chain: on a GPU it
+    # would run on ONE lane (~67M dependent block encryptions per GiB), far
+    # slower than one AES-NI core, so GPU tensors take the host chain unless
+    # the caller opts in with device_serial=True (small buffers, no host trip)
+    def _serial_on_host(self, mode: str, data: torch.Tensor, iv: bytes, out):
+        res = cpu_ref.serial_encrypt(mode, self._key, iv, data.reshape(-1).view(torch.uint8).cpu().numpy().tobytes())
+        t = torch.frombuffer(bytearray(res), dtype=torch.uint8).to(data.device)
+        if out is None:
+            return t.view(data.dtype).view(data.shape)
+        out.reshape(-1).view(torch.uint8).copy_(t)
+        return out
+
+    def cbc_encrypt(self, data, iv: bytes, segment_bytes: int | None = None, out=None, device_serial: bool = False):
         """CBC encryption.  ``segment_bytes``: independent segments with
-        IV_s = iv + s (parallel); None = one exact serial stream."""
+        IV_s = iv + s (parallel, one lane per segment); None = one exact
+        serial stream (host AES-NI chain for GPU tensors, see above)."""
         if isinstance(data, torch.Tensor):
-            seg = segment_bytes or data.numel() * data.element_size()
-            return ops.cbc_encrypt_segments(data, self._key, iv, seg, out=out)
+            if segment_bytes:
+                return ops.cbc_encrypt_segments(data, self._key, iv, segment_bytes, out=out)
+            if device_serial:
+                return ops.cbc_encrypt_segments(data, self._key, iv, data.numel() * data.element_size(), out=out)
+            return self._serial_on_host("cbc", data, iv, out)
         if segment_bytes:
             return cpu_ref.cbc_segments(self._key, iv, data, segment_bytes)
-        return cpu_ref.cbc(self._key, iv, data)
+        return cpu_ref.serial_encrypt("cbc", self._key, iv, data)
 
     def cbc_decrypt(self, data, iv: bytes, segment_bytes: int | None = None, out=None):
         if isinstance(data, torch.Tensor):
@@ -90,11 +106,27 @@ class AES:
             return cpu_ref.cbc_segments(self._key, iv, data, segment_bytes, decrypt=True)
         return cpu_ref.cbc(self._key, iv, data, decrypt=True)
 
-    def cfb128_decrypt(self, data, iv: bytes, out=None):
+    def cfb128_decrypt(self, data, iv: bytes, segment_bytes: int | None = None, out=None):
         if isinstance(data, torch.Tensor):
+            if segment_bytes:
+                return ops.cfb128_decrypt_segments(data, self._key, iv, segment_bytes, out=out)
             return ops.cfb128_decrypt(data, self._key, iv, out=out)
+        if segment_bytes:
+            return cpu_ref.cfb128_segments(self._key, iv, data, segment_bytes, decrypt=True)
         return cpu_ref.cfb128(self._key, iv, data, decrypt=True)
 
-    def cfb128_encrypt(self, data: bytes, iv: bytes):
-        """CFB encryption is a serial chain -> CPU oracle only."""
-        return cpu_ref.cfb128(self._key, iv, data)
+    def cfb128_encrypt(self, data, iv: bytes, segment_bytes: int | None = None, out=None,
+                       device_serial: bool = False):
+        """CFB128 encryption (reference aes-modes/aes.c:822-862): a serial
+        chain.  ``segment_bytes``: independent segments with IV_s = iv + s on
+        the GPU sector kernel; None = exact single stream (host AES-NI chain
+        for GPU tensors unless ``device_serial``)."""
+        if isinstance(data, torch.Tensor):
+            if segment_bytes:
+                return ops.cfb128_encrypt_segments(data, self._key, iv, segment_bytes, out=out)
+            if device_serial:
+                return ops.cfb128_encrypt_segments(data, self._key, iv, data.numel() * data.element_size(), out=out)
+            return self._serial_on_host("cfb128", data, iv, out)
+        if segment_bytes:
+            return cpu_ref.cfb128_segments(self._key, iv, data, segment_bytes)
+        return cpu_ref.serial_encrypt("cfb128", self._key, iv, data)

@@ -96,6 +96,32 @@ def cbc_segments(key: bytes, iv0: bytes, data: bytes, segment_bytes: int, decryp
     return bytes(out)
 
 
+def cfb128_segments(key: bytes, iv0: bytes, data: bytes, segment_bytes: int, decrypt: bool = False) -> bytes:
+    """Per-segment CFB128 with IV_s = iv0 + s (the device segment semantics)."""
+    out = bytearray()
+    for s, off in enumerate(range(0, len(data), segment_bytes)):
+        out += cfb128(key, ctr128_add(iv0, s), data[off: off + segment_bytes], decrypt)
+    return bytes(out)
+
+
+def serial_encrypt(mode: str, key: bytes, iv: bytes, data: bytes) -> bytes:
+    """Exact single-stream CBC / CFB128 encryption on one core with AES-NI
+    (the C oracle where AES-NI is absent).  This is the host path for the
+    serial chain: a GPU runs it on one lane, far slower than one x86 core."""
+    if mode not in ("cbc", "cfb128"):
+        raise ValueError("mode must be 'cbc' or 'cfb128'")
+    if mode == "cbc" and len(data) % 16:
+        raise ValueError("CBC needs a multiple of 16 bytes")
+    if not aesni_supported():
+        return cbc(key, iv, data) if mode == "cbc" else cfb128(key, iv, data)
+    sched, nr = aesni_schedule(key)
+    ivb = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(iv))
+    out = _buf(len(data))
+    fn = _native.cpu_lib().AES_CBC_encrypt if mode == "cbc" else _native.cpu_lib().AES_CFB128_encrypt
+    fn(_native.as_u8p(bytes(data)), out, ivb, len(data), _native.as_u8p(sched), nr)
+    return bytes(out)[: len(data)]
+
+
 def arc4_keystream(key: bytes, n: int, drop: int = 0) -> bytes:
     lib = _native.cpu_lib()
     ctx = _native.Arc4Context()

@@ -407,7 +407,10 @@ def cbc_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None) -> torch.Tenso
 
 def cbc_encrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None) -> torch.Tensor:
     """CBC encryption of independent contiguous segments; segment s uses
-    IV = iv0 + s (128-bit BE).  One segment == exact serial CBC."""
+    IV = iv0 + s (128-bit BE), one serial chain per GPU lane.  A single
+    segment is exact serial CBC on ONE lane -- use ``models.AES.cbc_encrypt``
+    (routes exact single-stream encryption to the host AES-NI chain) unless
+    the buffer is small."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     n = _nbytes(x)
@@ -444,3 +447,28 @@ def cfb128_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None) -> torch.Te
             _stream(x)), inplace_ok=False)
     _native.check(rc, "otc_aes_cfb128_decrypt")
     return out
+
+
+def _seg_call(fn_name: str, x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out, inplace_ok: bool):
+    _check_dev(x, "x")
+    out = _out_like(x, out)
+    n = _nbytes(x)
+    if segment_bytes <= 0 or segment_bytes % 16 or n % segment_bytes:
+        raise ValueError("segment_bytes must be a positive multiple of 16 dividing the byte size")
+    k = expand_key(key)
+    with torch.cuda.device(x.device):
+        rc = _run(x, out, lambda ip, op: getattr(_lib(), fn_name)(ip, op, segment_bytes, n // segment_bytes,
+                  ctypes.byref(k), _b16(iv0, "iv0"), _stream(x)), inplace_ok=inplace_ok)
+    _native.check(rc, fn_name)
+    return out
+
+
+def cfb128_encrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None) -> torch.Tensor:
+    """CFB128 encryption of independent segments (IV_s = iv0 + s), one
+    serial chain per lane (the CBC sector kernel with the CFB chain step)."""
+    return _seg_call("otc_aes_cfb128_encrypt_segments", x, key, iv0, segment_bytes, out, True)
+
+
+def cfb128_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None) -> torch.Tensor:
+    """Inverse of ``cfb128_encrypt_segments``: fully parallel."""
+    return _seg_call("otc_aes_cfb128_decrypt_segments", x, key, iv0, segment_bytes, out, False)

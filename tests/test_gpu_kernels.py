@@ -132,6 +132,46 @@ def test_cbc_single_segment_is_exact_cbc(gpu):
     assert host(y) == cpu_ref.cbc(key, iv, pt)
 
 
+@pytest.mark.parametrize("bits", [128, 192, 256])
+@pytest.mark.parametrize("seg", [16, 48, 512, 4096, 16 * 37])
+def test_cfb128_segments_roundtrip(gpu, bits, seg):
+    """CFB128 sector kernel (one serial chain per lane) vs the oracle per
+    segment, every key size and every sector-kernel path (seg_blocks < 4, the
+    4/8-block burst loops and their remainders), IV carry across segments;
+    the parallel segment decryption inverts it (power-of-two and general
+    segment lengths)."""
+    key, iv0 = os.urandom(bits // 8), (2**128 - 5).to_bytes(16, "big")
+    nseg = 700
+    pt = os.urandom(seg * nseg)
+    x = torch.frombuffer(bytearray(pt), dtype=torch.uint8).to(gpu)
+    y = ops.cfb128_encrypt_segments(x, key, iv0, seg)
+    torch.cuda.synchronize()
+    assert host(y) == cpu_ref.cfb128_segments(key, iv0, pt, seg)
+    z = ops.cfb128_decrypt_segments(y, key, iv0, seg)
+    torch.cuda.synchronize()
+    assert host(z) == pt
+    ops.cfb128_encrypt_segments(x, key, iv0, seg, out=x)  # in place (lane-private chains)
+    assert torch.equal(x, y)
+
+
+def test_serial_chains_route_to_host(gpu):
+    """Exact single-stream CBC / CFB128 encryption of a GPU tensor runs the
+    host AES-NI chain (not one GPU lane) and equals the oracle; device_serial
+    opts in to the one-lane kernel."""
+    from our_tree_amd.models import AES
+
+    key, iv = os.urandom(16), os.urandom(16)
+    pt = os.urandom(16 * 4099)
+    x = torch.frombuffer(bytearray(pt), dtype=torch.uint8).to(gpu)
+    aes = AES(key)
+    for mode, ref in (("cbc", cpu_ref.cbc(key, iv, pt)), ("cfb128", cpu_ref.cfb128(key, iv, pt))):
+        enc = aes.cbc_encrypt if mode == "cbc" else aes.cfb128_encrypt
+        y = enc(x, iv)
+        assert y.device == x.device and host(y) == ref
+        assert host(enc(x, iv, device_serial=True)) == ref
+    assert host(aes.cfb128_decrypt(aes.cfb128_encrypt(x, iv, segment_bytes=16 * 4099), iv, segment_bytes=16 * 4099)) == pt
+
+
 def test_cfb128_decrypt(gpu):
     key, iv = os.urandom(24), os.urandom(16)
     pt = os.urandom(16 * 5001)
