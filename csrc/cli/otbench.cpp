@@ -3,7 +3,7 @@
  * gfx950 kernels (the profiling target for rocprofv3).  Prints one JSON line
  * per configuration.
  *
- *   otbench --mode ctr|ecb|ecb-dec|cbc-dec|cbc-enc-seg|cfb-enc-seg|cfb-dec-seg|cfb-dec|xor|rc4
+ *   otbench --mode ctr|ecb|ecb-dec|cbc-dec|cbc-enc-seg|cfb-enc-seg|cfb-dec-seg|cfb-dec|ctr-stream|xor|rc4
  *           [--bits 128] [--bytes 1G] [--iters 20] [--warmup 3]
  *           [--impl auto|ttable|bitslice] [--inplace] [--verify] [--clock]
  *           [--e2e --chunk 256M]            host-resident, pinned pipeline
@@ -72,6 +72,12 @@ static int run_op(void *p)
     if (c.mode == "cbc-dec") return otc_aes_cbc_decrypt(a->in, a->out, c.bytes, a->k, a->iv, nullptr);
     if (c.mode == "cbc-enc-seg")
         return otc_aes_cbc_encrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
+    if (c.mode == "ctr-stream") { /* resumed mid-block: 1-byte head, then a body misaligned by 1 */
+        otc_aes_ctr_ctx ctx;
+        otc_aes_ctr_ctx_init(&ctx, a->iv);
+        ctx.nc_off = 15;
+        return otc_aes_ctr_stream(&ctx, a->k, c.bytes, a->in, a->out, c.impl, nullptr);
+    }
     if (c.mode == "cfb-enc-seg")
         return otc_aes_cfb128_encrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
     if (c.mode == "cfb-dec-seg")

@@ -180,6 +180,16 @@ int aes_export_rk32(const aes_context *ctx, uint32_t *out)
     return n;
 }
 
+int aes_import_rk32(aes_context *ctx, const uint32_t *rk, int nr)
+{
+    if (nr != 10 && nr != 12 && nr != 14) return POLARSSL_ERR_AES_INVALID_KEY_LENGTH;
+    ensure_tables();
+    ctx->nr = nr;
+    ctx->rk = ctx->buf;
+    for (int i = 0; i < 4 * (nr + 1); ++i) ctx->buf[i] = rk[i];
+    return 0;
+}
+
 /* ---------------------------------------------------------------------------
  * Block functions
  * ------------------------------------------------------------------------- */

@@ -817,6 +817,96 @@ __global__ __launch_bounds__(256) void k_cbc_seg_fixup(const uint8_t *in, uint8_
 }
 
 /* ---------------------------------------------------------------------------
+ * CTR over a body whose data pointer is NOT 16-byte aligned (the resumable
+ * stream API after a partial block: nc_off != 0 leaves the next call's data at
+ * body = in + head).  Keystream block b still covers data bytes
+ * [16b, 16b + 16); the memory is processed in ALIGNED 16-byte chunks J, and
+ * with a = body & 15 chunk J holds data bytes [16J - a, 16J - a + 16), i.e.
+ * the last a bytes of keystream block J-1 and the first 16 - a of block J.
+ * Lane l of a wave encrypts block J0 + l - 1, takes block J0 + l - 2 from lane
+ * l - 1 (one cross-lane shuffle per word) and funnel-shifts the two
+ * (v_alignbyte) into the chunk's keystream: 63 chunks per wave, dwordx4 loads
+ * and stores, byte accesses only for the two edge chunks.  In and out must
+ * share the misalignment (in place always does).
+ * ------------------------------------------------------------------------- */
+struct CtrShiftParams {
+    const uint8_t *in; /* aligned base: body - a */
+    uint8_t *out;
+    uint64_t len;      /* body bytes */
+    uint32_t a;        /* misalignment 1..15 */
+    uint32_t pad;
+    Ctr128 ctr;        /* counter of the body's keystream block 0 */
+};
+
+template <int NR, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_aes_ctr_shift(CtrShiftParams P, otc_aes_key K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
+    fill_tbl4<THREADS>(tbl, g_tab.te0);
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    uint32_t lk[4];
+    tbl4_lane_consts(lane, lk);
+    constexpr uint64_t WPB = THREADS / 64;
+    const uint64_t nchunks = (P.a + P.len + 15) / 16;
+    const uint32_t d = 16u - P.a, dq = d >> 2, db = d & 3u;
+
+    for (uint64_t w = (uint64_t)blockIdx.x * WPB + wave; w * 63u < nchunks; w += (uint64_t)gridDim.x * WPB) {
+        const uint64_t J0 = w * 63u;
+        /* block J0 - 1 for lane 0 (wraps to the counter's predecessor for the
+         * very first wave: computed, never used) */
+        uint32_t s[1][4];
+        ctr_words(P.ctr, J0 + lane - 1u, false, s[0][0], s[0][1], s[0][2], s[0][3]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[0][j] ^= K.rk[j];
+        enc_rounds4_from<1, NR, 1>(tbl, lk, K, s);
+        uint32_t cat[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            cat[j] = (uint32_t)__shfl_up((int)s[0][j], 1);
+            cat[4 + j] = s[0][j];
+        }
+        const uint64_t J = J0 + lane - 1u;
+        if (lane == 0 || J >= nchunks) continue;
+        /* chunk byte t = concatenated keystream byte d + t */
+        uint32_t ks[4];
+#define OTC_KS_SHIFT(Q)                                                                  \
+    for (int k = 0; k < 4; ++k) ks[k] = __builtin_amdgcn_alignbyte(cat[(Q) + k + 1], cat[(Q) + k], db);
+        switch (dq) {
+        case 0: OTC_KS_SHIFT(0) break;
+        case 1: OTC_KS_SHIFT(1) break;
+        case 2: OTC_KS_SHIFT(2) break;
+        default: OTC_KS_SHIFT(3) break;
+        }
+#undef OTC_KS_SHIFT
+        const int64_t lo = (int64_t)(16u * J) - (int64_t)P.a; /* data index of the chunk's byte 0 */
+        if (J >= 1 && lo + 16 <= (int64_t)P.len) {
+            const uint4 x = ld16(P.in, J);
+            st16(P.out, J, make_uint4(x.x ^ ks[0], x.y ^ ks[1], x.z ^ ks[2], x.w ^ ks[3]));
+        } else { /* edge chunk: only the bytes inside the body */
+            for (int t = 0; t < 16; ++t) {
+                const int64_t i = lo + t;
+                if (i >= 0 && i < (int64_t)P.len)
+                    P.out[16u * J + t] = P.in[16u * J + t] ^ (uint8_t)(ks[t >> 2] >> (8 * (t & 3)));
+            }
+        }
+    }
+}
+
+/* Tiny XOR with up to 16 keystream bytes passed by value (head of a resumed
+ * CTR stream: the bytes of the context's stream_block) */
+struct SmallXor {
+    uint8_t ks[16];
+};
+__global__ __launch_bounds__(64) void k_xor_small(const uint8_t *in, uint8_t *out, uint32_t n, SmallXor k)
+{
+    const uint32_t t = threadIdx.x;
+    if (t < n) out[t] = in[t] ^ k.ks[t];
+}
+
+/* ---------------------------------------------------------------------------
  * Batched CTR (otc_aes_ctr_batch): many independent messages, each with its
  * own buffers, key and counter, in ONE launch.  Work unit: a wave tile of
  * 64 x B blocks of one message; tile t belongs to message tile_msg[t] at local
@@ -1300,6 +1390,40 @@ hipError_t tt_cbc_encrypt_seg(const void *in, void *out, uint64_t seg_blocks, ui
                               const otc_aes_key &K, Ctr128 iv0, hipStream_t st)
 {
     return chain_encrypt_seg<false>(in, out, seg_blocks, nseg, K, iv0, st);
+}
+
+hipError_t tt_ctr_shift(const void *body_in, void *body_out, size_t len, const otc_aes_key &K, Ctr128 c,
+                        hipStream_t st)
+{
+    const uint32_t a = (uint32_t)((uintptr_t)body_in & 15u);
+    if (a == 0 || a != ((uintptr_t)body_out & 15u)) return hipErrorInvalidValue;
+    if (len == 0) return hipSuccess;
+    CtrShiftParams P{};
+    P.in = (const uint8_t *)body_in - a;
+    P.out = (uint8_t *)body_out - a;
+    P.len = len;
+    P.a = a;
+    P.ctr = c;
+    constexpr int T = 1024;
+    const uint64_t waves = ((a + len + 15) / 16 + 62) / 63;
+    const int grid = grid_for(waves, T / 64, 1);
+    switch (K.nr) {
+    case 10: hipLaunchKernelGGL((k_aes_ctr_shift<10, T>), dim3(grid), dim3(T), 0, st, P, K); break;
+    case 12: hipLaunchKernelGGL((k_aes_ctr_shift<12, T>), dim3(grid), dim3(T), 0, st, P, K); break;
+    case 14: hipLaunchKernelGGL((k_aes_ctr_shift<14, T>), dim3(grid), dim3(T), 0, st, P, K); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t xor_small(const void *in, void *out, uint32_t n, const uint8_t *ks, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    if (n > 16) return hipErrorInvalidValue;
+    SmallXor k{};
+    for (uint32_t i = 0; i < n; ++i) k.ks[i] = ks[i];
+    hipLaunchKernelGGL(k_xor_small, dim3(1), dim3(64), 0, st, (const uint8_t *)in, (uint8_t *)out, n, k);
+    return hipGetLastError();
 }
 
 hipError_t tt_cfb_encrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,

@@ -49,6 +49,8 @@ hipError_t tt_cbc_encrypt_seg(const void *, void *, uint64_t, uint64_t, const ot
 hipError_t tt_cfb_encrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t tt_cfb_decrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
+hipError_t tt_ctr_shift(const void *, void *, size_t, const otc_aes_key &, Ctr128, hipStream_t);
+hipError_t xor_small(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
 hipError_t bs_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
 hipError_t tt_ctr_batch(const otc_ctr_msg *, const otc_aes_key *, const uint32_t *, const uint64_t *, uint64_t, int, int,
                         hipStream_t);
@@ -324,6 +326,75 @@ extern "C" int otc_aes_ctr(const void *in, void *out, size_t nbytes, const otc_a
     Range rg("otc_aes_ctr");
     if (!ctr0) return set_err(OTC_ERR_ARG, "null counter");
     return ctr_common(in, out, nbytes, k, ctr_add(ctr_from_bytes(ctr0), block_offset, false), false, impl, stream);
+}
+
+/* ---- resumable CTR stream (PolarSSL aes_crypt_ctr semantics on device) ----
+ * Reference: aes-modes/aes.c:869-900 -- byte-granular nc_off, the keystream
+ * block of the current counter kept in stream_block, the counter advanced when
+ * a block is generated.  The host edge does the partial blocks: the head
+ * (bytes left in stream_block) is one tiny XOR launch with those bytes as
+ * kernel arguments, the tail's keystream block is computed on the host (one
+ * AES block) and kept in the context; the kernels do every whole block.  A
+ * body left misaligned by the head runs the funnel-shift kernel. */
+extern "C" int otc_aes_ctr_ctx_init(otc_aes_ctr_ctx *ctx, const uint8_t nonce_counter[16])
+{
+    if (!ctx || !nonce_counter) return set_err(OTC_ERR_ARG, "null argument");
+    memset(ctx, 0, sizeof *ctx);
+    memcpy(ctx->nonce_counter, nonce_counter, 16);
+    return OTC_OK;
+}
+
+extern "C" int otc_aes_ctr_stream(otc_aes_ctr_ctx *ctx, const otc_aes_key *k, size_t length, const void *in,
+                                  void *out, int impl, void *stream)
+{
+    Range rg("otc_aes_ctr_stream");
+    if (!ctx) return set_err(OTC_ERR_ARG, "null context");
+    if (ctx->nc_off > 15) return set_err(OTC_ERR_ARG, "nc_off must be 0..15");
+    int r = check_key(k, OTC_DIR_ENCRYPT);
+    if (r) return r;
+    if (length == 0) return OTC_OK;
+    if (!in || !out) return set_err(OTC_ERR_ARG, "aes_ctr_stream: null buffer");
+    const uintptr_t a = (uintptr_t)in, b = (uintptr_t)out;
+    if (a != b && a < b + length && b < a + length)
+        return set_err(OTC_ERR_ARG, "aes_ctr_stream: input and output overlap partially");
+    if ((a & 15u) != (b & 15u))
+        return set_err(OTC_ERR_ARG, "aes_ctr_stream: in and out must have the same alignment modulo 16");
+    hipStream_t st = (hipStream_t)stream;
+    const size_t n0 = ctx->nc_off;
+    const size_t head = n0 ? std::min(length, (size_t)16 - n0) : 0;
+    if (head) {
+        hipError_t e = otc_impl::xor_small(in, out, (uint32_t)head, ctx->stream_block + n0, st);
+        if (e != hipSuccess) return hip_fail(e, "ctr_stream head");
+    }
+    const size_t body = length - head;
+    if (body == 0) {
+        ctx->nc_off = (n0 + head) & 15u;
+        return OTC_OK;
+    }
+    const uint8_t *bi = (const uint8_t *)in + head;
+    uint8_t *bo = (uint8_t *)out + head;
+    const Ctr128 c = ctr_from_bytes(ctx->nonce_counter);
+    if ((((uintptr_t)bi) & 15u) == 0) {
+        if ((r = ctr_common(bi, bo, body, k, c, false, impl, stream))) return r;
+    } else {
+        hipError_t e = otc_impl::tt_ctr_shift(bi, bo, body, *k, c, st);
+        if (e != hipSuccess) return hip_fail(e, "ctr_stream body (misaligned)");
+    }
+    const uint64_t full = body / 16, tail = body % 16;
+    if (tail) { /* keep the keystream block of the partial tail */
+        Ctr128 t = ctr_add(c, full, false);
+        uint8_t cb[16];
+        for (int i = 0; i < 8; ++i) cb[i] = (uint8_t)(t.hi >> (56 - 8 * i));
+        for (int i = 0; i < 8; ++i) cb[8 + i] = (uint8_t)(t.lo >> (56 - 8 * i));
+        aes_context actx;
+        aes_import_rk32(&actx, k->rk, k->nr);
+        aes_crypt_ecb(&actx, AES_ENCRYPT, cb, ctx->stream_block);
+    }
+    const Ctr128 nx = ctr_add(c, full + (tail ? 1 : 0), false);
+    for (int i = 0; i < 8; ++i) ctx->nonce_counter[i] = (uint8_t)(nx.hi >> (56 - 8 * i));
+    for (int i = 0; i < 8; ++i) ctx->nonce_counter[8 + i] = (uint8_t)(nx.lo >> (56 - 8 * i));
+    ctx->nc_off = (size_t)tail;
+    return OTC_OK;
 }
 
 extern "C" int otc_aes_ctr_rfc3686(const void *in, void *out, size_t nbytes, const otc_aes_key *k,

@@ -62,6 +62,9 @@ int aes_self_test(int verbose);
 /* Copy the (4*(nr+1)) round-key words into a packed uint32 array; returns the
  * word count.  This is the format uploaded to the GPU kernels. */
 int aes_export_rk32(const aes_context *ctx, uint32_t *out);
+/* Inverse of aes_export_rk32: a context over (4*(nr+1)) packed round-key
+ * words (either direction's schedule). */
+int aes_import_rk32(aes_context *ctx, const uint32_t *rk, int nr);
 
 /* Multi-threaded bulk helpers used by the CPU-baseline harness and the tests.
  * Counter semantics = aes_crypt_ctr with nc_off == 0 (full 128-bit BE add). */

@@ -79,6 +79,21 @@ int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_aes_key *k, 
 int otc_aes_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
                 const uint8_t ctr0[16], uint64_t block_offset, int impl, void *stream);
 
+/* Resumable CTR stream on device buffers with the PolarSSL context semantics
+ * (reference aes-modes/aes.c:869-900): nonce_counter = counter of the NEXT
+ * block to generate, stream_block = keystream of the current block, nc_off =
+ * bytes of it already used.  Calls may split the stream at any byte; in and
+ * out may be misaligned but must share their alignment modulo 16.  The
+ * context is updated on return (the launches are asynchronous on `stream`). */
+typedef struct {
+    uint8_t nonce_counter[16];
+    uint8_t stream_block[16];
+    size_t nc_off;
+} otc_aes_ctr_ctx;
+int otc_aes_ctr_ctx_init(otc_aes_ctr_ctx *ctx, const uint8_t nonce_counter[16]);
+int otc_aes_ctr_stream(otc_aes_ctr_ctx *ctx, const otc_aes_key *k, size_t length, const void *in, void *out,
+                       int impl, void *stream);
+
 /* CTR with the AES-NI/RFC 3686 counter layout nonce[4] || ivec[8] || BE32(1),
  * the low 8 bytes incremented as a 64-bit big-endian integer
  * (reference aesni.c:120-152). */

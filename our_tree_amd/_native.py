@@ -69,6 +69,14 @@ class Rc4State(ctypes.Structure):
     _fields_ = [("perm", ctypes.c_char * 256), ("index1", ctypes.c_int), ("index2", ctypes.c_int)]
 
 
+class OtcCtrCtx(ctypes.Structure):
+    """Mirror of ``otc_aes_ctr_ctx`` (PolarSSL CTR resume state,
+    reference aes-modes/aes.c:869-900)."""
+
+    _fields_ = [("nonce_counter", ctypes.c_uint8 * 16), ("stream_block", ctypes.c_uint8 * 16),
+                ("nc_off", ctypes.c_size_t)]
+
+
 class StreamStats(ctypes.Structure):
     _fields_ = [
         ("total_ms", ctypes.c_double),
@@ -152,6 +160,8 @@ def _declare_gpu(lib):
         "otc_aes_ecb": (c_int, [c_vp, c_vp, c_sz, K, c_int, c_vp]),
         "otc_aes_ctr": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_u64, c_int, c_vp]),
         "otc_aes_ctr_rfc3686": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_u8p, c_u64, c_int, c_vp]),
+        "otc_aes_ctr_ctx_init": (c_int, [P(OtcCtrCtx), c_u8p]),
+        "otc_aes_ctr_stream": (c_int, [P(OtcCtrCtx), K, c_sz, c_vp, c_vp, c_int, c_vp]),
         "otc_aes_cbc_decrypt": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cbc_encrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cbc_decrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),

@@ -119,6 +119,68 @@ BATCH_ALIGN_MIN_TILES = 6  # counter-aligned tiling pays once (n+1) x 133 < n x 
 BATCH_TILE_COST = {256: 1.0, 128: 1.015, 64: 1.055}
 
 
+class CtrStream:
+    """Resumable AES-CTR over device tensors with the PolarSSL context
+    semantics (reference aes-modes/aes.c:869-900): the stream may be split at
+    ANY byte across ``update`` calls and the result equals one-shot ``ctr``.
+    The context (``nonce_counter``, ``stream_block``, ``nc_off``) is host
+    state; ``state()`` / ``CtrStream.from_state`` checkpoint and resume it.
+
+    Tensors may start at any byte (slices): the native call handles a head
+    from ``stream_block``, a misaligned body with the funnel-shift kernel and a
+    tail whose keystream block is kept for the next call."""
+
+    def __init__(self, key: bytes, nonce_counter: bytes, impl="auto"):
+        self._key = bytes(key)
+        self._k = expand_key(self._key)
+        self._impl = _impl(impl)
+        self.ctx = _native.OtcCtrCtx()
+        _native.check(_lib().otc_aes_ctr_ctx_init(ctypes.byref(self.ctx), _b16(nonce_counter, "nonce_counter")),
+                      "otc_aes_ctr_ctx_init")
+
+    @property
+    def nonce_counter(self) -> bytes:
+        return bytes(self.ctx.nonce_counter)
+
+    @property
+    def stream_block(self) -> bytes:
+        return bytes(self.ctx.stream_block)
+
+    @property
+    def nc_off(self) -> int:
+        return int(self.ctx.nc_off)
+
+    def state(self) -> dict:
+        return {"nonce_counter": self.nonce_counter, "stream_block": self.stream_block, "nc_off": self.nc_off}
+
+    @classmethod
+    def from_state(cls, key: bytes, state: dict, impl="auto") -> "CtrStream":
+        s = cls(key, state["nonce_counter"], impl)
+        ctypes.memmove(s.ctx.stream_block, bytes(state["stream_block"]), 16)
+        s.ctx.nc_off = int(state["nc_off"])
+        return s
+
+    def update(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        _check_dev(x, "x")
+        out = _out_like(x, out)
+        n = _nbytes(x)
+        if n == 0:
+            return out
+        xp, op = x.data_ptr(), out.data_ptr()
+        target = out
+        if xp % 16 != op % 16:  # the native call needs a common alignment: stage the output
+            tmp = torch.empty(n + 16, dtype=torch.uint8, device=x.device)
+            off = (xp - tmp.data_ptr()) % 16
+            target = tmp[off:off + n]
+        with torch.cuda.device(x.device):
+            rc = _lib().otc_aes_ctr_stream(ctypes.byref(self.ctx), ctypes.byref(self._k), n, xp, target.data_ptr(),
+                                           self._impl, _stream(x))
+        _native.check(rc, "otc_aes_ctr_stream")
+        if target is not out:
+            _bytes(out).copy_(target)
+        return out
+
+
 def _pick_tile(nbytes) -> int:
     """Tile size minimising (tile slots issued) x (cost per slot)."""
     best, best_cost = 256, None
