@@ -56,7 +56,7 @@ $(OBJ)/cpu/%.o: csrc/cpu/%.c $(wildcard csrc/include/*.h)
 
 $(OBJ)/cpu/bs_selftest.o: csrc/cpu/bs_selftest.cpp csrc/include/otc_bitslice.h
 	@mkdir -p $(dir $@)
-	$(CXX) $(CXXFLAGS) $(INC) -c $< -o $@
+	$(CXX) $(CXXFLAGS) -Wno-unknown-pragmas $(INC) -c $< -o $@
 
 # -fno-slp-vectorize: the SLP vectorizer packs the 4 independent transposes /
 # 16 S-boxes of the bitsliced kernel into lock-stepped vector ops, which doubles

@@ -131,6 +131,37 @@ extern "C" int otc_bitslice_selftest(int verbose)
         }
         if (verbose) printf("  bitsliced AES-%d kernel schedule: %s\n", bits, bad ? "failed" : "passed");
         fails += bad;
+
+        /* rolled-loop round structure (round_step / round_final), both
+         * MixColumns forms */
+        for (int mixt = 0; mixt < 2; ++mixt) {
+            for (int w = 0; w < 4; ++w) {
+                W m[32];
+                for (int k = 0; k < 32; ++k) memcpy(&m[k], &pt[k][4 * w], 4);
+                transpose32(m);
+                for (int q = 0; q < 32; ++q) s[32 * w + q] = m[q];
+            }
+            for (int r = 0; r + 1 < ctx.nr; ++r) {
+                auto kr = [&](int p) -> W { return kf(r, p); };
+                if (mixt) round_step<true>(s, kr);
+                else round_step<false>(s, kr);
+            }
+            round_final(s, [&](int p) -> W { return kf(ctx.nr - 1, p); });
+            bad = 0;
+            for (int w = 0; w < 4; ++w) {
+                W m[32];
+                for (int q = 0; q < 32; ++q) m[q] = s[32 * w + q];
+                transpose32(m);
+                for (int k = 0; k < 32; ++k) {
+                    uint32_t v = m[k] ^ rk[4 * ctx.nr + w];
+                    bad += memcmp(&v, &ref[k][4 * w], 4) != 0;
+                }
+            }
+            if (verbose)
+                printf("  bitsliced AES-%d rolled rounds%s: %s\n", bits, mixt ? " (low-register MixColumns)" : "",
+                       bad ? "failed" : "passed");
+            fails += bad;
+        }
     }
     return fails ? 1 : 0;
 }

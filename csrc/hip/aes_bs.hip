@@ -46,7 +46,21 @@ struct BsParams {
     uint32_t wrap64;    /* CTR: 64-bit counter increment */
     uint64_t shift;     /* CTR: ctr0.lo mod 2048 (virtual index = i + shift) */
     Ctr128 cbase;       /* CTR: ctr0 with the low 11 bits cleared */
+    uint32_t stagger;   /* 100 MHz ticks of start delay per residency slot (0: none) */
+    uint32_t cus;       /* CUs (residency slot of workgroup b = b / cus) */
 };
+
+/* Start-time stagger for the first resident round of workgroups: slot
+ * b / cus (0, 1, 2 on a 3-wave build) waits slot * stagger ticks, so the
+ * waves sharing a SIMD do not run their memory phases in lockstep.  Later
+ * workgroups replace finished ones and inherit the offsets. */
+__device__ __forceinline__ void stagger_start(const BsParams &P, uint32_t slots)
+{
+    if (P.stagger == 0 || blockIdx.x >= slots * P.cus) return;
+    const uint64_t wait = (uint64_t)(blockIdx.x / P.cus) * P.stagger;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < wait) __builtin_amdgcn_s_sleep(8);
+}
 
 enum : int { BS_CTR = 0, BS_ECB = 1 };
 
@@ -226,6 +240,173 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
     }
 }
 
+/* Same task with a ROLLED round loop: the fully unrolled kernel is ~150 KB
+ * of code (AES-128), larger than the instruction cache, so every wave streams
+ * the whole kernel from L2 (SQ_IFETCH ~4800 x 32 B per wave).  Here rounds
+ * 0..NR-2 are one ~14 KB loop body (round keys read per round from the
+ * kernel-argument segment by scalar loads), the final round is peeled.
+ * MIXT: low-register MixColumns (mix_column_t). */
+template <int NR, int MODE, bool MIXT, int LS, bool ZEROKEY = false, int FENCE = 2>
+__device__ __forceinline__ void aes_bs_task_loop(const BsParams &P, const otc_aes_key &K, uint4 *stage)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t gwave = (uint64_t)blockIdx.x * 4u + wave;
+    const uint64_t shift = (MODE == BS_CTR) ? P.shift : 0;
+    const uint64_t vtotal = P.nblocks + shift;
+    const uint64_t task = gwave;
+    if (task * 2048u >= vtotal) return;
+    const uint64_t vbase = task * 2048u;
+    const bool full = vbase >= shift && vbase + 2048u - shift <= P.nblocks;
+    W s[128];
+    if (MODE == BS_CTR && LS > 0) {
+        /* plaintext of slots 0..LS-1 straight into LDS (no VGPRs): lands
+         * while the rounds run; the rounds issue no vector memory op, so no
+         * vmcnt wait before the output phase depends on it */
+        const int64_t t0 = (int64_t)vbase - (int64_t)P.shift;
+        const uint8_t *ib0 = P.in + t0 * 16 + lane * 16u;
+#pragma unroll
+        for (int k = 0; k < LS; ++k) {
+            const int64_t si = t0 + (int64_t)lane + 64 * k;
+            const bool ok = full || (si >= 0 && (uint64_t)si < P.nblocks);
+            __builtin_amdgcn_global_load_lds((const void *)(ok ? ib0 + 1024u * k : P.in),
+                                             (__attribute__((address_space(3))) void *)&stage[(wave * LS + k) * 64],
+                                             16, 0, 0);
+        }
+    }
+    if (MODE == BS_CTR) {
+        uint64_t clo = P.cbase.lo + vbase;
+        uint64_t chi = P.cbase.hi + ((!P.wrap64 && clo < P.cbase.lo) ? 1u : 0u);
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int n = 8 * (15 - b) + i;
+                W v;
+                if (n < 6) {
+                    v = lane_mask(lane, n);
+                } else if (n < 11) {
+                    constexpr W pat[5] = {0xAAAAAAAAu, 0xCCCCCCCCu, 0xF0F0F0F0u, 0xFF00FF00u, 0xFFFF0000u};
+                    v = pat[n - 6];
+                } else if (n < 64) {
+                    v = (W)(0u - (uint32_t)((clo >> n) & 1u));
+                } else {
+                    v = (W)(0u - (uint32_t)((chi >> (n - 64)) & 1u));
+                }
+                s[8 * b + i] = v;
+            }
+        }
+        /* the counter planes are uniform except 11 per-lane ones: make them
+         * VGPRs now (the loop needs one register layout for every round) */
+#pragma unroll
+        for (int q = 0; q < 128; ++q) asm volatile("" : "+v"(s[q]));
+    } else {
+        const uint8_t *tb = P.in + vbase * 16;
+        const uint32_t lo = lane * 16u;
+        uint4 blk[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            const uint64_t i = vbase + lane + 64u * k;
+            blk[k] = (full || i < P.nblocks) ? *(const uint4 *)(tb + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            W m[32];
+#pragma unroll
+            for (int k = 0; k < 32; ++k) m[k] = w == 0 ? blk[k].x : w == 1 ? blk[k].y : w == 2 ? blk[k].z : blk[k].w;
+            transpose32(m);
+            pin_n(m, 32);
+#pragma unroll
+            for (int q = 0; q < 32; ++q) s[32 * w + q] = m[q];
+            sched_fence();
+        }
+    }
+    sched_fence();
+#pragma nounroll
+    for (int r = 0; r < NR - 1; ++r) {
+        uint32_t kw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) kw[j] = K.rk[4 * r + j];
+        auto kz = [&](int p) -> W { return (W)0; };
+        auto kr = [&](int p) -> W { return (W)(0u - ((kw[p >> 5] >> (p & 31)) & 1u)); };
+        if (ZEROKEY) /* measurement only: key masks folded away (wrong output) */
+            round_step<MIXT, decltype(kz), FENCE>(s, kz);
+        else
+            round_step<MIXT, decltype(kr), FENCE>(s, kr);
+        pin_n(s, 128);
+    }
+    {
+        uint32_t kw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) kw[j] = K.rk[4 * (NR - 1) + j];
+        round_final(s, [&](int p) -> W { return (W)(0u - ((kw[p >> 5] >> (p & 31)) & 1u)); });
+    }
+    pin_n(s, 128);
+    sched_fence();
+
+    const int64_t tstart = (int64_t)vbase - (int64_t)shift;
+    const uint8_t *ib = P.in + tstart * 16;
+    uint8_t *ob = P.out + tstart * 16;
+    uint32_t lo = lane * 16u;
+    asm volatile("" : "+v"(lo));
+    auto slot_ok = [&](int k) {
+        const int64_t si = tstart + (int64_t)lane + 64 * k;
+        return full || (si >= 0 && (uint64_t)si < P.nblocks);
+    };
+    /* register-loaded plaintext (slots LS..31): all issued before the
+     * transposes, none after a store -- vmcnt is in order on gfx9, so a load
+     * issued behind stores would also wait for them */
+    uint4 pt[32];
+    if (MODE == BS_CTR) {
+#pragma unroll
+        for (int k = LS; k < 32; ++k)
+            pt[k] = slot_ok(k) ? *(const uint4 *)(ib + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
+    }
+    sched_fence();
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        transpose32(s + 32 * w);
+        pin_n(s + 32 * w, 32);
+        sched_fence();
+    }
+    const uint32_t k0 = K.rk[4 * NR + 0], k1 = K.rk[4 * NR + 1], k2 = K.rk[4 * NR + 2], k3 = K.rk[4 * NR + 3];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t off = lo + 1024u * k;
+        if (slot_ok(k)) {
+            uint4 o;
+            if (MODE == BS_CTR) {
+                const uint4 x = k < LS ? stage[(wave * LS + k) * 64 + (lo >> 4)] : pt[k];
+                o.x = x3(x.x, s[k], k0);
+                o.y = x3(x.y, s[32 + k], k1);
+                o.z = x3(x.z, s[64 + k], k2);
+                o.w = x3(x.w, s[96 + k], k3);
+            } else {
+                o = make_uint4(s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3);
+            }
+            *(uint4 *)(ob + off) = o;
+        }
+    }
+}
+
+template <int NR, int MODE, bool MIXT, int LS, bool ZK = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_aes_bs_loop3(BsParams P,
+                                                                                                 otc_aes_key K)
+{
+    __shared__ uint4 stage[LS > 0 ? 4 * LS * 64 : 1];
+    stagger_start(P, 3);
+    aes_bs_task_loop<NR, MODE, MIXT, LS, ZK>(P, K, stage);
+}
+
+template <int NR, int MODE, bool MIXT, int LS, bool ZK = false, int FENCE = 2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_aes_bs_loop2(BsParams P,
+                                                                                                 otc_aes_key K)
+{
+    __shared__ uint4 stage[LS > 0 ? 4 * LS * 64 : 1];
+    stagger_start(P, 2);
+    aes_bs_task_loop<NR, MODE, MIXT, LS, ZK, FENCE>(P, K, stage);
+}
+
 template <int NR, int MODE, bool CACHE, int PF, int LS>
 __global__ __launch_bounds__(256) void k_aes_bs(BsParams P, otc_aes_key K)
 {
@@ -241,6 +422,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                                                                                              otc_aes_key K)
 {
     __shared__ uint4 stage[LS > 0 ? 4 * LS * 64 : 1];
+    stagger_start(P, 3);
     aes_bs_task<NR, MODE, false, 0, LS>(P, K, stage);
 }
 
@@ -266,8 +448,33 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
      * (measured: docs/PERF.md).  OTC_BS_W3=0 selects the 2-wave builds. */
     static const bool w3 = !getenv("OTC_BS_W3") || atoi(getenv("OTC_BS_W3")) != 0;
     static const bool lds = getenv("OTC_BS_LDS") && atoi(getenv("OTC_BS_LDS")) != 0;
-    if (w3 && !(MODE == BS_CTR && cache)) {
-        hipLaunchKernelGGL((k_aes_bs_w3<NR, MODE, 0>), g, b, 0, st, P, K);
+    /* OTC_BS_LOOP=1|2|3: rolled round loop (1: 3 waves + low-register
+     * MixColumns, 2: 2 waves, 3: 3 waves + classic MixColumns);
+     * OTC_BS_STAGGER=ticks: start stagger per residency slot (A/B knobs) */
+    static const int loop = getenv("OTC_BS_LOOP") ? atoi(getenv("OTC_BS_LOOP")) : 0;
+    BsParams Q = P;
+    Q.stagger = getenv("OTC_BS_STAGGER") ? (uint32_t)atoi(getenv("OTC_BS_STAGGER")) : 0u;
+    Q.cus = (uint32_t)device_cus();
+    if (loop == 1) {
+        hipLaunchKernelGGL((k_aes_bs_loop3<NR, MODE, true, 0>), g, b, 0, st, Q, K);
+    } else if (loop == 2) {
+        hipLaunchKernelGGL((k_aes_bs_loop2<NR, MODE, true, 0>), g, b, 0, st, Q, K);
+    } else if (loop == 4) { /* 2 waves, 20 LDS-prefetched slots (2 x 80 KiB per CU) */
+        hipLaunchKernelGGL((k_aes_bs_loop2<NR, MODE, true, (MODE == BS_CTR ? 20 : 0)>), g, b, 0, st, Q, K);
+    } else if (loop == 5) { /* 2 waves, 16 LDS slots */
+        hipLaunchKernelGGL((k_aes_bs_loop2<NR, MODE, true, (MODE == BS_CTR ? 16 : 0)>), g, b, 0, st, Q, K);
+    } else if (loop == 7) { /* measurement only: 3 waves, zero key */
+        hipLaunchKernelGGL((k_aes_bs_loop3<NR, MODE, true, 0, true>), g, b, 0, st, Q, K);
+    } else if (loop == 8) { /* measurement only: 2 waves, zero key, LDS prefetch */
+        hipLaunchKernelGGL((k_aes_bs_loop2<NR, MODE, true, (MODE == BS_CTR ? 20 : 0), true>), g, b, 0, st, Q, K);
+    } else if (loop == 9) { /* 2 waves, LDS prefetch, pins only */
+        hipLaunchKernelGGL((k_aes_bs_loop2<NR, MODE, true, (MODE == BS_CTR ? 20 : 0), false, 1>), g, b, 0, st, Q, K);
+    } else if (loop == 10) { /* 2 waves, LDS prefetch, no fences */
+        hipLaunchKernelGGL((k_aes_bs_loop2<NR, MODE, true, (MODE == BS_CTR ? 20 : 0), false, 0>), g, b, 0, st, Q, K);
+    } else if (loop == 6) { /* 3 waves, 12 LDS slots (3 x 48 KiB per CU) */
+        hipLaunchKernelGGL((k_aes_bs_loop3<NR, MODE, true, (MODE == BS_CTR ? 12 : 0)>), g, b, 0, st, Q, K);
+    } else if (w3 && !(MODE == BS_CTR && cache)) {
+        hipLaunchKernelGGL((k_aes_bs_w3<NR, MODE, 0>), g, b, 0, st, Q, K);
     } else if (MODE == BS_CTR && cache) {
         hipLaunchKernelGGL((k_aes_bs<NR, MODE, true, 0, 0>), g, b, 0, st, P, K);
     } else if constexpr (MODE == BS_CTR && NR == 10) {

@@ -32,6 +32,7 @@
 #define OTC_BS_FENCE_MC 0
 #endif
 
+
 namespace otc_bs {
 
 typedef uint32_t W;
@@ -208,6 +209,33 @@ OTC_HD void mix_column(const W *in, W *out)
     }
 }
 
+/* Low-register MixColumns of one column: t = a0^a1^a2^a3 first, then rows
+ * in order, out_r[i] = xt(a_r ^ a_{r+1})[i] ^ t[i] ^ a_r[i] computed bit by
+ * bit (only d7 = a_r[7] ^ a_{r+1}[7] is kept), so besides the 32 inputs only
+ * t and one row of outputs are live (vs the 32 d_r planes of mix_column):
+ * 80 ops instead of 76, ~20 fewer live registers at the mix peak. */
+template <bool VEC>
+OTC_HD void mix_column_t(const W *in, W *out)
+{
+    W t[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[i] = xx3<VEC>(in[i], in[8 + i], in[16 + i]) ^ in[24 + i];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const W *ar = in + 8 * r, *an = in + 8 * ((r + 1) & 3);
+        W *o = out + 8 * r;
+        const W d7 = ar[7] ^ an[7];
+        o[0] = xx3<VEC>(d7, t[0], ar[0]);
+#pragma unroll
+        for (int i = 1; i < 8; ++i) {
+            const bool fb = (i == 1 || i == 3 || i == 4); /* x^8 = x^4+x^3+x+1 feedback */
+            const W u = fb ? xx3<VEC>(ar[i - 1], an[i - 1], d7) : xx3<VEC>(ar[i - 1], an[i - 1], t[i]);
+            o[i] = fb ? xx3<VEC>(u, t[i], ar[i]) : (u ^ ar[i]);
+        }
+        if (OTC_BS_FENCE_MC) sched_fence();
+    }
+}
+
 /* ShiftRows: new byte (r,c) = old byte (r, c+r mod 4). */
 OTC_HD void shift_rows(const W *in, W *out)
 {
@@ -326,6 +354,65 @@ OTC_HD void encrypt_round(W *s, KF &kf)
 #pragma unroll
         for (int q = 0; q < 128; ++q) s[q] = t[q];
     }
+}
+
+/* One non-final round as a self-contained step (the body of a ROLLED round
+ * loop): S-box every byte with the round key folded in (kf(p): mask of plane
+ * p), ShiftRows by renaming, MixColumns (MIXT: the low-register form), result
+ * back in s[] in the canonical layout.  Streaming column order as in
+ * encrypt_round. */
+template <bool MIXT, class KF, int FENCE = 2>
+OTC_HD void round_step(W *s, KF kf)
+{
+    W ns[128];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        W col[32];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int b = r + 4 * ((c + r) & 3);
+            W *x = s + 8 * b;
+            const int p = 8 * b;
+            sbox_lut3(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kf(p), kf(p + 1), kf(p + 2), kf(p + 3),
+                      kf(p + 4), kf(p + 5), kf(p + 6), kf(p + 7));
+            /* FENCE 2: pin + scheduling barrier per S-box (lowest register
+             * pressure); 1: pin only; 0: the scheduler may interleave
+             * S-boxes (more ILP, more registers) */
+            if (FENCE >= 1) pin8(x);
+            if (FENCE >= 2) sched_fence();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) col[8 * r + i] = x[i];
+        }
+        if (MIXT)
+            mix_column_t<true>(col, ns + 32 * c);
+        else
+            mix_column<true>(col, ns + 32 * c);
+        if (FENCE >= 2) {
+            pin_n(ns + 32 * c, 32);
+            sched_fence();
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 128; ++q) s[q] = ns[q];
+}
+
+/* Final round: S-box with key kf folded in + ShiftRows (the last round key
+ * is left to the caller's output XOR, as in encrypt_planes). */
+template <class KF>
+OTC_HD void round_final(W *s, KF kf)
+{
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        W *x = s + 8 * b;
+        const int p = 8 * b;
+        sbox_lut3(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kf(p), kf(p + 1), kf(p + 2), kf(p + 3),
+                  kf(p + 4), kf(p + 5), kf(p + 6), kf(p + 7));
+        pin8(x);
+    }
+    W t[128];
+    shift_rows(s, t);
+#pragma unroll
+    for (int q = 0; q < 128; ++q) s[q] = t[q];
 }
 
 /* Rounds 1..NR of AES on bitsliced planes s[128] (AddRoundKey r folded into
