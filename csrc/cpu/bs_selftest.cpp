@@ -162,6 +162,38 @@ extern "C" int otc_bitslice_selftest(int verbose)
                        bad ? "failed" : "passed");
             fails += bad;
         }
+
+        /* rounds reading the precomputed key-term table (the GPU kernel's
+         * scalar-load key path) */
+        {
+            static uint32_t tab[14 * 16 * OTC_BS_KT_STRIDE];
+            key_term_table(rk, ctx.nr, tab);
+            for (int w = 0; w < 4; ++w) {
+                W m[32];
+                for (int k = 0; k < 32; ++k) memcpy(&m[k], &pt[k][4 * w], 4);
+                transpose32(m);
+                for (int q = 0; q < 32; ++q) s[32 * w + q] = m[q];
+            }
+            for (int r = 0; r + 1 < ctx.nr; ++r)
+                round_step_kt<true>(s, [&](int b, W *t) {
+                    for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = tab[(r * 16 + b) * OTC_BS_KT_STRIDE + j];
+                });
+            round_final_kt(s, [&](int b, W *t) {
+                for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = tab[((ctx.nr - 1) * 16 + b) * OTC_BS_KT_STRIDE + j];
+            });
+            bad = 0;
+            for (int w = 0; w < 4; ++w) {
+                W m[32];
+                for (int q = 0; q < 32; ++q) m[q] = s[32 * w + q];
+                transpose32(m);
+                for (int k = 0; k < 32; ++k) {
+                    uint32_t v = m[k] ^ rk[4 * ctx.nr + w];
+                    bad += memcmp(&v, &ref[k][4 * w], 4) != 0;
+                }
+            }
+            if (verbose) printf("  bitsliced AES-%d key-term table rounds: %s\n", bits, bad ? "failed" : "passed");
+            fails += bad;
+        }
     }
     return fails ? 1 : 0;
 }

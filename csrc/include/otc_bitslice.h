@@ -356,13 +356,16 @@ OTC_HD void encrypt_round(W *s, KF &kf)
     }
 }
 
-/* One non-final round as a self-contained step (the body of a ROLLED round
- * loop): S-box every byte with the round key folded in (kf(p): mask of plane
- * p), ShiftRows by renaming, MixColumns (MIXT: the low-register form), result
- * back in s[] in the canonical layout.  Streaming column order as in
- * encrypt_round. */
-template <bool MIXT, class KF, int FENCE = 2>
-OTC_HD void round_step(W *s, KF kf)
+/* One non-final round as a self-contained step: S-box every byte with the
+ * round key folded in, ShiftRows by renaming, MixColumns (MIXT: the
+ * low-register form), result back in s[] in the canonical layout, in the
+ * streaming column order of encrypt_round.
+ *
+ * The key comes as S-box key TERMS: kt(b, t) fills the OTC_SBOX_KEY_TERMS
+ * values of byte b (sbox_key_terms of its 8 plane masks) -- computed from the
+ * round key on the fly (KeyMasks) or read from a precomputed table. */
+template <bool MIXT, class KT, int FENCE = 2>
+OTC_HD void round_step_kt(W *s, KT kt)
 {
     W ns[128];
 #pragma unroll
@@ -372,12 +375,14 @@ OTC_HD void round_step(W *s, KF kf)
         for (int r = 0; r < 4; ++r) {
             const int b = r + 4 * ((c + r) & 3);
             W *x = s + 8 * b;
-            const int p = 8 * b;
-            sbox_lut3(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kf(p), kf(p + 1), kf(p + 2), kf(p + 3),
-                      kf(p + 4), kf(p + 5), kf(p + 6), kf(p + 7));
-            /* FENCE 2: pin + scheduling barrier per S-box (lowest register
-             * pressure); 1: pin only; 0: the scheduler may interleave
-             * S-boxes (more ILP, more registers) */
+            W t[OTC_SBOX_KEY_TERMS];
+            kt(b, t);
+            /* FENCE 3: every LUT output pinned in the low-pressure order of
+             * tools/sbox_schedule.py; 2: pin + scheduling barrier per S-box;
+             * 1: pin only; 0: the scheduler may interleave S-boxes (more ILP,
+             * more registers) */
+            sbox_lut3_c<(FENCE >= 3)>(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], t[0], t[1], t[2], t[3], t[4],
+                                      t[5], t[6], t[7], t[8], t[9], t[10]);
             if (FENCE >= 1) pin8(x);
             if (FENCE >= 2) sched_fence();
 #pragma unroll
@@ -396,23 +401,65 @@ OTC_HD void round_step(W *s, KF kf)
     for (int q = 0; q < 128; ++q) s[q] = ns[q];
 }
 
-/* Final round: S-box with key kf folded in + ShiftRows (the last round key
+/* Final round: S-box with the key folded in + ShiftRows (the last round key
  * is left to the caller's output XOR, as in encrypt_planes). */
-template <class KF>
-OTC_HD void round_final(W *s, KF kf)
+template <class KT>
+OTC_HD void round_final_kt(W *s, KT kt)
 {
 #pragma unroll
     for (int b = 0; b < 16; ++b) {
         W *x = s + 8 * b;
-        const int p = 8 * b;
-        sbox_lut3(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kf(p), kf(p + 1), kf(p + 2), kf(p + 3),
-                  kf(p + 4), kf(p + 5), kf(p + 6), kf(p + 7));
+        W t[OTC_SBOX_KEY_TERMS];
+        kt(b, t);
+        sbox_lut3_c(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7],
+                    t[8], t[9], t[10]);
         pin8(x);
     }
     W t[128];
     shift_rows(s, t);
 #pragma unroll
     for (int q = 0; q < 128; ++q) s[q] = t[q];
+}
+
+/* key terms from a plane-mask functor kf(p) */
+template <class KF>
+struct KeyMasks {
+    KF kf;
+    OTC_HD void operator()(int b, W *t) const
+    {
+        const int p = 8 * b;
+        sbox_key_terms(kf(p), kf(p + 1), kf(p + 2), kf(p + 3), kf(p + 4), kf(p + 5), kf(p + 6), kf(p + 7), t);
+    }
+};
+
+template <bool MIXT, class KF, int FENCE = 2>
+OTC_HD void round_step(W *s, KF kf)
+{
+    round_step_kt<MIXT, KeyMasks<KF>, FENCE>(s, KeyMasks<KF>{kf});
+}
+
+template <class KF>
+OTC_HD void round_final(W *s, KF kf)
+{
+    round_final_kt(s, KeyMasks<KF>{kf});
+}
+
+/* Precomputed key-term table of a whole key schedule: for round r (0..NR-1,
+ * the key folded into that round's S-boxes) and byte b, OTC_BS_KT_STRIDE
+ * words at ((r * 16 + b) * OTC_BS_KT_STRIDE): the 11 terms + 1 pad word (so
+ * a byte's terms are 3 aligned 16-byte scalar loads). */
+#define OTC_BS_KT_STRIDE 12
+OTC_HD void key_term_table(const uint32_t *rk, int nr, uint32_t *tab)
+{
+    for (int r = 0; r < nr; ++r)
+        for (int b = 0; b < 16; ++b) {
+            const uint32_t byte = (rk[4 * r + (b >> 2)] >> (8 * (b & 3))) & 0xFFu;
+            W k[8];
+            for (int i = 0; i < 8; ++i) k[i] = ((byte >> i) & 1u) ? ~0u : 0u;
+            uint32_t *t = tab + (r * 16 + b) * OTC_BS_KT_STRIDE;
+            sbox_key_terms(k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7], t);
+            t[OTC_SBOX_KEY_TERMS] = 0;
+        }
 }
 
 /* Rounds 1..NR of AES on bitsliced planes s[128] (AddRoundKey r folded into

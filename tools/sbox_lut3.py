@@ -190,16 +190,19 @@ static inline W lut3_host(W a, W b, W c, unsigned imm)
 #define lut3(a, b, c, imm) lut3_host((a), (b), (c), (imm))
 #endif
 
-OTC_HD void sbox_lut3(W &x0, W &x1, W &x2, W &x3, W &x4, W &x5, W &x6, W &x7, W k0, W k1, W k2, W k3, W k4,
-                      W k5, W k6, W k7)
+#define OTC_SBOX_KEY_TERMS 11
+
+OTC_HD void sbox_lut3_c(W &x0, W &x1, W &x2, W &x3, W &x4, W &x5, W &x6, W &x7, W K7, W K03, W K05, W K06, W K35,
+                        W K46, W K12, W K15, W K25, W K37, W K67)
 {{
     const W U0 = x7, U1 = x6, U2 = x5, U3 = x4, U4 = x3, U5 = x2, U6 = x1, U7 = x0;
-    const W K7 = k0, K03 = k7 ^ k4, K05 = k7 ^ k2, K06 = k7 ^ k1, K35 = k4 ^ k2, K46 = k3 ^ k1;
-    const W K12 = k6 ^ k5, K15 = k6 ^ k2, K25 = k5 ^ k2, K37 = k4 ^ k0, K67 = k1 ^ k0;
     (void)K7; (void)K03; (void)K05; (void)K06; (void)K35; (void)K46; (void)K12; (void)K15; (void)K25; (void)K37; (void)K67;
 ''' + "\n".join(lines) + '''
     x7 = S0; x6 = S1; x5 = S2; x4 = S3; x3 = S4; x2 = S5; x1 = S6; x0 = S7;
 }
+
+/* (then run tools/sbox_schedule.py: low-pressure statement order, pins, and
+ * the sbox_key_terms / sbox_lut3 wrappers over sbox_lut3_c) */
 
 #undef lut3
 } /* namespace otc_bs */
