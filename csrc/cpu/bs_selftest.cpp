@@ -132,9 +132,9 @@ extern "C" int otc_bitslice_selftest(int verbose)
         if (verbose) printf("  bitsliced AES-%d kernel schedule: %s\n", bits, bad ? "failed" : "passed");
         fails += bad;
 
-        /* rolled-loop round structure (round_step / round_final), both
+        /* rolled-loop round structure (round_step / round_final), all three
          * MixColumns forms */
-        for (int mixt = 0; mixt < 2; ++mixt) {
+        for (int mixt = 0; mixt < 3; ++mixt) {
             for (int w = 0; w < 4; ++w) {
                 W m[32];
                 for (int k = 0; k < 32; ++k) memcpy(&m[k], &pt[k][4 * w], 4);
@@ -143,8 +143,9 @@ extern "C" int otc_bitslice_selftest(int verbose)
             }
             for (int r = 0; r + 1 < ctx.nr; ++r) {
                 auto kr = [&](int p) -> W { return kf(r, p); };
-                if (mixt) round_step<true>(s, kr);
-                else round_step<false>(s, kr);
+                if (mixt == 2) round_step<2>(s, kr);
+                else if (mixt == 1) round_step<1>(s, kr);
+                else round_step<0>(s, kr);
             }
             round_final(s, [&](int p) -> W { return kf(ctx.nr - 1, p); });
             bad = 0;
@@ -158,7 +159,8 @@ extern "C" int otc_bitslice_selftest(int verbose)
                 }
             }
             if (verbose)
-                printf("  bitsliced AES-%d rolled rounds%s: %s\n", bits, mixt ? " (low-register MixColumns)" : "",
+                printf("  bitsliced AES-%d rolled rounds%s: %s\n", bits,
+                       mixt == 2 ? " (searched 55-node MixColumns)" : mixt ? " (low-register MixColumns)" : "",
                        bad ? "failed" : "passed");
             fails += bad;
         }
@@ -192,6 +194,61 @@ extern "C" int otc_bitslice_selftest(int verbose)
                 }
             }
             if (verbose) printf("  bitsliced AES-%d key-term table rounds: %s\n", bits, bad ? "failed" : "passed");
+            fails += bad;
+
+            /* counter-cached CTR task (the GPU kernel's default CTR path):
+             * group constants + per-call S15/S14 planes + rounds 3.. from the
+             * table, for a few lanes of tasks with different u5 / groups */
+            bad = 0;
+            for (int trial = 0; trial < 4; ++trial) {
+                uint64_t hi = ((uint64_t)rand() << 32) ^ (uint64_t)rand();
+                uint64_t lo = (((uint64_t)rand() << 32) ^ (uint64_t)rand()) & ~(uint64_t)2047u;
+                if (trial == 3) lo = ~(uint64_t)0 << 11; /* all-ones bytes, u5 = 31 */
+                const uint32_t u5 = (uint32_t)(lo >> 11) & 31u;
+                uint8_t ctr[16];
+                for (int b = 0; b < 8; ++b) ctr[b] = (uint8_t)(hi >> (8 * (7 - b)));
+                for (int b = 0; b < 8; ++b) ctr[8 + b] = (uint8_t)(lo >> (8 * (7 - b)));
+                static uint32_t grp[OTC_BS_CTR_GRP_WORDS];
+                ctr_group_terms(ctr, rk, grp);
+                const uint32_t *kt15 = tab + 15 * OTC_BS_KT_STRIDE, *kt14 = tab + 14 * OTC_BS_KT_STRIDE;
+                W s14[8];
+                ctr_s14_planes(u5, kt14, s14);
+                for (int lane = 0; lane < 64; lane += 21) {
+                    W s15[8];
+                    ctr_s15_planes((uint32_t)lane, kt15, s15);
+                    ctr_rounds12(s15, s14, [&](int b, W *t) {
+                        for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = grp[b * OTC_BS_KT_STRIDE + j];
+                    }, s);
+                    round_step_kt<true>(s, [&](int b, W *t) {
+                        for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = grp[(8 + b) * OTC_BS_KT_STRIDE + j];
+                    });
+                    for (int r = 3; r + 1 < ctx.nr; ++r)
+                        round_step_kt<true>(s, [&](int b, W *t) {
+                            for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = tab[(r * 16 + b) * OTC_BS_KT_STRIDE + j];
+                        });
+                    round_final_kt(s, [&](int b, W *t) {
+                        for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j)
+                            t[j] = tab[((ctx.nr - 1) * 16 + b) * OTC_BS_KT_STRIDE + j];
+                    });
+                    for (int w = 0; w < 4; ++w) {
+                        W m[32];
+                        for (int q = 0; q < 32; ++q) m[q] = s[32 * w + q];
+                        transpose32(m);
+                        for (int k = 0; k < 32; ++k) {
+                            /* block (lane, slot k) encrypts counter C + 64k + lane */
+                            uint8_t cb[16], ks[16];
+                            memcpy(cb, ctr, 16);
+                            const uint32_t add = 64u * (uint32_t)k + (uint32_t)lane; /* < 2048: bytes 14-15 */
+                            cb[15] = (uint8_t)add;
+                            cb[14] = (uint8_t)((u5 << 3) | (add >> 8));
+                            aes_crypt_ecb(&ctx, AES_ENCRYPT, cb, ks);
+                            uint32_t v = m[k] ^ rk[4 * ctx.nr + w];
+                            bad += memcmp(&v, &ks[4 * w], 4) != 0;
+                        }
+                    }
+                }
+            }
+            if (verbose) printf("  bitsliced AES-%d counter-cached CTR task: %s\n", bits, bad ? "failed" : "passed");
             fails += bad;
         }
     }

@@ -16,14 +16,19 @@
  *     6..10   : 0xAAAAAAAA, 0xCCCCCCCC, ... (a constant pattern over slots)
  *     n >= 11 : bit n of C                  (wave uniform)
  *
- * Default kernel (k_aes_bs_t3), built for 3 waves per SIMD (<= 168 VGPRs)
- * WITHOUT spilling the 128-plane state:
+ * Default kernel (k_aes_bs_t3), built for 3 waves per SIMD (<= 168 VGPRs):
+ *   - CTR counter caching (otc_bitslice.h): bytes 0..13 of the 2048 counters
+ *     of a task are constant, so rounds 1-2 reduce to 8 S-boxes on top of
+ *     per-group constants (k_bs_ctr_table, one thread per 32 tasks) -- 24 of
+ *     the 160 AES-128 S-boxes and 2 MixColumns rounds disappear;
  *   - the S-box's key-dependent terms (11 words per round byte, see
  *     sbox_key_terms) come from a per-call table written by k_bs_key_table
  *     and read with scalar loads next to each S-box: no SALU mask arithmetic
  *     and no round-key SGPRs live across the kernel;
- *   - MixColumns in the 80-op low-register form (mix_column_t) and the
- *     S-box statements in minimum-live-plane order (tools/sbox_schedule.py);
+ *   - an 83-LUT3 S-box (tools/sbox_lut3.py: ILP cover after re-synthesising
+ *     the bottom linear layer) in minimum-live-plane order
+ *     (tools/sbox_schedule.py) and a 55-node MixColumns column
+ *     (tools/mixcol_search.py; the textbook forms take 76-80);
  *   - CTR: the plaintext of the first 8 slots goes straight to LDS by the
  *     DMA path at task start (no VGPRs) and lands while the rounds run; the
  *     other slots are loaded 8 slots ahead of their use in groups of 4;
@@ -56,6 +61,7 @@ struct BsParams {
     uint64_t shift;       /* CTR: ctr0.lo mod 2048 (virtual index = i + shift) */
     Ctr128 cbase;         /* CTR: ctr0 with the low 11 bits cleared */
     const uint32_t *ktab; /* key-term table (key_term_table layout) */
+    const uint32_t *ctab; /* CTR counter-caching tables (OTC_BS_CTR_*), or null */
 };
 
 enum : int { BS_CTR = 0, BS_ECB = 1 };
@@ -238,13 +244,59 @@ struct TableTerms {
  * slower -- its back edge permutes 128 planes and spills), low-register
  * MixColumns, S-box fence level 2 (per-S-box fences: LUT-level pins cost an
  * s_nop per asm boundary). */
-template <int R, int NR>
+/* key terms of the counter-cached rounds 2 (BASE 0, bytes 0..7) and 3
+ * (BASE 8) from the task's group entry */
+template <int BASE>
+struct GroupTerms {
+    ktab_ptr gp;
+    __device__ __forceinline__ void operator()(int b, W *t) const
+    {
+        ktab_ptr q = gp;
+        asm volatile("" : "+s"(q));
+#pragma unroll
+        for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = q[(BASE + b) * OTC_BS_KT_STRIDE + j];
+    }
+};
+
+/* CTR counter-caching tables of one call (otc_bitslice.h, "CTR counter
+ * caching"): threads 0..63 the S15 planes of each lane, 64..95 the S14 planes
+ * of each u5, then one thread per group of 32 tasks.  Group g's counter
+ * prefix is (cbase with bits 0-15 cleared) + g * 2^16, with the same carry
+ * rule as the kernel (128-bit, or 64-bit wrap). */
+__global__ __launch_bounds__(256) void k_bs_ctr_table(otc_aes_key K, Ctr128 cbase, uint32_t wrap64,
+                                                      uint64_t ngroups, uint32_t *ctab)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    auto rkb = [&](int r, int b) -> uint32_t { return (K.rk[4 * r + (b >> 2)] >> (8 * (b & 3))) & 0xFFu; };
+    if (i < 64) {
+        uint32_t kt[OTC_BS_KT_STRIDE];
+        key_terms_of_byte(rkb(0, 15), kt);
+        ctr_s15_planes((uint32_t)i, kt, ctab + i * 8);
+    } else if (i < 96) {
+        uint32_t kt[OTC_BS_KT_STRIDE];
+        key_terms_of_byte(rkb(0, 14), kt);
+        ctr_s14_planes((uint32_t)(i - 64), kt, ctab + OTC_BS_CTR_S14_OFF + (i - 64) * 8);
+    } else if (i - 96 < ngroups) {
+        const uint64_t g = i - 96;
+        const uint64_t base = cbase.lo & ~(uint64_t)0xFFFF;
+        const uint64_t lo = base + (g << 16);
+        const uint64_t hi = cbase.hi + ((!wrap64 && lo < base) ? 1u : 0u);
+        uint8_t pre[14];
+#pragma unroll
+        for (int b = 0; b < 8; ++b) pre[b] = (uint8_t)(hi >> (8 * (7 - b)));
+#pragma unroll
+        for (int b = 0; b < 6; ++b) pre[8 + b] = (uint8_t)(lo >> (8 * (7 - b)));
+        ctr_group_terms(pre, K.rk, ctab + OTC_BS_CTR_GRP_OFF + g * OTC_BS_CTR_GRP_WORDS);
+    }
+}
+
+template <int R, int NR, int MIX>
 __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
 {
     if constexpr (R < NR - 1) {
-        round_step_kt<true, TableTerms<R>, 2>(s, TableTerms<R>{tp});
+        round_step_kt<MIX, TableTerms<R>, 2>(s, TableTerms<R>{tp});
         pin_n(s, 128);
-        rounds_table<R + 1, NR>(s, tp);
+        rounds_table<R + 1, NR, MIX>(s, tp);
     } else {
         round_final_kt(s, TableTerms<NR - 1>{tp});
     }
@@ -257,7 +309,7 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
  * ops cover their latency.  D: the other register slots are loaded D slots
  * ahead of use, in groups of 4, as the keystream of consumed slots frees
  * registers (loading all of them up front spills at 3 waves). */
-template <int NR, int MODE, int LS, int PRE = 4, int D = 8>
+template <int NR, int MODE, int LS, bool CACHE, int MIX = 2, int PRE = 4, int D = 8>
 __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key &K, uint4 *stage)
 {
     Task t;
@@ -282,7 +334,27 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
                                              16, 0, 0);
         }
     }
-    if (MODE == BS_CTR) {
+    if (MODE == BS_CTR && CACHE) {
+        /* counter caching: rounds 1-2 from the per-call / per-group tables */
+        const uint64_t task = t.vbase >> 11;
+        const uint32_t u5 = ((uint32_t)(P.cbase.lo >> 11) + (uint32_t)task) & 31u;
+        const uint64_t g = (((P.cbase.lo >> 11) & 31u) + task) >> 5;
+        const uint4 *q15 = (const uint4 *)(P.ctab + lane * 8u);
+        const uint4 a = q15[0], b = q15[1];
+        const W s15[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        const ktab_ptr s14p = (ktab_ptr)P.ctab + OTC_BS_CTR_S14_OFF + u5 * 8u;
+        W s14[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s14[i] = s14p[i];
+        const ktab_ptr gp = (ktab_ptr)P.ctab + OTC_BS_CTR_GRP_OFF + g * OTC_BS_CTR_GRP_WORDS;
+        ctr_rounds12(s15, s14, GroupTerms<0>{gp}, s);
+        pin_n(s, 128);
+        sched_fence();
+        round_step_kt<MIX, GroupTerms<8>, 2>(s, GroupTerms<8>{gp});
+        pin_n(s, 128);
+        sched_fence();
+        rounds_table<3, NR, MIX>(s, (ktab_ptr)P.ktab);
+    } else if (MODE == BS_CTR) {
         const uint64_t clo = P.cbase.lo + t.vbase;
         const uint64_t chi = P.cbase.hi + ((!P.wrap64 && clo < P.cbase.lo) ? 1u : 0u);
         /* the four counter words as VGPRs, so the 117 uniform counter planes
@@ -313,8 +385,10 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
     } else {
         ecb_load_planes(P, t, s);
     }
-    sched_fence();
-    rounds_table<0, NR>(s, (ktab_ptr)P.ktab);
+    if (!(MODE == BS_CTR && CACHE)) {
+        sched_fence();
+        rounds_table<0, NR, MIX>(s, (ktab_ptr)P.ktab);
+    }
     pin_n(s, 128);
     sched_fence();
 
@@ -347,6 +421,14 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
         sched_fence();
     }
     const uint32_t k0 = K.rk[4 * NR + 0], k1 = K.rk[4 * NR + 1], k2 = K.rk[4 * NR + 2], k3 = K.rk[4 * NR + 3];
+    auto ks_xor = [&](int k, uint4 x) {
+        uint4 o;
+        o.x = x3(x.x, s[k], k0);
+        o.y = x3(x.y, s[32 + k], k1);
+        o.z = x3(x.z, s[64 + k], k2);
+        o.w = x3(x.w, s[96 + k], k3);
+        return o;
+    };
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
         if ((k & 3) == 0) {
@@ -356,16 +438,8 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
                 if ((j - D < 0 ? 0 : ((j - D) & ~3)) == k) issue(j);
         }
         if (slot_ok(k)) {
-            uint4 o;
-            if (MODE == BS_CTR) {
-                const uint4 x = k < LS ? stage[(wave * LS + k) * 64 + (lo >> 4)] : pt[k];
-                o.x = x3(x.x, s[k], k0);
-                o.y = x3(x.y, s[32 + k], k1);
-                o.z = x3(x.z, s[64 + k], k2);
-                o.w = x3(x.w, s[96 + k], k3);
-            } else {
-                o = make_uint4(s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3);
-            }
+            const uint4 o = MODE == BS_CTR ? ks_xor(k, k < LS ? stage[(wave * LS + k) * 64 + (lo >> 4)] : pt[k])
+                                           : make_uint4(s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3);
             *(uint4 *)(ob + lo + 1024u * k) = o;
         }
     }
@@ -375,12 +449,12 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
  * workgroups per CU); ECB loads its whole input before the rounds. */
 constexpr int BS_LS = 8;
 
-template <int NR, int MODE, int LS>
+template <int NR, int MODE, int LS, bool CACHE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_aes_bs_t3(BsParams P,
                                                                                              otc_aes_key K)
 {
     __shared__ uint4 stage[LS > 0 ? 4 * LS * 64 : 1];
-    aes_bs_task<NR, MODE, LS>(P, K, stage);
+    aes_bs_task<NR, MODE, LS, CACHE>(P, K, stage);
 }
 
 template <int NR, int MODE>
@@ -404,15 +478,29 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
         hipLaunchKernelGGL((k_aes_bs_w3<NR, MODE>), g, b, 0, st, P, K);
         return hipGetLastError();
     }
-    /* per-call key-term table, stream-ordered: written by one small kernel,
-     * freed behind the main kernel (the pool recycles it) */
+    /* CTR counter caching (OTC_BS_CTR_NOCACHE=1: off, for A/B runs) */
+    static const bool nocache = getenv("OTC_BS_CTR_NOCACHE") && atoi(getenv("OTC_BS_CTR_NOCACHE")) != 0;
+    const bool cache = MODE == BS_CTR && !nocache;
+    const uint64_t ngroups = cache ? (((P.cbase.lo >> 11) & 31u) + tasks + 31) >> 5 : 0;
+    const size_t kt_words = (size_t)NR * 16 * OTC_BS_KT_STRIDE;
+    const size_t words = kt_words + (cache ? OTC_BS_CTR_GRP_OFF + ngroups * OTC_BS_CTR_GRP_WORDS : 0);
+    /* per-call tables, stream-ordered: written by small kernels, freed behind
+     * the main kernel (the pool recycles the memory) */
     uint32_t *tab = nullptr;
-    hipError_t e = hipMallocAsync((void **)&tab, (size_t)NR * 16 * OTC_BS_KT_STRIDE * 4, st);
+    hipError_t e = hipMallocAsync((void **)&tab, words * 4, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_bs_key_table, dim3(1), dim3(256), 0, st, K, tab);
     BsParams Q = P;
     Q.ktab = tab;
-    hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, (MODE == BS_CTR ? BS_LS : 0)>), g, b, 0, st, Q, K);
+    if (cache) {
+        Q.ctab = tab + kt_words;
+        const uint64_t n = 96 + ngroups;
+        hipLaunchKernelGGL(k_bs_ctr_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, P.cbase, P.wrap64,
+                           ngroups, (uint32_t *)Q.ctab);
+        hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, (MODE == BS_CTR ? BS_LS : 0), true>), g, b, 0, st, Q, K);
+    } else {
+        hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, (MODE == BS_CTR ? BS_LS : 0), false>), g, b, 0, st, Q, K);
+    }
     e = hipGetLastError();
     const hipError_t f = hipFreeAsync(tab, st);
     return e != hipSuccess ? e : f;

@@ -293,6 +293,7 @@ OTC_HD void mix_columns_ark(const W *in, W *out, KF kf)
 
 } /* namespace otc_bs */
 #include "otc_sbox_lut3.h"
+#include "otc_mixcol.h"
 namespace otc_bs {
 
 template <bool CTR_CACHE, int R, class KF>
@@ -357,14 +358,15 @@ OTC_HD void encrypt_round(W *s, KF &kf)
 }
 
 /* One non-final round as a self-contained step: S-box every byte with the
- * round key folded in, ShiftRows by renaming, MixColumns (MIXT: the
- * low-register form), result back in s[] in the canonical layout, in the
+ * round key folded in, ShiftRows by renaming, MixColumns (MIX 0: the d-form
+ * mix_column, 1: the low-register t-form, 2: the searched 55-node circuit
+ * mix_column_g), result back in s[] in the canonical layout, in the
  * streaming column order of encrypt_round.
  *
  * The key comes as S-box key TERMS: kt(b, t) fills the OTC_SBOX_KEY_TERMS
  * values of byte b (sbox_key_terms of its 8 plane masks) -- computed from the
  * round key on the fly (KeyMasks) or read from a precomputed table. */
-template <bool MIXT, class KT, int FENCE = 2>
+template <int MIX, class KT, int FENCE = 2>
 OTC_HD void round_step_kt(W *s, KT kt)
 {
     W ns[128];
@@ -388,7 +390,9 @@ OTC_HD void round_step_kt(W *s, KT kt)
 #pragma unroll
             for (int i = 0; i < 8; ++i) col[8 * r + i] = x[i];
         }
-        if (MIXT)
+        if (MIX == 2)
+            mix_column_g(col, ns + 32 * c);
+        else if (MIX == 1)
             mix_column_t<true>(col, ns + 32 * c);
         else
             mix_column<true>(col, ns + 32 * c);
@@ -432,10 +436,10 @@ struct KeyMasks {
     }
 };
 
-template <bool MIXT, class KF, int FENCE = 2>
+template <int MIX, class KF, int FENCE = 2>
 OTC_HD void round_step(W *s, KF kf)
 {
-    round_step_kt<MIXT, KeyMasks<KF>, FENCE>(s, KeyMasks<KF>{kf});
+    round_step_kt<MIX, KeyMasks<KF>, FENCE>(s, KeyMasks<KF>{kf});
 }
 
 template <class KF>
@@ -460,6 +464,195 @@ OTC_HD void key_term_table(const uint32_t *rk, int nr, uint32_t *tab)
             sbox_key_terms(k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7], t);
             t[OTC_SBOX_KEY_TERMS] = 0;
         }
+}
+
+/* ---- CTR counter caching -----------------------------------------------
+ * The bitsliced CTR kernel (csrc/hip/aes_bs.hip) gives each wave ("task") the
+ * 2048 counters C + 64k + l (slot k < 32, lane l < 64, C = 0 mod 2048).  So
+ * counter byte 15 (bits 0-7) = lane bits 0-5 + slot bits 0-1, byte 14 = slot
+ * bits 2-4 + the task's counter bits 11-15 ("u5"), and bytes 0..13 (bits 16+)
+ * are a prefix shared by a GROUP of 32 consecutive tasks.  Rounds 1 and 2
+ * then split into a per-group constant part, precomputed once per group, and
+ * a small varying part:
+ *   round 1: only S(byte 15) (per lane) and S(byte 14) (wave-uniform) vary --
+ *            both read from a per-call table.  ShiftRows/MixColumns take them
+ *            into columns 0 and 1 as (1,1,3,2)*S15 and (1,3,2,1)*S14 on top of
+ *            a group constant, and that constant becomes the round-2 S-box KEY
+ *            of those 8 bytes;
+ *   round 2: only those 8 S-boxes vary; the other 8 are group constants whose
+ *            MixColumns contribution folds into the round-3 S-box key.
+ * Rounds 1-2 thus cost 8 S-boxes + ~170 XORs instead of 32 S-boxes + 640.
+ * Per group: key terms of the 8 varying round-2 bytes and of all 16 round-3
+ * bytes (OTC_BS_CTR_GRP_WORDS words). */
+#define OTC_BS_CTR_GRP_WORDS (24 * OTC_BS_KT_STRIDE)
+/* per-call part: S15 planes [64 lanes][8], S14 planes [32 u5][8] */
+#define OTC_BS_CTR_S14_OFF (64 * 8)
+#define OTC_BS_CTR_GRP_OFF (64 * 8 + 32 * 8)
+
+/* S-box of one byte value through the bitsliced circuit (table-free, so
+ * the device precompute and the host tests share it) */
+OTC_HD uint32_t sbox_value(uint32_t v)
+{
+    W x[8];
+    for (int i = 0; i < 8; ++i) x[i] = (v >> i) & 1u;
+    sbox(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
+    uint32_t r = 0;
+    for (int i = 0; i < 8; ++i) r |= (x[i] & 1u) << i;
+    return r;
+}
+OTC_HD uint32_t xtime_value(uint32_t a) { return ((a << 1) ^ ((a & 0x80u) ? 0x1Bu : 0u)) & 0xFFu; }
+
+/* MixColumns of one column of byte values a[row] */
+OTC_HD void mix_column_bytes(const uint32_t *a, uint32_t *o)
+{
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t a0 = a[r], a1 = a[(r + 1) & 3], a2 = a[(r + 2) & 3], a3 = a[(r + 3) & 3];
+        o[r] = xtime_value(a0) ^ xtime_value(a1) ^ a1 ^ a2 ^ a3;
+    }
+}
+
+/* ShiftRows + MixColumns of 16 byte values (state byte b = row + 4*col) */
+OTC_HD void shift_mix_bytes(const uint32_t *in, uint32_t *out)
+{
+    for (int c = 0; c < 4; ++c) {
+        uint32_t col[4];
+        for (int r = 0; r < 4; ++r) col[r] = in[r + 4 * ((c + r) & 3)];
+        mix_column_bytes(col, out + 4 * c);
+    }
+}
+
+/* key terms (+ pad word) of one key byte */
+OTC_HD void key_terms_of_byte(uint32_t byte, uint32_t *t)
+{
+    W k[8];
+    for (int i = 0; i < 8; ++i) k[i] = ((byte >> i) & 1u) ? ~0u : 0u;
+    sbox_key_terms(k[0], k[1], k[2], k[3], k[4], k[5], k[6], k[7], t);
+    t[OTC_SBOX_KEY_TERMS] = 0;
+}
+
+/* Group constants: pre[0..13] = counter bytes 0..13 of the group, rk = the
+ * LE round-key words (aes_export_rk32).  out: OTC_BS_CTR_GRP_WORDS words --
+ * terms of round-2 bytes 0..7, then of round-3 bytes 0..15. */
+OTC_HD void ctr_group_terms(const uint8_t *pre, const uint32_t *rk, uint32_t *out)
+{
+    auto rkb = [&](int r, int b) -> uint32_t { return (rk[4 * r + (b >> 2)] >> (8 * (b & 3))) & 0xFFu; };
+    uint32_t a[16], B[16], d[16], Q[16];
+    for (int b = 0; b < 14; ++b) a[b] = sbox_value(pre[b] ^ rkb(0, b));
+    a[14] = a[15] = 0; /* varying: added by the kernel */
+    shift_mix_bytes(a, B);
+    for (int b = 0; b < 8; ++b) key_terms_of_byte(B[b] ^ rkb(1, b), out + b * OTC_BS_KT_STRIDE);
+    for (int b = 0; b < 8; ++b) d[b] = 0; /* varying: the kernel's 8 S-boxes */
+    for (int b = 8; b < 16; ++b) d[b] = sbox_value(B[b] ^ rkb(1, b));
+    shift_mix_bytes(d, Q);
+    for (int b = 0; b < 16; ++b) key_terms_of_byte(Q[b] ^ rkb(2, b), out + (8 + b) * OTC_BS_KT_STRIDE);
+}
+
+/* Round-1 S-box output planes of counter byte 15 in lane `lane` (bits 0-5 =
+ * lane, bits 6-7 = slot pattern) and of byte 14 for task bits u5 (bits 0-2 =
+ * slot pattern, bits 3-7 = u5); kt: the round-0 key terms of that byte. */
+OTC_HD void ctr_s15_planes(uint32_t lane, const uint32_t *kt, W *o)
+{
+    W x[8];
+    for (int i = 0; i < 6; ++i) x[i] = ((lane >> i) & 1u) ? ~0u : 0u;
+    x[6] = 0xAAAAAAAAu;
+    x[7] = 0xCCCCCCCCu;
+    sbox_lut3_c(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kt[0], kt[1], kt[2], kt[3], kt[4], kt[5], kt[6], kt[7],
+                kt[8], kt[9], kt[10]);
+    for (int i = 0; i < 8; ++i) o[i] = x[i];
+}
+OTC_HD void ctr_s14_planes(uint32_t u5, const uint32_t *kt, W *o)
+{
+    W x[8];
+    x[0] = 0xF0F0F0F0u;
+    x[1] = 0xFF00FF00u;
+    x[2] = 0xFFFF0000u;
+    for (int i = 0; i < 5; ++i) x[3 + i] = ((u5 >> i) & 1u) ? ~0u : 0u;
+    sbox_lut3_c(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kt[0], kt[1], kt[2], kt[3], kt[4], kt[5], kt[6], kt[7],
+                kt[8], kt[9], kt[10]);
+    for (int i = 0; i < 8; ++i) o[i] = x[i];
+}
+
+/* xtime on 8 planes */
+OTC_HD void xt8(const W *a, W *o)
+{
+    o[0] = a[7];
+    o[1] = a[0] ^ a[7];
+    o[2] = a[1];
+    o[3] = a[2] ^ a[7];
+    o[4] = a[3] ^ a[7];
+    o[5] = a[4];
+    o[6] = a[5];
+    o[7] = a[6];
+}
+
+/* MixColumns of a column whose only non-zero rows are i (a) and j (b):
+ * out_r = M[r][i] a ^ M[r][j] b, M[r][j] = (2,3,1,1)[(j - r) mod 4]; one
+ * 3-input XOR per output plane for the row pairs that occur here. */
+OTC_HD void mix_column2(const W *a, int i, const W *b, int j, W *out)
+{
+    W a2[8], b2[8];
+    xt8(a, a2);
+    xt8(b, b2);
+    const int cf[4] = {2, 3, 1, 1};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int ca = cf[(i - r) & 3], cb = cf[(j - r) & 3];
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            W v;
+            if (ca == 3 && cb == 3)
+                v = x3(a[p], a2[p], b[p]) ^ b2[p];
+            else if (ca == 3)
+                v = x3(a[p], a2[p], cb == 1 ? b[p] : b2[p]);
+            else if (cb == 3)
+                v = x3(b[p], b2[p], ca == 1 ? a[p] : a2[p]);
+            else
+                v = (ca == 1 ? a[p] : a2[p]) ^ (cb == 1 ? b[p] : b2[p]);
+            out[8 * r + p] = v;
+        }
+    }
+}
+
+/* Rounds 1 and 2 of a counter-cached CTR task: s15/s14 = round-1 S-box
+ * planes (ctr_s15_planes / ctr_s14_planes), kt(b, t) = round-2 key terms of
+ * bytes 0..7 (ctr_group_terms).  Result in s[128]: the round-3 S-box input
+ * WITHOUT its key (that is folded into the group's round-3 terms). */
+template <class KT>
+OTC_HD void ctr_rounds12(const W *s15, const W *s14, KT kt, W *s)
+{
+    /* round-2 S-box inputs: column 0 = (1,1,3,2) S15, column 1 = (1,3,2,1) S14 */
+    W e[8][8];
+    W d15[8], d14[8];
+    xt8(s15, d15);
+    xt8(s14, d14);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        e[0][p] = s15[p];
+        e[1][p] = s15[p];
+        e[2][p] = s15[p] ^ d15[p];
+        e[3][p] = d15[p];
+        e[4][p] = s14[p];
+        e[5][p] = s14[p] ^ d14[p];
+        e[6][p] = d14[p];
+        e[7][p] = s14[p];
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        W t[OTC_SBOX_KEY_TERMS];
+        kt(b, t);
+        W *x = e[b];
+        sbox_lut3_c(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7],
+                    t[8], t[9], t[10]);
+        pin8(x);
+        sched_fence();
+    }
+    /* ShiftRows: column c row r <- byte r + 4((c + r) & 3); the varying bytes
+     * 0..7 land at col0 rows 0,1 (bytes 0,5), col1 rows 0,3 (4,3), col2 rows
+     * 2,3 (2,7), col3 rows 1,2 (1,6) */
+    mix_column2(e[0], 0, e[5], 1, s);
+    mix_column2(e[4], 0, e[3], 3, s + 32);
+    mix_column2(e[2], 2, e[7], 3, s + 64);
+    mix_column2(e[1], 1, e[6], 2, s + 96);
 }
 
 /* Rounds 1..NR of AES on bitsliced planes s[128] (AddRoundKey r folded into

@@ -51,6 +51,31 @@ def test_ctr_counter_carries(gpu, impl, ctr_low):
     assert host(y) == cpu_ref.ctr(key, ctr0, host(x))
 
 
+@pytest.mark.parametrize("bits", KEYBITS)
+@pytest.mark.parametrize("ctr_low", [(1 << 64) - 70000, (1 << 16) - 2048 * 3 - 5, 0xFFFF0000 + 2048 * 17])
+def test_ctr_bitslice_group_boundaries(gpu, bits, ctr_low):
+    """The bitsliced kernel's counter caching precomputes rounds 1-2 per group
+    of 32 tasks (counter bits 16+): many groups, a group straddling the 2^64
+    carry into the high half, and groups starting mid-way."""
+    key = os.urandom(bits // 8)
+    ctr0 = os.urandom(8) + ctr_low.to_bytes(8, "big")
+    x = rnd(16 * 300000 + 5, gpu, 13)
+    y = ops.ctr(x, key, ctr0, impl="bitslice")
+    torch.cuda.synchronize()
+    assert host(y) == cpu_ref.ctr(key, ctr0, host(x))
+
+
+def test_ctr_bitslice_wrap64_many_groups(gpu):
+    """64-bit counter wrap (RFC 3686 layout) across group boundaries."""
+    if not cpu_ref.aesni_supported():
+        pytest.skip("no AES-NI on this host")
+    key, nonce, ivec = os.urandom(16), os.urandom(4), b"\xff" * 4 + b"\xff\xfe\x00\x00"
+    x = rnd(16 * 200000 + 7, gpu, 17)
+    y = ops.ctr_rfc3686(x, key, nonce, ivec, impl="bitslice")
+    torch.cuda.synchronize()
+    assert host(y) == cpu_ref.aesni_ctr(key, nonce, ivec, host(x))
+
+
 @pytest.mark.parametrize("impl", IMPLS)
 def test_ctr_block_offset_and_inplace(gpu, impl):
     key = os.urandom(16)

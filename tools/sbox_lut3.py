@@ -18,6 +18,14 @@ Model
   every gate leaf to be implemented; minimise the number of LUTs.
 * bitop3 immediate: f(0xF0, 0xCC, 0xAA) for f(src0, src1, src2) (verified
   against hipcc's own lowering of (a&b)^c and (a|b)&~c on gfx950).
+* Bottom linear layer re-synthesised: BP's 38 XOR2 gates (L0..L29, S0..S7)
+  compute 8 linear forms of the 18 AND outputs M46..M63; a randomised greedy
+  over XOR2/XOR3 nodes with shared subexpressions (Paar-style, cancellation
+  free) finds a 19-node layer, after which the ILP cover drops from 86 to 83
+  LUTs.  (--bp-bottom keeps the original layer.)
+
+Then run tools/sbox_schedule.py (statement order for the fewest live planes
++ the OTC_LUT_PIN markers).
 """
 import itertools
 import os
@@ -58,9 +66,68 @@ L14 xor M52 M61;L15 xor M55 L1;L16 xor M56 L0;L17 xor M57 L1;L18 xor M58 L8;L19 
 L21 xor L1 L7;L22 xor L3 L12;L23 xor L18 L2;L24 xor L15 L9;L25 xor L6 L10;L26 xor L7 L9;L27 xor L8 L10;
 L28 xor L11 L14;L29 xor L11 L17;S0 xor L6 L24;S1 xnor L16 L26;S2 xnor L19 L28;S3 xor L6 L21;S4 xor L20 L22;
 S5 xor L25 L29;S6 xnor L13 L27;S7 xnor L6 L23"""
+BP_BOTTOM = "--bp-bottom" in sys.argv
+
+
+def linear_form(n, gates, leaves):
+    """S output as (set of leaves, complement) over the XOR/XNOR gates."""
+    if n in leaves:
+        return frozenset([n]), 0
+    op, a, b = gates[n]
+    la, ca = linear_form(a, gates, leaves)
+    lb, cb = linear_form(b, gates, leaves)
+    return la ^ lb, ca ^ cb ^ (1 if op == "xnor" else 0)
+
+
+def bottom_greedy(forms, seed):
+    """XOR2/XOR3 circuit for the linear forms; returns (nodes, remaining terms)."""
+    import random
+    rnd = random.Random(seed)
+    cost = lambda k: 0 if k <= 1 else k // 2
+    ts = [set(f) for f in forms]
+    prog = []
+    while True:
+        cnt = {}
+        for t in ts:
+            for size in (2, 3):
+                for c in itertools.combinations(sorted(t), size):
+                    cnt.setdefault(c, []).append(t)
+        best, bs = None, 0.0
+        for c, tt in cnt.items():
+            sc = sum(cost(len(t)) - cost(len(t) - (len(c) - 1)) for t in tt) - 1 + 0.5 * rnd.random()
+            if sc > bs:
+                best, bs = c, sc
+        if best is None or bs <= 0.5:
+            break
+        name = f"B{len(prog)}"
+        prog.append((name, best))
+        for t in ts:
+            if all(x in t for x in best):
+                t.difference_update(best)
+                t.add(name)
+    return prog, ts
+
+
+_bp = {}
 for item in M.replace("\n", "").split(";"):
     n, op, a, b = item.split()
-    g(n, op, a, b)
+    if BP_BOTTOM or not (n.startswith("L") or n.startswith("S")):
+        g(n, op, a, b)
+    _bp[n] = (op, a, b)
+if not BP_BOTTOM:
+    leaves = {f"M{i}" for i in range(46, 64)}
+    forms = [linear_form(f"S{j}", _bp, leaves) for j in range(8)]
+    prog, ts = bottom_greedy([f for f, _ in forms], seed=1)
+    for name, c in prog:
+        g(name, "xor", *c)
+    for j, t in enumerate(ts):  # each output: XOR3 chain of its remaining terms
+        lst = sorted(t)
+        cur, rest, k = lst[0], lst[1:], 0
+        while rest:
+            last = len(rest) <= 2
+            name = f"S{j}" if last else f"Q{j}_{k}"
+            g(name, "xnor" if (last and forms[j][1]) else "xor", cur, *rest[:2])
+            cur, rest, k = name, rest[2:], k + 1
 OUTS = [f"S{i}" for i in range(8)]
 GATE = {n: (op, ins) for n, op, ins in G}
 ORDER = [n for n, _, _ in G]
@@ -78,7 +145,9 @@ def ev(n, env, memo):
         for x in v:
             r ^= x
     elif op == "xnor":
-        r = (v[0] ^ v[1]) ^ 1
+        r = 1
+        for x in v:
+            r ^= x
     else:
         r = v[0] & v[1]
     memo[n] = r
@@ -164,12 +233,14 @@ for o in OUTS:
     emit(o)
 
 hdr = f'''/*
- * otc_sbox_lut3.h -- GENERATED by tools/sbox_lut3.py; do not edit.
+ * otc_sbox_lut3.h -- GENERATED by tools/sbox_lut3.py (+ tools/sbox_schedule.py);
+ * do not edit.
  *
- * The Boyar-Peralta AES S-box ({len(G)} gates incl. the key-folded inputs)
- * mapped onto {len(sel)} three-input LUTs = gfx950 v_bitop3_b32 (exact minimum
- * cover by ILP over all 3-feasible cuts, <= 1 SGPR key operand per LUT).
- * Computes S(x ^ k) for plane masks k (0 / ~0).
+ * The Boyar-Peralta AES S-box with the key folded into its inputs and its
+ * bottom linear layer re-synthesised ({len(G)} gates) mapped onto {len(sel)}
+ * three-input LUTs = gfx950 v_bitop3_b32 (exact minimum cover by ILP over all
+ * 3-feasible cuts, <= 1 SGPR key operand per LUT).  Computes S(x ^ k) for
+ * plane masks k (0 / ~0).
  */
 #ifndef OTC_SBOX_LUT3_H
 #define OTC_SBOX_LUT3_H
@@ -190,8 +261,21 @@ static inline W lut3_host(W a, W b, W c, unsigned imm)
 #define lut3(a, b, c, imm) lut3_host((a), (b), (c), (imm))
 #endif
 
+/* OTC_LUT_PIN: pins each LUT output in order when PIN (no instructions;
+ * statement order from tools/sbox_schedule.py, minimum peak of live planes) */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define OTC_LUT_PIN(x) \\
+    if (PIN) asm volatile("" : "+v"(x))
+#else
+#define OTC_LUT_PIN(x) (void)0
+#endif
+
+/* The 11 key terms the LUTs read (K7 = k0 and 10 pairwise XORs of the key
+ * bit masks), in the order of sbox_lut3_c's parameters: also the layout of a
+ * precomputed per-S-box key table (otc_bs::sbox_key_terms). */
 #define OTC_SBOX_KEY_TERMS 11
 
+template <int PIN = 0>
 OTC_HD void sbox_lut3_c(W &x0, W &x1, W &x2, W &x3, W &x4, W &x5, W &x6, W &x7, W K7, W K03, W K05, W K06, W K35,
                         W K46, W K12, W K15, W K25, W K37, W K67)
 {{
@@ -201,10 +285,34 @@ OTC_HD void sbox_lut3_c(W &x0, W &x1, W &x2, W &x3, W &x4, W &x5, W &x6, W &x7, 
     x7 = S0; x6 = S1; x5 = S2; x4 = S3; x3 = S4; x2 = S5; x1 = S6; x0 = S7;
 }
 
-/* (then run tools/sbox_schedule.py: low-pressure statement order, pins, and
- * the sbox_key_terms / sbox_lut3 wrappers over sbox_lut3_c) */
+/* key terms of S(x ^ k) from the 8 plane masks k0..k7 */
+OTC_HD void sbox_key_terms(W k0, W k1, W k2, W k3, W k4, W k5, W k6, W k7, W *t)
+{
+    t[0] = k0;      /* K7  */
+    t[1] = k7 ^ k4; /* K03 */
+    t[2] = k7 ^ k2; /* K05 */
+    t[3] = k7 ^ k1; /* K06 */
+    t[4] = k4 ^ k2; /* K35 */
+    t[5] = k3 ^ k1; /* K46 */
+    t[6] = k6 ^ k5; /* K12 */
+    t[7] = k6 ^ k2; /* K15 */
+    t[8] = k5 ^ k2; /* K25 */
+    t[9] = k4 ^ k0; /* K37 */
+    t[10] = k1 ^ k0; /* K67 */
+}
+
+template <int PIN = 0>
+OTC_HD void sbox_lut3(W &x0, W &x1, W &x2, W &x3, W &x4, W &x5, W &x6, W &x7, W k0, W k1, W k2, W k3, W k4,
+                      W k5, W k6, W k7)
+{
+    W t[OTC_SBOX_KEY_TERMS];
+    sbox_key_terms(k0, k1, k2, k3, k4, k5, k6, k7, t);
+    sbox_lut3_c<PIN>(x0, x1, x2, x3, x4, x5, x6, x7, t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7], t[8], t[9],
+                     t[10]);
+}
 
 #undef lut3
+#undef OTC_LUT_PIN
 } /* namespace otc_bs */
 
 #endif

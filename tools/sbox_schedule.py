@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Register-pressure scheduling of the generated LUT3 S-box.
 
-tools/sbox_lut3.py maps the Boyar-Peralta circuit onto 86 v_bitop3_b32 LUTs
-and emits them in depth-first order (peak 31 live planes incl. the 8 inputs).
+tools/sbox_lut3.py maps the (key-folded, bottom-resynthesised) Boyar-Peralta
+circuit onto 83 v_bitop3_b32 LUTs and emits them in depth-first order.
 Inside the bitsliced kernel every live plane is a VGPR on top of the 120 other
 state planes, and the 3-waves-per-SIMD budget is 168 VGPRs, so the S-box's
 peak matters.  This post-pass re-orders the statements of
@@ -29,9 +29,10 @@ INPUTS = ["U%d" % i for i in range(8)]
 def parse(text):
     lines = text.split("\n")
     stmts, idx = [], []
-    body = next(i for i, l in enumerate(lines) if "void sbox_lut3(" in l)
+    body = next(i for i, l in enumerate(lines) if "void sbox_lut3_c(" in l)
+    end = next(i for i, l in enumerate(lines) if i > body and l.strip().startswith("x7 = S0"))
     for i, l in enumerate(lines):
-        if i <= body:
+        if i <= body or i >= end:
             continue
         m = STMT.match(l)
         if not m or m.group(1).startswith("K") or m.group(1) in INPUTS:
@@ -104,16 +105,7 @@ def main():
     out = lines[:]
     for k, i in enumerate(idx):
         out[i] = new[k]
-    text = "\n".join(out)
-    if "OTC_LUT_PIN(x)" not in text:
-        text = text.replace("OTC_HD void sbox_lut3(", "/* OTC_LUT_PIN: pins each LUT output in order when PIN (no instructions;\n"
-                            " * statement order from tools/sbox_schedule.py, minimum peak of live planes) */\n"
-                            "#if defined(__HIP_DEVICE_COMPILE__)\n"
-                            "#define OTC_LUT_PIN(x) \\\n    if (PIN) asm volatile(\"\" : \"+v\"(x))\n"
-                            "#else\n#define OTC_LUT_PIN(x) (void)0\n#endif\n\n"
-                            "template <int PIN = 0>\nOTC_HD void sbox_lut3(", 1)
-        text = text.replace("#undef lut3\n", "#undef lut3\n#undef OTC_LUT_PIN\n", 1)
-    open(HDR, "w").write(text)
+    open(HDR, "w").write("\n".join(out))
     print(f"peak live planes: {start_peak} -> {best_peak}", file=sys.stderr)
 
 
