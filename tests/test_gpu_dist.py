@@ -76,3 +76,45 @@ def test_rccl_sharded_cbc_decrypt(gpu, rccl_world1):
     pdist.sharded_ctr_(loc, key[:16], ctr0)
     torch.cuda.synchronize()
     assert loc.cpu().numpy().tobytes() == cpu_ref.ctr(key[:16], ctr0, pt)
+
+
+def test_multi_gpu_api_matrix(gpu, rccl_world1, monkeypatch):
+    """One shared matrix over every multi-GPU entry point: the same stream,
+    key and counter/IV through the single-process C++ paths (otc_multi_run
+    direct with 1 and 3 logical shards, otc_multi_run over RCCL,
+    otc_multi_ctr_resident) and the one-process-per-GPU torch.distributed
+    paths (sharded_ctr_, scatter_ctr over several scatter rounds,
+    cbc_decrypt_sharded), against the one-shot device ops and the C oracle.
+    The semantics table is in docs/COMPONENTS.md (2.5)."""
+    import numpy as np
+
+    from our_tree_amd import ops
+    from our_tree_amd.parallel import stream as pstream
+
+    pdist = rccl_world1
+    monkeypatch.setenv("OTC_SHARE_GPUS", "1")
+    key, iv = os.urandom(16), (2**64 - 300).to_bytes(16, "big")  # crosses the 64-bit carry
+    n = (3 << 20) + 16 * 11
+    x = np.random.default_rng(11).integers(0, 256, n, dtype=np.uint8)
+    want = {"ctr": cpu_ref.ctr(key, iv, x.tobytes()), "cbc-dec": cpu_ref.cbc(key, iv, x.tobytes(), decrypt=True)}
+    got = {}
+    for mode in ("ctr", "cbc-dec"):
+        for name, ngpus, strategy in (("direct1", 1, "direct"), ("direct3", 3, "direct"), ("rccl1", 1, "rccl")):
+            y = np.zeros(n, np.uint8)
+            pstream.multi_gpu_run(mode, x, y, key, iv, ngpus=ngpus, strategy=strategy, chunk_bytes=256 << 10)
+            got[(mode, "otc_multi_run/" + name)] = y.tobytes()
+    t = torch.from_numpy(x.copy()).to(gpu)
+    r = t.clone()
+    pstream.multi_ctr_resident([r], key, iv)
+    got[("ctr", "otc_multi_ctr_resident")] = r.cpu().numpy().tobytes()
+    r = t.clone()
+    pdist.sharded_ctr_(r, key, iv)
+    got[("ctr", "dist.sharded_ctr_")] = r.cpu().numpy().tobytes()
+    got[("ctr", "dist.scatter_ctr")] = pdist.scatter_ctr(t, n, key, iv, chunk_per_rank=1 << 20).cpu().numpy().tobytes()
+    got[("cbc-dec", "dist.cbc_decrypt_sharded")] = pdist.cbc_decrypt_sharded(t, key, iv).cpu().numpy().tobytes()
+    got[("ctr", "ops.ctr")] = ops.ctr(t, key, iv).cpu().numpy().tobytes()
+    got[("cbc-dec", "ops.cbc_decrypt")] = ops.cbc_decrypt(t, key, iv).cpu().numpy().tobytes()
+    torch.cuda.synchronize()
+    bad = [k for k, v in got.items() if v != want[k[0]]]
+    assert not bad, bad
+    assert len(got) == 12
