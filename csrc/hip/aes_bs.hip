@@ -480,14 +480,24 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     }
     /* CTR counter caching (OTC_BS_CTR_NOCACHE=1: off, for A/B runs) */
     static const bool nocache = getenv("OTC_BS_CTR_NOCACHE") && atoi(getenv("OTC_BS_CTR_NOCACHE")) != 0;
-    const bool cache = MODE == BS_CTR && !nocache;
+    bool cache = MODE == BS_CTR && !nocache;
     const uint64_t ngroups = cache ? (((P.cbase.lo >> 11) & 31u) + tasks + 31) >> 5 : 0;
     const size_t kt_words = (size_t)NR * 16 * OTC_BS_KT_STRIDE;
-    const size_t words = kt_words + (cache ? OTC_BS_CTR_GRP_OFF + ngroups * OTC_BS_CTR_GRP_WORDS : 0);
     /* per-call tables, stream-ordered: written by small kernels, freed behind
-     * the main kernel (the pool recycles the memory) */
+     * the main kernel (the pool recycles the memory).  The group table is
+     * ~3.4e-5 of the data; if even that does not fit beside a near-full HBM,
+     * CTR runs without counter caching rather than failing. */
     uint32_t *tab = nullptr;
-    hipError_t e = hipMallocAsync((void **)&tab, words * 4, st);
+    hipError_t e = hipErrorOutOfMemory;
+    if (cache) {
+        e = alloc_fault() ? hipErrorOutOfMemory
+                          : hipMallocAsync((void **)&tab, (kt_words + OTC_BS_CTR_GRP_OFF + ngroups * OTC_BS_CTR_GRP_WORDS) * 4, st);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            cache = false;
+        }
+    }
+    if (!cache) e = alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&tab, kt_words * 4, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_bs_key_table, dim3(1), dim3(256), 0, st, K, tab);
     BsParams Q = P;

@@ -109,6 +109,20 @@ int check_key(const otc_aes_key *k, int dir)
 
 } // namespace otc_rt
 
+namespace otc_dev {
+namespace {
+std::atomic<long> g_fault_alloc{-1};
+}
+bool alloc_fault()
+{
+    /* armed with n >= 0: allocations n+1 from now fail once, then disarm */
+    return g_fault_alloc.load(std::memory_order_relaxed) >= 0 &&
+           g_fault_alloc.fetch_sub(1, std::memory_order_relaxed) == 0;
+}
+} // namespace otc_dev
+
+extern "C" void otc_fault_inject_alloc(long after) { otc_dev::g_fault_alloc.store(after < 0 ? -1 : after); }
+
 using namespace otc_rt;
 
 namespace {
@@ -685,7 +699,7 @@ extern "C" int otc_device_sync(void)
 extern "C" void *otc_dev_malloc(size_t nbytes)
 {
     void *p = nullptr;
-    hipError_t e = hipMalloc(&p, nbytes ? nbytes : 16);
+    hipError_t e = dev_alloc(&p, nbytes ? nbytes : 16);
     if (e != hipSuccess) {
         hip_fail(e, "hipMalloc");
         return nullptr;

@@ -36,6 +36,13 @@ struct Range {
     Range &operator=(const Range &) = delete;
 };
 
+/* hipMalloc behind the fault-injection hook */
+inline hipError_t dev_alloc(void **p, size_t n)
+{
+    if (otc_dev::alloc_fault()) return hipErrorOutOfMemory;
+    return hipMalloc(p, n);
+}
+
 /* releases the hybrid-CTR auxiliary stream pool (engine.cpp) */
 void aux_release_all();
 

@@ -103,6 +103,11 @@ __device__ __forceinline__ void ctr_words(const Ctr128 &c, uint64_t idx, bool wr
     w3 = bswap32((uint32_t)lo);
 }
 
+/* Allocation fault injection, a test hook (otc_fault_inject_alloc): true
+ * when the runtime allocation about to be made should fail.  One atomic
+ * countdown; off (no cost beyond a relaxed load) unless armed. */
+bool alloc_fault();
+
 /* Host: CU count of the calling thread's current device, cached per device.
  * Thread-safe (the multi-GPU paths launch from one host thread per GPU): the
  * attribute is immutable, so a relaxed atomic cache is enough. */

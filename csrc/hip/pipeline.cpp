@@ -63,7 +63,7 @@ struct PinnedBuf {
 
 hipError_t pinned_alloc(PinnedBuf &b, size_t n, int node)
 {
-    b.p = otc_numa_alloc(n, node);
+    b.p = otc_dev::alloc_fault() ? nullptr : otc_numa_alloc(n, node);
     if (!b.p) return hipErrorOutOfMemory;
     b.n = n;
     hipError_t e = hipHostRegister(b.p, n, hipHostRegisterDefault);
@@ -197,7 +197,7 @@ extern "C" otc_engine *otc_engine_create(int device, size_t chunk_bytes, int dep
     e->h_out.assign(depth, PinnedBuf{});
     for (auto *v : {&e->ev_h2d0, &e->ev_h2d, &e->ev_k0, &e->ev_k, &e->ev_d2h0, &e->ev_d2h}) v->assign(depth, nullptr);
     for (int i = 0; ok && i < depth; ++i) {
-        ok = hipMalloc(&e->d_in[i], chunk_bytes) == hipSuccess && hipMalloc(&e->d_out[i], chunk_bytes) == hipSuccess;
+        ok = dev_alloc(&e->d_in[i], chunk_bytes) == hipSuccess && dev_alloc(&e->d_out[i], chunk_bytes) == hipSuccess;
         for (auto *v : {&e->ev_h2d0, &e->ev_h2d, &e->ev_k0, &e->ev_k, &e->ev_d2h0, &e->ev_d2h})
             ok = ok && hipEventCreate(&(*v)[i]) == hipSuccess;
     }
@@ -457,8 +457,8 @@ static int rccl_job_init(RcclJob &J, int ngpus, size_t S)
         HIPCHK(hipSetDevice(g));
         for (hipStream_t *s : {&J.sc[g], &J.kst[g], &J.ga[g]}) HIPCHK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
         for (int b = 0; b < 2; ++b) {
-            HIPCHK(hipMalloc(&J.pin[b][g], S));
-            HIPCHK(hipMalloc(&J.pout[b][g], S));
+            HIPCHK(dev_alloc(&J.pin[b][g], S));
+            HIPCHK(dev_alloc(&J.pout[b][g], S));
             for (hipEvent_t *ev : {&J.ev_sc[b][g], &J.ev_k[b][g], &J.ev_ga[b][g]})
                 HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
         }
@@ -467,8 +467,8 @@ static int rccl_job_init(RcclJob &J, int ngpus, size_t S)
     HIPCHK(hipStreamCreateWithFlags(&J.h2d, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&J.d2h, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
-        HIPCHK(hipMalloc(&J.root_in[i], round));
-        HIPCHK(hipMalloc(&J.root_out[i], round));
+        HIPCHK(dev_alloc(&J.root_in[i], round));
+        HIPCHK(dev_alloc(&J.root_out[i], round));
         for (hipEvent_t *ev : {&J.ev_in[i], &J.ev_drained[i]}) HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
     }
     return OTC_OK;

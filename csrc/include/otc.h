@@ -297,6 +297,11 @@ void otc_multi_release(void);
 /* otc_multi_release + the pooled auxiliary streams of the hybrid CTR path. */
 void otc_release_resources(void);
 
+/* Test hook: make the (after+1)-th runtime allocation from now fail once
+ * (device buffers, NUMA-pinned host windows, per-call kernel tables), so the
+ * error paths can be exercised on a healthy GPU; after < 0 disarms. */
+void otc_fault_inject_alloc(long after);
+
 /* Device-resident multi-GPU CTR: buffers dev_bufs[g] (already on GPU g) hold
  * shard g of `shard_bytes`; all GPUs encrypt in place concurrently with the
  * right counter offsets.  Returns elapsed ms (wall, all GPUs). */

@@ -179,6 +179,7 @@ def _declare_gpu(lib):
         "otc_AES_CTR_encrypt": (c_int, [c_vp, c_vp, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int, c_vp]),
         "otc_multi_release": (None, []),
         "otc_release_resources": (None, []),
+        "otc_fault_inject_alloc": (None, [ctypes.c_long]),
         "otc_device_numa_node": (c_int, [c_int]),
         "otc_engine_numa_node": (c_int, [c_vp]),
         "otc_engine_staging": (c_vp, [c_vp, c_int]),

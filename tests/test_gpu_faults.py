@@ -1,0 +1,100 @@
+"""Allocation-failure injection on a healthy GPU ("Failure
+detection / fault injection"): ``otc_fault_inject_alloc(n)`` makes the
+(n+1)-th runtime allocation from now fail once -- device chunk buffers,
+NUMA-pinned host windows, RCCL job buffers, the bitsliced kernel's per-call
+tables.  Every entry point must then fail cleanly with an error (or, for the
+bitsliced CTR tables, fall back to the uncached kernel with identical output),
+release what it had built, and work again on the next call."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from our_tree_amd import _native, ops
+from our_tree_amd.models import cpu_ref
+from our_tree_amd.parallel import stream as pstream
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def inject(gpu):
+    lib = _native.require_gpu_lib()
+    yield lib.otc_fault_inject_alloc
+    lib.otc_fault_inject_alloc(-1)
+
+
+def _rnd(n, seed):
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
+
+
+def test_engine_create_and_run_under_alloc_faults(inject):
+    key, ctr = os.urandom(16), os.urandom(16)
+    x = _rnd((3 << 20) + 5, 1)
+    ref = cpu_ref.ctr(key, ctr, x.tobytes())
+    failed = 0
+    for k in range(12):
+        inject(k)
+        try:
+            with pstream.StreamEngine(0, chunk_bytes=1 << 20, depth=3) as eng:
+                y = np.zeros_like(x)
+                eng.run("ctr", x, y, key, ctr)
+                assert y.tobytes() == ref  # the fault landed after this call's allocations
+        except RuntimeError as e:
+            failed += 1
+            assert "otc_engine" in str(e)
+        finally:
+            inject(-1)
+    assert failed >= 6  # 3 x (d_in, d_out) device buffers at least
+    with pstream.StreamEngine(0, chunk_bytes=1 << 20, depth=3) as eng:
+        y = np.zeros_like(x)
+        eng.run("ctr", x, y, key, ctr)
+    assert y.tobytes() == ref
+
+
+def test_multi_rccl_job_under_alloc_faults(inject):
+    key, iv = os.urandom(32), os.urandom(16)
+    x = _rnd((2 << 20) + 48, 2)
+    ref = cpu_ref.cbc(key, iv, x.tobytes(), decrypt=True)
+    failed = 0
+    for k in range(8):
+        inject(k)
+        try:
+            y = np.zeros_like(x)
+            pstream.multi_gpu_run("cbc-dec", x, y, key, iv, ngpus=1, strategy="rccl", chunk_bytes=256 << 10)
+            assert y.tobytes() == ref
+        except RuntimeError as e:
+            failed += 1
+            assert "otc_multi_run" in str(e)
+        finally:
+            inject(-1)
+        _native.require_gpu_lib().otc_release_resources()  # next attempt builds the job afresh
+    assert failed >= 4  # 2 x (pin, pout) + 2 x (root_in, root_out)
+    y = np.zeros_like(x)
+    pstream.multi_gpu_run("cbc-dec", x, y, key, iv, ngpus=1, strategy="rccl", chunk_bytes=256 << 10)
+    assert y.tobytes() == ref
+
+
+@pytest.mark.parametrize("bits", [128, 256])
+def test_bitslice_ctr_falls_back_without_group_table(inject, gpu, bits):
+    """No room for the counter-caching tables: the uncached kernel runs."""
+    key, ctr = os.urandom(bits // 8), os.urandom(8) + (2**64 - 50000).to_bytes(8, "big")
+    x = torch.from_numpy(_rnd(16 * 100000 + 3, 3)).to(gpu)
+    inject(0)
+    y = ops.ctr(x, key, ctr, impl="bitslice")
+    torch.cuda.synchronize()
+    assert y.cpu().numpy().tobytes() == cpu_ref.ctr(key, ctr, x.cpu().numpy().tobytes())
+
+
+def test_bitslice_ecb_table_failure_is_an_error(inject, gpu):
+    key = os.urandom(16)
+    x = torch.from_numpy(_rnd(16 * 4096, 4)).to(gpu)
+    inject(0)
+    with pytest.raises(RuntimeError):
+        ops.ecb_encrypt(x, key, impl="bitslice")
+        torch.cuda.synchronize()
+    inject(-1)
+    y = ops.ecb_encrypt(x, key, impl="bitslice")
+    torch.cuda.synchronize()
+    assert y.cpu().numpy().tobytes() == cpu_ref.ecb(key, x.cpu().numpy().tobytes())
