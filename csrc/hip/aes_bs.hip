@@ -43,6 +43,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "otc_bitslice.h"
 #include "otc_device.h"
@@ -62,7 +63,17 @@ struct BsParams {
     Ctr128 cbase;         /* CTR: ctr0 with the low 11 bits cleared */
     const uint32_t *ktab; /* key-term table (key_term_table layout) */
     const uint32_t *ctab; /* CTR counter-caching tables (OTC_BS_CTR_*), or null */
+    uint64_t tasks;       /* 2048-block tasks of the call */
+    uint32_t part;        /* BS_ALL, BS_FULL_ONLY or BS_EDGE_ONLY */
 };
+
+/* Which tasks a launch runs.  The bulk launch (BS_FULL_ONLY) takes only tasks
+ * whose 2048 slots are all in range and is compiled knowing it: its load and
+ * store phases are single basic blocks, where hipcc's waitcnt pass keeps
+ * precise vmcnt(N) counts -- per-slot range branches made it fall back to
+ * vmcnt(0) around nearly every slot.  A one-workgroup launch (BS_EDGE_ONLY)
+ * runs the first and the last task (wave 0 / wave 1) if they are partial. */
+enum : uint32_t { BS_ALL = 0, BS_FULL_ONLY = 1, BS_EDGE_ONLY = 2 };
 
 enum : int { BS_CTR = 0, BS_ECB = 1 };
 
@@ -85,16 +96,23 @@ __device__ __forceinline__ bool task_of(const BsParams &P, Task &t)
      * hoist loop-invariant plane/mask values out of it, which costs more
      * registers than the 128-plane state leaves.  Full blocks only; the host
      * routes a trailing partial CTR block to the T-table kernel. */
-    t.vbase = ((uint64_t)blockIdx.x * 4u + t.wave) * 2048u;
+    uint64_t task = (uint64_t)blockIdx.x * 4u + t.wave;
+    if (P.part == BS_EDGE_ONLY) {
+        if (t.wave > 1 || (t.wave == 1 && P.tasks < 2)) return false;
+        task = t.wave == 0 ? 0 : P.tasks - 1;
+    }
+    t.vbase = task * 2048u;
     if (t.vbase >= P.nblocks + shift) return false;
     t.full = t.vbase >= shift && t.vbase + 2048u - shift <= P.nblocks;
+    if (P.part == BS_FULL_ONLY && !t.full) return false;
+    if (P.part == BS_EDGE_ONLY && t.full) return false;
     return true;
 }
 
 /* ECB input: load 32 blocks (uniform task base + 32-bit lane offsets: 64-bit
  * per-slot addresses would be CSE'd with the stores and kept live across the
  * rounds) and transpose each word column into 32 planes */
-__device__ __forceinline__ void ecb_load_planes(const BsParams &P, const Task &t, W *s)
+__device__ __forceinline__ void ecb_load_planes(const BsParams &P, const Task &t, W *s, bool full)
 {
     const uint8_t *tb = P.in + t.vbase * 16;
     const uint32_t lo = t.lane * 16u;
@@ -102,7 +120,7 @@ __device__ __forceinline__ void ecb_load_planes(const BsParams &P, const Task &t
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
         const uint64_t i = t.vbase + t.lane + 64u * k;
-        blk[k] = (t.full || i < P.nblocks) ? *(const uint4 *)(tb + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
+        blk[k] = (full || i < P.nblocks) ? *(const uint4 *)(tb + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -151,7 +169,7 @@ __device__ __forceinline__ void aes_bs_task_legacy(const BsParams &P, const otc_
             }
         }
     } else {
-        ecb_load_planes(P, t, s);
+        ecb_load_planes(P, t, s, t.full);
     }
     sched_fence();
     /* round keys laundered through an empty asm so hipcc materialises each
@@ -309,15 +327,20 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
  * ops cover their latency.  D: the other register slots are loaded D slots
  * ahead of use, in groups of 4, as the keystream of consumed slots frees
  * registers (loading all of them up front spills at 3 waves). */
-template <int NR, int MODE, int LS, bool CACHE, int MIX = 2, int PRE = 4, int D = 8>
+template <int NR, int MODE, int LS, bool CACHE, bool FO, bool LATE = true, int MIX = 2, int PRE = 4, int D = 8>
 __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key &K, uint4 *stage)
 {
     Task t;
     if (!task_of<MODE>(P, t)) return;
     const uint32_t lane = t.lane, wave = t.wave;
     const uint64_t shift = (MODE == BS_CTR) ? P.shift : 0;
-    const bool full = t.full;
+    const bool full = FO || t.full; /* FO: a BS_FULL_ONLY launch */
     W s[128];
+    /* LATE (counter caching): issued after rounds 1-2 have consumed the
+     * per-lane table loads -- vmcnt retires in order and hipcc waits for a
+     * vector load queued behind LDS DMA with vmcnt(0), so a DMA issued first
+     * put its whole latency in front of every task's round 1 */
+    auto prefetch = [&]() {
     if (MODE == BS_CTR && LS > 0) {
         /* branch-free (a per-slot branch splits the kernel's one basic block
          * and costs registers): lanes outside the buffer load block 0 instead,
@@ -334,6 +357,8 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
                                              16, 0, 0);
         }
     }
+    };
+    if (!(MODE == BS_CTR && CACHE && LATE)) prefetch();
     if (MODE == BS_CTR && CACHE) {
         /* counter caching: rounds 1-2 from the per-call / per-group tables */
         const uint64_t task = t.vbase >> 11;
@@ -350,6 +375,10 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
         ctr_rounds12(s15, s14, GroupTerms<0>{gp}, s);
         pin_n(s, 128);
         sched_fence();
+        if (LATE) {
+            prefetch();
+            sched_fence();
+        }
         round_step_kt<MIX, GroupTerms<8>, 2>(s, GroupTerms<8>{gp});
         pin_n(s, 128);
         sched_fence();
@@ -383,7 +412,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
 #pragma unroll
         for (int q = 0; q < 128; ++q) asm volatile("" : "+v"(s[q]));
     } else {
-        ecb_load_planes(P, t, s);
+        ecb_load_planes(P, t, s, full);
     }
     if (!(MODE == BS_CTR && CACHE)) {
         sched_fence();
@@ -449,12 +478,12 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
  * workgroups per CU); ECB loads its whole input before the rounds. */
 constexpr int BS_LS = 8;
 
-template <int NR, int MODE, int LS, bool CACHE>
+template <int NR, int MODE, int LS, bool CACHE, bool FO, bool LATE = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_aes_bs_t3(BsParams P,
                                                                                              otc_aes_key K)
 {
     __shared__ uint4 stage[LS > 0 ? 4 * LS * 64 : 1];
-    aes_bs_task<NR, MODE, LS, CACHE>(P, K, stage);
+    aes_bs_task<NR, MODE, LS, CACHE, FO, LATE>(P, K, stage);
 }
 
 template <int NR, int MODE>
@@ -502,14 +531,42 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     hipLaunchKernelGGL(k_bs_key_table, dim3(1), dim3(256), 0, st, K, tab);
     BsParams Q = P;
     Q.ktab = tab;
+    Q.tasks = tasks;
+    constexpr int LS = MODE == BS_CTR ? BS_LS : 0;
+    /* Split (bulk BS_FULL_ONLY launch + edge launch) or one launch with
+     * runtime range checks: ECB +5% split (1240 vs 1178 GB/s, 4 GiB), CTR
+     * -0.8% (its plaintext loads are mostly DMA'd, and the clock it holds
+     * decides), so the default is per mode; OTC_BS_SPLIT=0|1 overrides.
+     * OTC_BS_DMA_EARLY=1: plaintext DMA before the table loads (A/B, -1%). */
+    static const int split_env = getenv("OTC_BS_SPLIT") ? atoi(getenv("OTC_BS_SPLIT")) : -1;
+    const bool onepass = split_env < 0 ? MODE == BS_CTR : split_env == 0;
+    static const bool early = getenv("OTC_BS_DMA_EARLY") && atoi(getenv("OTC_BS_DMA_EARLY")) != 0;
+    const bool edge = (MODE == BS_CTR && P.shift != 0) || vt % 2048 != 0;
+    auto run = [&](auto cachec, auto latec) {
+        constexpr bool C = decltype(cachec)::value, L = decltype(latec)::value;
+        if (onepass) {
+            Q.part = BS_ALL;
+            hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, false, L>), g, b, 0, st, Q, K);
+            return;
+        }
+        Q.part = BS_FULL_ONLY;
+        hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, true, L>), g, b, 0, st, Q, K);
+        if (edge) {
+            Q.part = BS_EDGE_ONLY;
+            hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, false, L>), dim3(1), b, 0, st, Q, K);
+        }
+    };
     if (cache) {
         Q.ctab = tab + kt_words;
         const uint64_t n = 96 + ngroups;
         hipLaunchKernelGGL(k_bs_ctr_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, P.cbase, P.wrap64,
                            ngroups, (uint32_t *)Q.ctab);
-        hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, (MODE == BS_CTR ? BS_LS : 0), true>), g, b, 0, st, Q, K);
+        if (early)
+            run(std::true_type{}, std::false_type{});
+        else
+            run(std::true_type{}, std::true_type{});
     } else {
-        hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, (MODE == BS_CTR ? BS_LS : 0), false>), g, b, 0, st, Q, K);
+        run(std::false_type{}, std::true_type{});
     }
     e = hipGetLastError();
     const hipError_t f = hipFreeAsync(tab, st);

@@ -399,3 +399,46 @@ def test_aesni_shaped_device_api(gpu, bits):
     z = torch.empty_like(x)
     assert lib.otc_AES_ECB_decrypt(y.data_ptr(), z.data_ptr(), n, u8(ds), nr, st) == 0
     assert torch.equal(z, x)
+
+
+_SPLIT_CHILD = r"""
+import os, sys
+import torch
+from our_tree_amd import ops
+from our_tree_amd.models import cpu_ref
+dev = torch.device("cuda:0")
+g = torch.Generator().manual_seed(5)
+bad = []
+for bits in (128, 256):
+    for n, low in ((16 * 2048 * 9 + 16 * 77 + 3, 1000), (16 * 2048 * 2, 0), (16 * 100, 2040), (16 * 2048 * 40 + 16, 5)):
+        key = os.urandom(bits // 8)
+        ctr0 = os.urandom(8) + low.to_bytes(8, "big")
+        x = torch.randint(0, 256, (n,), dtype=torch.uint8, generator=g).to(dev)
+        y = ops.ctr(x, key, ctr0, impl="bitslice")
+        torch.cuda.synchronize()
+        if y.cpu().numpy().tobytes() != cpu_ref.ctr(key, ctr0, x.cpu().numpy().tobytes()):
+            bad.append(("ctr", bits, n, low))
+        m = n & ~15
+        e = ops.ecb_encrypt(x[:m], key, impl="bitslice")
+        torch.cuda.synchronize()
+        if e.cpu().numpy().tobytes() != cpu_ref.ecb(key, x[:m].cpu().numpy().tobytes()):
+            bad.append(("ecb", bits, m))
+print("BAD", bad)
+sys.exit(1 if bad else 0)
+"""
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_bitslice_split_and_onepass_launches(gpu, split):
+    """Both launch structures of the bitsliced kernels (OTC_BS_SPLIT: bulk
+    full-task launch + one-workgroup edge launch, or one launch with range
+    checks; the default picks one per mode) on shapes with a partial first
+    task, a partial last task, both, a single partial task and none.  The knob
+    is read once per process, so each structure runs in a child process."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OTC_BS_SPLIT=split, PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", _SPLIT_CHILD], env=env, cwd=root, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
