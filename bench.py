@@ -67,6 +67,14 @@ def main():
     from our_tree_amd.parallel import dist as pdist
     from our_tree_amd.utils import device as dinfo
 
+    # The clock probe's stream is created before RCCL creates its streams: a
+    # later one shared a hardware queue with the compute stream (4 per process
+    # here), so the probe ran after the steps and read the idle clock (2.4 GHz
+    # instead of the ~2.0 held under load).
+    gpu = pdist.local_gpu()
+    torch.cuda.set_device(gpu)
+    probe_stream = torch.cuda.Stream(device=gpu, priority=-1)
+
     # a process group even at N=1 (a 1-rank RCCL group) so the scatter pass
     # always runs the collective code path
     rank, world, local = pdist.init_from_env(force=not args.no_scatter)
@@ -136,7 +144,7 @@ def main():
     if not args.no_clock:
         n_clk = max(3, int(0.3 / max(ms_per_step * 1e-3, 1e-6)) + 1)
         window = 0.6 * n_clk * ms_per_step * 1e-3
-        probe = ops.clock_probe(0.2 * n_clk * ms_per_step * 1e-3, window, device=dev)
+        probe = ops.clock_probe(0.2 * n_clk * ms_per_step * 1e-3, window, device=dev, stream=probe_stream)
         for _ in range(n_clk):
             step()
         torch.cuda.synchronize()

@@ -27,6 +27,22 @@ from ..models import cpu_ref
 from . import shard as sh
 
 
+def local_gpu() -> int:
+    """The GPU this rank drives: LOCAL_RANK, or LOCAL_RANK mod the visible
+    device count under OTC_SHARE_GPUS=1 (rehearsals with more ranks than
+    GPUs).  Needs no process group, so callers can bind the device and create
+    streams before RCCL creates its own."""
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        return local
+    n = torch.cuda.device_count()
+    if local >= n:
+        if os.environ.get("OTC_SHARE_GPUS") != "1":
+            raise RuntimeError(f"LOCAL_RANK {local} but only {n} GPU(s) visible (OTC_SHARE_GPUS=1 to share)")
+        return local % n
+    return local
+
+
 def init_from_env(backend: str | None = None, force: bool = False):
     """Initialise the default process group from torchrun's env and bind the
     rank to its GPU.  Returns (rank, world, gpu): gpu = LOCAL_RANK (one
@@ -41,15 +57,9 @@ def init_from_env(backend: str | None = None, force: bool = False):
     port)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = backend or os.environ.get("OTC_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
-    gpu = local
+    gpu = local_gpu()
     if torch.cuda.is_available():
-        n = torch.cuda.device_count()
-        if local >= n:
-            if os.environ.get("OTC_SHARE_GPUS") != "1":
-                raise RuntimeError(f"LOCAL_RANK {local} but only {n} GPU(s) visible (OTC_SHARE_GPUS=1 to share)")
-            gpu = local % n
         torch.cuda.set_device(gpu)
     force = force or os.environ.get("OTC_DIST_FORCE") == "1"  # a 1-rank group too (exercises the RCCL path)
     if (world > 1 or force) and not dist.is_initialized():

@@ -11,6 +11,9 @@
 #   kt NAME -- CMD...   rocprofv3 kernel trace + stats of CMD, summarised to gpurun_out/NAME/kernels.txt
 #   pmc NAME "COUNTERS" -- CMD...   one counter pass (<= 8 SQ, 4 TCC, ...) of CMD, CSV in gpurun_out/NAME
 #   otbench [otbench args]          bin/otbench JSON lines
+#   ab "name:ENV=V,ENV2=V name2:..." [otbench args]
+#                       A/B: the otbench run once per variant (env knobs), 2 reps
+#                       interleaved, lines prefixed with the variant name
 #   cmd -- CMD...       anything else, under a time limit
 #
 # Every GPU step runs under its own `timeout -k 10`, steps are chained with &&
@@ -74,6 +77,13 @@ pmc)
 otbench)
     timeout -k 10 600 ./bin/otbench "$@" > $OUT/otbench.jsonl 2> $OUT/otbench.err || { tail -20 $OUT/otbench.err; exit 1; }
     cat $OUT/otbench.jsonl
+    ;;
+ab)
+    variants=$1; shift
+    for rep in 1 2; do for v in $variants; do
+        name=${v%%:*}; envs=${v#*:}
+        env ${envs//,/ } timeout -k 10 300 ./bin/otbench "$@" | sed "s/^/$name /" | tee -a $OUT/ab.txt || exit 1
+    done; done
     ;;
 cmd)
     [ "$1" = "--" ] && shift
