@@ -62,6 +62,16 @@ def main():
 
     launch.dispatch(args.gpus, os.path.abspath(__file__), sys.argv[1:])
 
+    # stdout carries exactly one JSON line (rank 0): everything else written
+    # to fd 1 from here on -- RCCL's version banner, library chatter -- goes
+    # to stderr, and the result is written to the saved descriptor
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
+
+    def emit(obj):
+        os.write(result_fd, (json.dumps(obj) + "\n").encode())
+
     from our_tree_amd import ops
     from our_tree_amd.models import cpu_ref
     from our_tree_amd.parallel import dist as pdist
@@ -107,7 +117,7 @@ def main():
     ok_all = pdist.allreduce_max(0.0 if ok else 1.0) == 0.0
     if not ok_all:
         if rank == 0:
-            print(json.dumps({"error": "verification failed"}))
+            emit({"error": "verification failed"})
         sys.exit(1)
 
     def step(k=key, impl=args.impl):
@@ -210,7 +220,7 @@ def main():
             "verified_sample": True,
             **extra,
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     if torch.distributed.is_initialized():
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

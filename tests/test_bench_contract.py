@@ -34,8 +34,9 @@ def test_bench_json_line(gpu):
                         "--scatter-mib", "64", "--scatter-rounds", "2"],
                        capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
+    # stdout is the one JSON line and nothing else (RCCL's banner goes to stderr)
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
     d = json.loads(lines[0])
     for k in REQUIRED:
         assert k in d, k
