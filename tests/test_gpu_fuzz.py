@@ -38,13 +38,13 @@ def _buf(dev, n, shift, seed):
 @FUZZ
 @given(bits=st.sampled_from([128, 192, 256]), n=LENGTHS, shift=st.integers(0, 15), inplace=st.booleans(),
        high=st.sampled_from([0, 2**64 - 3, 2**64 - 70000, 2**128 - 2]), off=st.integers(0, 1 << 20),
-       seed=st.integers(0, 2**31))
-def test_ctr_fuzz(gpu, bits, n, shift, inplace, high, off, seed):
+       seed=st.integers(0, 2**31), impl=st.sampled_from(["auto", "bitslice"]))
+def test_ctr_fuzz(gpu, bits, n, shift, inplace, high, off, seed, impl):
     key = os.urandom(bits // 8)
     ctr0 = ((high + seed) % 2**128).to_bytes(16, "big")
     x = _buf(gpu, n, shift, seed)
     src = host(x)
-    y = ops.ctr(x, key, ctr0, out=x if inplace else None, block_offset=off)
+    y = ops.ctr(x, key, ctr0, out=x if inplace else None, block_offset=off, impl=impl)
     torch.cuda.synchronize()
     assert host(y) == cpu_ref.ctr(key, ctr0, src, block_offset=off)
 
@@ -53,7 +53,7 @@ def test_ctr_fuzz(gpu, bits, n, shift, inplace, high, off, seed):
 @given(bits=st.sampled_from([128, 192, 256]), nb=st.one_of(st.integers(0, 400),
                                                            st.sampled_from([4096, 65536, 65537, 262144, 262160])),
        shift=st.integers(0, 15), inplace=st.booleans(), seed=st.integers(0, 2**31),
-       mode=st.sampled_from(["ecb", "ecb-dec", "cbc-dec", "cfb-dec"]))
+       mode=st.sampled_from(["ecb", "ecb-bitslice", "ecb-dec", "cbc-dec", "cfb-dec"]))
 def test_block_modes_fuzz(gpu, bits, nb, shift, inplace, seed, mode):
     key, iv = os.urandom(bits // 8), os.urandom(16)
     x = _buf(gpu, 16 * nb, shift, seed)
@@ -61,6 +61,8 @@ def test_block_modes_fuzz(gpu, bits, nb, shift, inplace, seed, mode):
     out = x if inplace else None
     if mode == "ecb":
         y, exp = ops.ecb_encrypt(x, key, out=out), cpu_ref.ecb(key, src)
+    elif mode == "ecb-bitslice":  # split bulk / edge launches of the bitsliced kernel
+        y, exp = ops.ecb_encrypt(x, key, out=out, impl="bitslice"), cpu_ref.ecb(key, src)
     elif mode == "ecb-dec":
         y, exp = ops.ecb_decrypt(x, key, out=out), cpu_ref.ecb(key, src, decrypt=True)
     elif mode == "cbc-dec":
