@@ -127,7 +127,13 @@ using namespace otc_rt;
 
 namespace {
 
-int pick_impl(int impl, int bits)
+/* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  CTR over >= 1 GiB with
+ * AES-192/256 runs bitsliced (64 GiB in place: AES-256 1165-1168 vs 1119-1121
+ * GB/s, AES-192 1317-1321 vs 1311-1312); AES-128 CTR (parity, the T-table
+ * steadier across boxes), every other mode and smaller calls (the bitsliced
+ * grid needs ~768 workgroups of 128 KiB to fill the chip, plus two table
+ * kernels per call) take the T-table.  ctr_bytes = 0 for non-CTR calls. */
+int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
 {
     if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_HYBRID) return impl;
     const char *env = getenv("OTC_IMPL");
@@ -136,8 +142,8 @@ int pick_impl(int impl, int bits)
         if (!strcmp(env, "bitslice")) return OTC_IMPL_BITSLICE;
         if (!strcmp(env, "hybrid")) return OTC_IMPL_HYBRID;
     }
-    (void)bits;
-    return OTC_IMPL_TTABLE; /* default: the measured winner (see docs/PERF.md) */
+    if (bits >= 192 && ctr_bytes >= ((size_t)1 << 30)) return OTC_IMPL_BITSLICE;
+    return OTC_IMPL_TTABLE;
 }
 
 /* Device buffers of the cipher ops: non-null, 16-byte aligned (every kernel
@@ -326,7 +332,7 @@ static int ctr_common(const void *in, void *out, size_t nbytes, const otc_aes_ke
     if ((r = check_bufs(in, out, nbytes, true, "aes_ctr"))) return r;
     if (nbytes == 0) return OTC_OK;
     hipStream_t st = (hipStream_t)stream;
-    const int im = pick_impl(impl, k->bits);
+    const int im = pick_impl(impl, k->bits, nbytes);
     hipError_t e = im == OTC_IMPL_BITSLICE ? otc_impl::bs_ctr(in, out, nbytes, *k, c, wrap64, st)
                    : im == OTC_IMPL_HYBRID ? hybrid_ctr(in, out, nbytes, *k, c, wrap64, st)
                                            : otc_impl::tt_ctr(in, out, nbytes, *k, c, wrap64, st);

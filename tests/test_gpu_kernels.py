@@ -442,3 +442,24 @@ def test_bitslice_split_and_onepass_launches(gpu, split):
     r = subprocess.run([sys.executable, "-c", _SPLIT_CHILD], env=env, cwd=root, capture_output=True, text=True,
                        timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("bits", [192, 256])
+def test_ctr_auto_large_aes256_bitsliced(gpu, bits):
+    """impl="auto" sends CTR of >= 1 GiB with AES-192/256 to the bitsliced
+    kernel (the measured winner there): head, a middle window and the tail of a
+    1 GiB + 3-byte buffer against the oracle, and equal to the forced
+    T-table output."""
+    n = (1 << 30) + 3
+    key, ctr0 = os.urandom(bits // 8), os.urandom(8) + (2**64 - 12345).to_bytes(8, "big")
+    x = torch.empty(n, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(x, seed=bits)
+    y = ops.ctr(x, key, ctr0, impl="auto")
+    t = ops.ctr(x, key, ctr0, impl="ttable")
+    torch.cuda.synchronize()
+    assert torch.equal(y, t)
+    S = 1 << 16
+    for off in (0, (n // 2) & ~15, n - S - 3):
+        blk = off // 16
+        exp = cpu_ref.ctr(key, ctr0, host(x[blk * 16:blk * 16 + S + 3]), block_offset=blk)
+        assert host(y[blk * 16:blk * 16 + S + 3]) == exp
