@@ -129,10 +129,12 @@ namespace {
 
 /* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  CTR over >= 1 GiB with
  * AES-192/256 runs bitsliced (64 GiB in place: AES-256 1165-1168 vs 1119-1121
- * GB/s, AES-192 1317-1321 vs 1311-1312); AES-128 CTR (parity, the T-table
- * steadier across boxes), every other mode and smaller calls (the bitsliced
- * grid needs ~768 workgroups of 128 KiB to fill the chip, plus two table
- * kernels per call) take the T-table.  ctr_bytes = 0 for non-CTR calls. */
+ * GB/s, AES-192 1317-1321 vs 1311-1312); AES-128 CTR (the two kernels at
+ * parity; the hybrid split measured +0.5..1.3% on one box and -0.3..+1.3% on
+ * another, within box noise, so the single T-table kernel stays), every
+ * other mode and smaller calls (the bitsliced grid needs ~768 workgroups of
+ * 128 KiB to fill the chip, plus two table kernels per call) take the
+ * T-table.  ctr_bytes = 0 for non-CTR calls. */
 int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
 {
     if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_HYBRID) return impl;
@@ -294,7 +296,10 @@ static hipError_t hybrid_ctr_on(const void *in, void *out, size_t nbytes, const 
                                 hipStream_t st, AuxStream &a)
 {
     hipError_t e;
-    double frac = 0.6;
+    /* T-table share of the blocks (64 GiB AES-128 in place, 2 reps each:
+     * 0.75 1547/1558, 0.8 1556/1556, 0.85 1564/1565, 0.9 1564/1553 GB/s;
+     * T-table alone 1544/1548); OTC_HYBRID_TT overrides */
+    double frac = 0.85;
     if (const char *f = getenv("OTC_HYBRID_TT")) frac = atof(f);
     const uint64_t nblk = nbytes / 16;
     uint64_t ntt = (uint64_t)(nblk * frac);

@@ -463,3 +463,22 @@ def test_ctr_auto_large_aes256_bitsliced(gpu, bits):
         blk = off // 16
         exp = cpu_ref.ctr(key, ctr0, host(x[blk * 16:blk * 16 + S + 3]), block_offset=blk)
         assert host(y[blk * 16:blk * 16 + S + 3]) == exp
+
+
+@pytest.mark.parametrize("n", [16 * 5000 + 9, 16 * 2048 * 40 + 3, (32 << 20) + 16 * 777 + 5])
+@pytest.mark.parametrize("ctr_low", [0, 2047, (1 << 64) - 100000])
+def test_ctr_hybrid_matches_oracle(gpu, n, ctr_low):
+    """impl="hybrid": the T-table kernel over the first 85% of the blocks
+    (rounded to 2048-block tasks) and the bitsliced kernel over the rest
+    (counter advanced by the split), concurrently on two streams; the split
+    can fall on a counter carry."""
+    key = os.urandom(16)
+    ctr0 = os.urandom(8) + ctr_low.to_bytes(8, "big")
+    x = rnd(n, gpu, n % 1000)
+    y = ops.ctr(x, key, ctr0, impl="hybrid")
+    torch.cuda.synchronize()
+    assert host(y) == cpu_ref.ctr(key, ctr0, host(x))
+    ops.ctr(x, key, ctr0, out=x, impl="hybrid")  # in place
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)
+
