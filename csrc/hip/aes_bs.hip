@@ -327,7 +327,7 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
  * ops cover their latency.  D: the other register slots are loaded D slots
  * ahead of use, in groups of 4, as the keystream of consumed slots frees
  * registers (loading all of them up front spills at 3 waves). */
-template <int NR, int MODE, int LS, bool CACHE, bool FO, bool LATE = true, int MIX = 2, int PRE = 4, int D = 8>
+template <int NR, int MODE, int LS, bool CACHE, bool FO, int MIX = 2, int PRE = 4, int D = 8>
 __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key &K, uint4 *stage)
 {
     Task t;
@@ -336,7 +336,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
     const uint64_t shift = (MODE == BS_CTR) ? P.shift : 0;
     const bool full = FO || t.full; /* FO: a BS_FULL_ONLY launch */
     W s[128];
-    /* LATE (counter caching): issued after rounds 1-2 have consumed the
+    /* with counter caching: issued after rounds 1-2 have consumed the
      * per-lane table loads -- vmcnt retires in order and hipcc waits for a
      * vector load queued behind LDS DMA with vmcnt(0), so a DMA issued first
      * put its whole latency in front of every task's round 1 */
@@ -358,7 +358,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
         }
     }
     };
-    if (!(MODE == BS_CTR && CACHE && LATE)) prefetch();
+    if (!(MODE == BS_CTR && CACHE)) prefetch();
     if (MODE == BS_CTR && CACHE) {
         /* counter caching: rounds 1-2 from the per-call / per-group tables */
         const uint64_t task = t.vbase >> 11;
@@ -375,10 +375,8 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
         ctr_rounds12(s15, s14, GroupTerms<0>{gp}, s);
         pin_n(s, 128);
         sched_fence();
-        if (LATE) {
-            prefetch();
-            sched_fence();
-        }
+        prefetch();
+        sched_fence();
         round_step_kt<MIX, GroupTerms<8>, 2>(s, GroupTerms<8>{gp});
         pin_n(s, 128);
         sched_fence();
@@ -478,12 +476,12 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
  * workgroups per CU); ECB loads its whole input before the rounds. */
 constexpr int BS_LS = 8;
 
-template <int NR, int MODE, int LS, bool CACHE, bool FO, bool LATE = true>
+template <int NR, int MODE, int LS, bool CACHE, bool FO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_aes_bs_t3(BsParams P,
                                                                                              otc_aes_key K)
 {
     __shared__ uint4 stage[LS > 0 ? 4 * LS * 64 : 1];
-    aes_bs_task<NR, MODE, LS, CACHE, FO, LATE>(P, K, stage);
+    aes_bs_task<NR, MODE, LS, CACHE, FO>(P, K, stage);
 }
 
 template <int NR, int MODE>
@@ -537,36 +535,39 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
      * runtime range checks: ECB +5% split (1240 vs 1178 GB/s, 4 GiB), CTR
      * -0.8% (its plaintext loads are mostly DMA'd, and the clock it holds
      * decides), so the default is per mode; OTC_BS_SPLIT=0|1 overrides.
-     * OTC_BS_DMA_EARLY=1: plaintext DMA before the table loads (A/B, -1%). */
+     * (The plaintext DMA before the table loads measured -1%: issued after
+     * rounds 1-2 only, no knob.) */
     static const int split_env = getenv("OTC_BS_SPLIT") ? atoi(getenv("OTC_BS_SPLIT")) : -1;
     const bool onepass = split_env < 0 ? MODE == BS_CTR : split_env == 0;
-    static const bool early = getenv("OTC_BS_DMA_EARLY") && atoi(getenv("OTC_BS_DMA_EARLY")) != 0;
     const bool edge = (MODE == BS_CTR && P.shift != 0) || vt % 2048 != 0;
-    auto run = [&](auto cachec, auto latec) {
-        constexpr bool C = decltype(cachec)::value, L = decltype(latec)::value;
+    auto run = [&](auto cachec) {
+        constexpr bool C = decltype(cachec)::value;
         if (onepass) {
             Q.part = BS_ALL;
-            hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, false, L>), g, b, 0, st, Q, K);
+            hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, false>), g, b, 0, st, Q, K);
             return;
         }
         Q.part = BS_FULL_ONLY;
-        hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, true, L>), g, b, 0, st, Q, K);
+        hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, true>), g, b, 0, st, Q, K);
         if (edge) {
             Q.part = BS_EDGE_ONLY;
-            hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, false, L>), dim3(1), b, 0, st, Q, K);
+            hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, false>), dim3(1), b, 0, st, Q, K);
         }
     };
-    if (cache) {
-        Q.ctab = tab + kt_words;
-        const uint64_t n = 96 + ngroups;
-        hipLaunchKernelGGL(k_bs_ctr_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, P.cbase, P.wrap64,
-                           ngroups, (uint32_t *)Q.ctab);
-        if (early)
-            run(std::true_type{}, std::false_type{});
-        else
-            run(std::true_type{}, std::true_type{});
+    /* counter caching exists for CTR only: no ECB kernels are instantiated
+     * with it */
+    if constexpr (MODE == BS_CTR) {
+        if (cache) {
+            Q.ctab = tab + kt_words;
+            const uint64_t n = 96 + ngroups;
+            hipLaunchKernelGGL(k_bs_ctr_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, P.cbase,
+                               P.wrap64, ngroups, (uint32_t *)Q.ctab);
+            run(std::true_type{});
+        } else {
+            run(std::false_type{});
+        }
     } else {
-        run(std::false_type{}, std::true_type{});
+        run(std::false_type{});
     }
     e = hipGetLastError();
     const hipError_t f = hipFreeAsync(tab, st);
