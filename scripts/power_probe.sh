@@ -9,7 +9,7 @@ for impl in ttable bitslice; do
     P=$!
     for i in $(seq 1 8); do
         sleep 2; echo "== $(date +%T) $impl" >> gpurun_out/power/smi.txt
-        timeout 20 amd-smi metric -p -c -g 0 >> gpurun_out/power/smi.txt 2>&1
+        timeout 20 amd-smi metric -p -c -t -v -g 0 >> gpurun_out/power/smi.txt 2>&1
     done
     wait $P || exit 1
 done
