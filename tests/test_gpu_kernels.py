@@ -418,11 +418,21 @@ for bits in (128, 256):
         torch.cuda.synchronize()
         if y.cpu().numpy().tobytes() != cpu_ref.ctr(key, ctr0, x.cpu().numpy().tobytes()):
             bad.append(("ctr", bits, n, low))
+        z = x.clone()  # in place: a task run by both launches would be XORed twice
+        ops.ctr(z, key, ctr0, out=z, impl="bitslice")
+        torch.cuda.synchronize()
+        if not torch.equal(z, y):
+            bad.append(("ctr-inplace", bits, n, low))
         m = n & ~15
         e = ops.ecb_encrypt(x[:m], key, impl="bitslice")
         torch.cuda.synchronize()
         if e.cpu().numpy().tobytes() != cpu_ref.ecb(key, x[:m].cpu().numpy().tobytes()):
             bad.append(("ecb", bits, m))
+        w = x[:m].clone()
+        ops.ecb_encrypt(w, key, out=w, impl="bitslice")
+        torch.cuda.synchronize()
+        if not torch.equal(w, e):
+            bad.append(("ecb-inplace", bits, m))
 print("BAD", bad)
 sys.exit(1 if bad else 0)
 """
