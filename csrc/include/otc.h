@@ -58,10 +58,11 @@ typedef struct {
 int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 
 /* ---- implementation selection ------------------------------------------- */
-#define OTC_IMPL_AUTO 0
+#define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for AES-192/256 CTR of >= 1 GiB,
+                               T-table otherwise (OTC_IMPL=ttable|bitslice|hybrid env overrides) */
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
 #define OTC_IMPL_BITSLICE 2 /* 32-block-per-lane bitsliced VALU kernel */
-#define OTC_IMPL_HYBRID 3   /* CTR: T-table + bitsliced kernels co-resident on every CU */
+#define OTC_IMPL_HYBRID 3   /* CTR: T-table (85% of the blocks) + bitsliced kernels co-resident on every CU */
 
 /* ---- device ops (device pointers; async on `stream`) ---------------------
  * All functions accept any byte length; the trailing partial block of CTR is
