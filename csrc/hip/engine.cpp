@@ -127,9 +127,11 @@ using namespace otc_rt;
 
 namespace {
 
-/* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  CTR over >= 1 GiB with
+/* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  CTR over >= 4 GiB with
  * AES-192/256 runs bitsliced (64 GiB in place: AES-256 1165-1168 vs 1119-1121
- * GB/s, AES-192 1317-1321 vs 1311-1312); AES-128 CTR (the two kernels at
+ * GB/s, AES-192 1317-1321 vs 1311-1312; 4 GiB: 1101 vs 1046-1053 and 1251 vs
+ * 1235; at 2 GiB AES-192 and at 1 GiB both still favour the T-table, whose
+ * persistent grid has no per-call table kernels); AES-128 CTR (the two kernels at
  * parity; the hybrid split measured +0.5..1.3% on one box and -0.3..+1.3% on
  * another, within box noise, so the single T-table kernel stays), every
  * other mode and smaller calls (the bitsliced grid needs ~768 workgroups of
@@ -144,7 +146,7 @@ int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
         if (!strcmp(env, "bitslice")) return OTC_IMPL_BITSLICE;
         if (!strcmp(env, "hybrid")) return OTC_IMPL_HYBRID;
     }
-    if (bits >= 192 && ctr_bytes >= ((size_t)1 << 30)) return OTC_IMPL_BITSLICE;
+    if (bits >= 192 && ctr_bytes >= ((size_t)4 << 30)) return OTC_IMPL_BITSLICE;
     return OTC_IMPL_TTABLE;
 }
 

@@ -58,7 +58,7 @@ typedef struct {
 int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 
 /* ---- implementation selection ------------------------------------------- */
-#define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for AES-192/256 CTR of >= 1 GiB,
+#define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for AES-192/256 CTR of >= 4 GiB,
                                T-table otherwise (OTC_IMPL=ttable|bitslice|hybrid env overrides) */
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
 #define OTC_IMPL_BITSLICE 2 /* 32-block-per-lane bitsliced VALU kernel */

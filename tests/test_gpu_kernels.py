@@ -456,11 +456,11 @@ def test_bitslice_split_and_onepass_launches(gpu, split):
 
 @pytest.mark.parametrize("bits", [192, 256])
 def test_ctr_auto_large_aes256_bitsliced(gpu, bits):
-    """impl="auto" sends CTR of >= 1 GiB with AES-192/256 to the bitsliced
+    """impl="auto" sends CTR of >= 4 GiB with AES-192/256 to the bitsliced
     kernel (the measured winner there): head, a middle window and the tail of a
-    1 GiB + 3-byte buffer against the oracle, and equal to the forced
+    4 GiB + 3-byte buffer against the oracle, and equal to the forced
     T-table output."""
-    n = (1 << 30) + 3
+    n = (4 << 30) + 3
     key, ctr0 = os.urandom(bits // 8), os.urandom(8) + (2**64 - 12345).to_bytes(8, "big")
     x = torch.empty(n, dtype=torch.uint8, device=gpu)
     ops.fill_random_(x, seed=bits)
