@@ -30,8 +30,13 @@
  *     (tools/sbox_schedule.py) and a 55-node MixColumns column
  *     (tools/mixcol_search.py; the textbook forms take 76-80);
  *   - CTR: the plaintext of the first 8 slots goes straight to LDS by the
- *     DMA path at task start (no VGPRs) and lands while the rounds run; the
- *     other slots are loaded 8 slots ahead of their use in groups of 4;
+ *     DMA path (no VGPRs) once rounds 1-2 have consumed the counter-cache
+ *     table loads, and lands while the other rounds run; the other slots are
+ *     loaded 8 slots ahead of their use in groups of 4;
+ *   - ECB (and CTR with OTC_BS_SPLIT=1): a bulk launch compiled for full
+ *     tasks only, whose load / store phases are straight-line code with exact
+ *     vmcnt waits, plus a one-workgroup launch for a partial first / last
+ *     task (BS_FULL_ONLY / BS_EDGE_ONLY);
  *   - the last round key is folded into the output XOR (ks ^ rk ^ pt as one
  *     v_bitop3 per word) after the single output transpose.
  * The round-1 kernel (3 waves, ~32 planes in scratch) stays selectable as
