@@ -73,7 +73,7 @@ $(OBJ)/hip/%.o: csrc/hip/%.cpp csrc/hip/otc_device.h csrc/hip/engine_internal.h 
 
 $(LIBDIR)/libotc.so: $(HIP_OBJ) $(CPU_OBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lrocprofiler-sdk-roctx -lpthread -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lrocprofiler-sdk-roctx -lpthread -Wl,--no-undefined -Wl,-rpath,$(ROCM)/lib
 
 $(LIBDIR)/libotc_cpu.so: $(CPU_OBJ)
 	@mkdir -p $(LIBDIR)

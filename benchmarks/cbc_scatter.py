@@ -21,24 +21,28 @@ piece carries the 16-byte ciphertext block in front of it (the halo), so each
 rank decrypts its piece independently and the gathered result equals the
 serial decryption of the whole stream.
 
-    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 benchmarks/cbc_scatter.py
-    python benchmarks/cbc_scatter.py --gib-per-gpu 4        # 1 GPU
+Every rank's piece is verified (checksums of what it received and produced
+against what the root sent and gathered, plus an oracle sample of its
+output) after the first and the last round; a failed rank fails the run.
+Even at one GPU the job runs through a (1-rank) RCCL process group with the
+duplex communicators, so the collective code path is what is measured.
+
+    python benchmarks/cbc_scatter.py --gpus 8                # self-spawns 8 ranks
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 benchmarks/cbc_scatter.py --gpus 8
+    python benchmarks/cbc_scatter.py --gib-per-gpu 4         # 1 GPU
 """
 import argparse
 import json
 import os
 import sys
 
-import torch
-
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-
-from our_tree_amd.parallel import dist as pdist  # noqa: E402
-from our_tree_amd.parallel import jobs  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); spawned here without a launcher")
+    ap.add_argument("--timeout", type=float, default=3600.0, help="seconds before a self-spawned run is stopped")
     ap.add_argument("--gib-per-gpu", type=float, default=32.0)
     ap.add_argument("--chunk-mib", type=int, default=1024, help="per-rank bytes per scatter round")
     ap.add_argument("--sector", type=int, default=4096)
@@ -48,7 +52,18 @@ def main():
                     help="exact single-stream CBC decryption: every piece travels with its 16-byte halo")
     args = ap.parse_args()
 
-    rank, world, local = pdist.init_from_env()
+    # the launch is decided before anything touches the GPU (parallel/launch.py)
+    from our_tree_amd.parallel import launch
+
+    launch.dispatch(args.gpus, os.path.abspath(__file__), sys.argv[1:], timeout_s=args.timeout)
+
+    import torch
+
+    from our_tree_amd.parallel import dist as pdist
+    from our_tree_amd.parallel import jobs
+
+    rank, world, local = pdist.init_from_env(force=True)
+    assert world == args.gpus, (world, args.gpus)
     dev = torch.device("cuda", local)
     chunk = args.chunk_mib << 20
     total = int(args.gib_per_gpu * (1 << 30)) * world
@@ -62,10 +77,14 @@ def main():
                           "n_gpus": world, "total_bytes": res["total_bytes"], "rounds": rounds,
                           "chunk_per_rank": chunk, "overlap": res["overlap"], "seconds": round(res["seconds"], 3),
                           "value": round(res["gbps"], 3), "unit": "GB/s", "verified_sample": res["verified"],
-                          "ranks": res["ranks"], "backend": res["backend"], "xgmi_bytes": res["xgmi_bytes"],
+                          "ranks": res["ranks"], "ranks_verified": res["ranks_verified"],
+                          "backend": res["backend"], "collectives": res["collectives"],
+                          "xgmi_bytes_verified": res["xgmi_bytes_verified"],
+                          "xgmi_bytes_timed": res["xgmi_bytes_timed"],
                           "data": "synthetic random (root GPU fill)"}), flush=True)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
+    sys.exit(0 if res["verified"] else 1)
 
 
 if __name__ == "__main__":

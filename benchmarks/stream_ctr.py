@@ -9,7 +9,8 @@ rank re-streams a pinned host window of --window-gib (plaintext repeats, the
 counter -- and therefore the keystream -- does not) until its share of
 --total-gib has crossed PCIe both ways.  Default: 1 TiB over the node.
 
-    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 benchmarks/stream_ctr.py
+    python benchmarks/stream_ctr.py --gpus 8            # self-spawns 8 ranks
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 benchmarks/stream_ctr.py --gpus 8
     python benchmarks/stream_ctr.py --total-gib 32      # 1 GPU
 """
 import argparse
@@ -19,23 +20,32 @@ import sys
 import time
 
 import numpy as np
-import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-
-from our_tree_amd.models import cpu_ref  # noqa: E402
-from our_tree_amd.parallel import dist as pdist  # noqa: E402
-from our_tree_amd.parallel import stream as pstream  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); spawned here without a launcher")
+    ap.add_argument("--timeout", type=float, default=3600.0, help="seconds before a self-spawned run is stopped")
     ap.add_argument("--total-gib", type=float, default=1024.0)
     ap.add_argument("--window-gib", type=float, default=4.0)
     ap.add_argument("--chunk-mib", type=int, default=64)
     args = ap.parse_args()
 
+    # the launch is decided before anything touches the GPU (parallel/launch.py)
+    from our_tree_amd.parallel import launch
+
+    launch.dispatch(args.gpus, os.path.abspath(__file__), sys.argv[1:], timeout_s=args.timeout)
+
+    import torch
+
+    from our_tree_amd.models import cpu_ref
+    from our_tree_amd.parallel import dist as pdist
+    from our_tree_amd.parallel import stream as pstream
+
     rank, world, local = pdist.init_from_env()
+    assert world == args.gpus, (world, args.gpus)
     share = int(args.total_gib * (1 << 30)) // world
     win = min(share, int(args.window_gib * (1 << 30)))
     win -= win % 16
@@ -53,18 +63,34 @@ def main():
         if world > 1:
             torch.distributed.barrier()
         t0 = time.perf_counter()
-        for p in range(share // win):
-            eng.run("ctr", hin, hout, key, ctr0, block_offset=base_blk + p * (win // 16))
+        h2d = d2h = 0.0
+        npass = share // win
+        for p in range(npass):
+            st = eng.run("ctr", hin, hout, key, ctr0, block_offset=base_blk + p * (win // 16))
+            h2d += st["h2d_gbps"] / npass
+            d2h += st["d2h_gbps"] / npass
         el = pdist.allreduce_max(time.perf_counter() - t0)
+        numa = eng.numa_node
+    ok_all = pdist.allreduce_max(0.0 if ok else 1.0) == 0.0
+    row = torch.tensor([float(rank), float(numa), h2d, d2h], dtype=torch.float64)
+    rows = [row]
+    if world > 1:
+        dev = torch.device("cuda", local) if torch.distributed.get_backend() == "nccl" else "cpu"
+        rows = [torch.empty(4, dtype=torch.float64, device=dev) for _ in range(world)]
+        torch.distributed.all_gather(rows, row.to(dev))
     if rank == 0:
         tot = share * world
         print(json.dumps({"metric": "GB/s AES-128-CTR host-streamed (pinned H2D/D2H overlap)", "n_gpus": world,
                           "total_bytes": tot, "window_bytes": win, "chunk": args.chunk_mib << 20,
                           "seconds": round(el, 3), "value": round(tot / el / 1e9, 3), "unit": "GB/s",
-                          "verified_sample": bool(ok), "data": "synthetic random host window, re-streamed"}),
+                          "verified_sample": ok_all,
+                          "per_rank": [{"rank": int(r[0]), "numa_node": int(r[1]), "h2d_gbps": round(float(r[2]), 2),
+                                        "d2h_gbps": round(float(r[3]), 2)} for r in (x.cpu().tolist() for x in rows)],
+                          "data": "synthetic random host window, re-streamed"}),
               flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+    sys.exit(0 if ok_all else 1)
 
 
 if __name__ == "__main__":

@@ -138,7 +138,7 @@ int main(int argc, char **argv)
         else if (a == "--warmup") c.warmup = atoi(nx());
         else if (a == "--impl") {
             std::string v = nx();
-            c.impl = v == "ttable" ? OTC_IMPL_TTABLE : v == "bitslice" ? OTC_IMPL_BITSLICE : v == "hybrid" ? OTC_IMPL_HYBRID : OTC_IMPL_AUTO;
+            c.impl = v == "ttable" ? OTC_IMPL_TTABLE : v == "bitslice" ? OTC_IMPL_BITSLICE : OTC_IMPL_AUTO;
         } else if (a == "--inplace") c.inplace = true;
         else if (a == "--verify") c.verify = true;
         else if (a == "--clock") c.clock = true;
@@ -260,7 +260,7 @@ int main(int argc, char **argv)
            "\"ms\": %.4f, \"gbps\": %.2f, \"cycles_per_byte_per_cu\": %.3f, \"cus\": %d, \"clock_mhz\": %.0f, %s"
            "\"verified\": %s}\n",
            c.mode.c_str(), c.bits, c.bytes,
-           c.impl == OTC_IMPL_TTABLE ? "ttable" : c.impl == OTC_IMPL_BITSLICE ? "bitslice" : c.impl == OTC_IMPL_HYBRID ? "hybrid" : "auto",
+           c.impl == OTC_IMPL_TTABLE ? "ttable" : c.impl == OTC_IMPL_BITSLICE ? "bitslice" : "auto",
            c.inplace ? "true" : "false", c.iters, ms, gbps, cpb, cus, clk_hz / 1e6, clk,
            c.verify ? (ok ? "true" : "false") : "null");
     otc_dev_free(a.in);

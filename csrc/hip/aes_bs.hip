@@ -33,14 +33,13 @@
  *     DMA path (no VGPRs) once rounds 1-2 have consumed the counter-cache
  *     table loads, and lands while the other rounds run; the other slots are
  *     loaded 8 slots ahead of their use in groups of 4;
- *   - ECB (and CTR with OTC_BS_SPLIT=1): a bulk launch compiled for full
- *     tasks only, whose load / store phases are straight-line code with exact
+ *   - ECB: a bulk launch compiled for full tasks only, whose load / store phases are straight-line code with exact
  *     vmcnt waits, plus a one-workgroup launch for a partial first / last
  *     task (BS_FULL_ONLY / BS_EDGE_ONLY);
  *   - the last round key is folded into the output XOR (ks ^ rk ^ pt as one
  *     v_bitop3 per word) after the single output transpose.
- * The round-1 kernel (3 waves, ~32 planes in scratch) stays selectable as
- * OTC_BS_LEGACY=1 for A/B runs.  Measurements: docs/PERF.md, profiles/r2/bitslice.
+ * Measurements (and the round-1 kernel this replaced): docs/PERF.md,
+ * profiles/r2/bitslice.
  *
  * No reference counterpart (the reference has only a T-table CUDA kernel,
  * /root/reference/aes-gpu/Source/AES.cu:284-392).
@@ -137,92 +136,6 @@ __device__ __forceinline__ void ecb_load_planes(const BsParams &P, const Task &t
 #pragma unroll
         for (int q = 0; q < 32; ++q) s[32 * w + q] = m[q];
         sched_fence();
-    }
-}
-
-/* Round-1 task (OTC_BS_LEGACY=1): round keys as laundered SGPR words, mask
- * arithmetic on the SALU, uniform counter planes left to hipcc's uniformity
- * analysis; at 3 waves per SIMD ~32 values spill to scratch. */
-template <int NR, int MODE>
-__device__ __forceinline__ void aes_bs_task_legacy(const BsParams &P, const otc_aes_key &K)
-{
-    Task t;
-    if (!task_of<MODE>(P, t)) return;
-    const uint32_t lane = t.lane;
-    const uint64_t shift = (MODE == BS_CTR) ? P.shift : 0;
-    W s[128];
-    if (MODE == BS_CTR) {
-        uint64_t clo = P.cbase.lo + t.vbase;
-        uint64_t chi = P.cbase.hi + ((!P.wrap64 && clo < P.cbase.lo) ? 1u : 0u);
-#pragma unroll
-        for (int b = 0; b < 16; ++b) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int n = 8 * (15 - b) + i; /* numeric counter bit */
-                W v;
-                if (n < 6) {
-                    v = lane_mask(lane, n);
-                } else if (n < 11) {
-                    constexpr W pat[5] = {0xAAAAAAAAu, 0xCCCCCCCCu, 0xF0F0F0F0u, 0xFF00FF00u, 0xFFFF0000u};
-                    v = pat[n - 6];
-                } else if (n < 64) {
-                    v = (W)(0u - (uint32_t)((clo >> n) & 1u));
-                } else {
-                    v = (W)(0u - (uint32_t)((chi >> (n - 64)) & 1u));
-                }
-                s[8 * b + i] = v;
-            }
-        }
-    } else {
-        ecb_load_planes(P, t, s, t.full);
-    }
-    sched_fence();
-    /* round keys laundered through an empty asm so hipcc materialises each
-     * key mask next to its use instead of all 128*NR up front */
-    uint32_t rk[4 * (NR + 1)];
-#pragma unroll
-    for (int q = 0; q < 4 * (NR + 1); ++q) {
-        uint32_t v = K.rk[q];
-        asm volatile("" : "+s"(v));
-        rk[q] = v;
-    }
-    encrypt_planes<NR, false>(s, [&](int r, int p) -> W {
-        /* plane p = 32*w + q  <->  bit q of round-key word w */
-        return (W)(0u - ((rk[4 * r + (p >> 5)] >> (p & 31)) & 1u));
-    });
-    pin_n(s, 128);
-    sched_fence();
-
-    const int64_t tstart = (int64_t)t.vbase - (int64_t)shift;
-    const uint8_t *ib = P.in + tstart * 16;
-    uint8_t *ob = P.out + tstart * 16;
-    uint32_t lo = lane * 16u;
-    asm volatile("" : "+v"(lo));
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        transpose32(s + 32 * w);
-        pin_n(s + 32 * w, 32);
-        sched_fence();
-    }
-    const uint32_t k0 = rk[4 * NR + 0], k1 = rk[4 * NR + 1], k2 = rk[4 * NR + 2], k3 = rk[4 * NR + 3];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        if ((k & 3) == 0) sched_fence();
-        const int64_t si = tstart + (int64_t)lane + 64 * k;
-        if (t.full || (si >= 0 && (uint64_t)si < P.nblocks)) {
-            const uint32_t off = lo + 1024u * k;
-            uint4 o;
-            if (MODE == BS_CTR) {
-                const uint4 x = *(const uint4 *)(ib + off);
-                o.x = x3(x.x, s[k], k0);
-                o.y = x3(x.y, s[32 + k], k1);
-                o.z = x3(x.z, s[64 + k], k2);
-                o.w = x3(x.w, s[96 + k], k3);
-            } else {
-                o = make_uint4(s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3);
-            }
-            *(uint4 *)(ob + off) = o;
-        }
     }
 }
 
@@ -490,13 +403,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 }
 
 template <int NR, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_aes_bs_w3(BsParams P,
-                                                                                             otc_aes_key K)
-{
-    aes_bs_task_legacy<NR, MODE>(P, K);
-}
-
-template <int NR, int MODE>
 hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
 {
     const uint64_t vt = P.nblocks + (MODE == BS_CTR ? P.shift : 0);
@@ -505,14 +411,8 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     if (wgs < 1) wgs = 1;
     if (wgs > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const dim3 g((unsigned)wgs), b(256);
-    static const bool legacy = getenv("OTC_BS_LEGACY") && atoi(getenv("OTC_BS_LEGACY")) != 0;
-    if (legacy) {
-        hipLaunchKernelGGL((k_aes_bs_w3<NR, MODE>), g, b, 0, st, P, K);
-        return hipGetLastError();
-    }
-    /* CTR counter caching (OTC_BS_CTR_NOCACHE=1: off, for A/B runs) */
-    static const bool nocache = getenv("OTC_BS_CTR_NOCACHE") && atoi(getenv("OTC_BS_CTR_NOCACHE")) != 0;
-    bool cache = MODE == BS_CTR && !nocache;
+    /* CTR counter caching (+34% over no caching, profiles/r2/bitslice) */
+    bool cache = MODE == BS_CTR;
     const uint64_t ngroups = cache ? (((P.cbase.lo >> 11) & 31u) + tasks + 31) >> 5 : 0;
     const size_t kt_words = (size_t)NR * 16 * OTC_BS_KT_STRIDE;
     /* per-call tables, stream-ordered: written by small kernels, freed behind
@@ -539,11 +439,8 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     /* Split (bulk BS_FULL_ONLY launch + edge launch) or one launch with
      * runtime range checks: ECB +5% split (1240 vs 1178 GB/s, 4 GiB), CTR
      * -0.8% (its plaintext loads are mostly DMA'd, and the clock it holds
-     * decides), so the default is per mode; OTC_BS_SPLIT=0|1 overrides.
-     * (The plaintext DMA before the table loads measured -1%: issued after
-     * rounds 1-2 only, no knob.) */
-    static const int split_env = getenv("OTC_BS_SPLIT") ? atoi(getenv("OTC_BS_SPLIT")) : -1;
-    const bool onepass = split_env < 0 ? MODE == BS_CTR : split_env == 0;
+     * decides), so the structure is per mode (profiles/r2/bitslice_out). */
+    const bool onepass = MODE == BS_CTR;
     const bool edge = (MODE == BS_CTR && P.shift != 0) || vt % 2048 != 0;
     auto run = [&](auto cachec) {
         constexpr bool C = decltype(cachec)::value;
@@ -596,7 +493,7 @@ hipError_t launch(const BsParams &P, const otc_aes_key &K, hipStream_t st)
 
 namespace otc_impl {
 
-hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t, int);
+hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
 
 hipError_t bs_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
                   hipStream_t st)
@@ -607,7 +504,7 @@ hipError_t bs_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K
         Ctr128 ct = c;
         ct.lo = c.lo + full / 16;
         if (!wrap64 && ct.lo < c.lo) ct.hi += 1;
-        hipError_t e = tt_ctr((const uint8_t *)in + full, (uint8_t *)out + full, nbytes % 16, K, ct, wrap64, st, 2);
+        hipError_t e = tt_ctr((const uint8_t *)in + full, (uint8_t *)out + full, nbytes % 16, K, ct, wrap64, st);
         if (e != hipSuccess) return e;
         nbytes = full;
         if (nbytes == 0) return hipSuccess;

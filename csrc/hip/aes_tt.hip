@@ -7,24 +7,28 @@
  * the whole block (data race) and a launch that asked for the whole buffer as
  * dynamic shared memory (never ran).  This file is a gfx950-first design:
  *
- *  * ONE 1 KiB T0 table replicated 64 ways in LDS (64 KiB): entry x of lane l
- *    lives at byte (x << 8) | (l << 2), so the 64 lanes of a ds_read_b32
- *    always hit 64 distinct banks -- conflict free for any data.  T1..T3 are
- *    byte rotations of T0 (one v_alignbit each).
+ *  * T0..T3 (T_k = rotl(T0, 8k)) each replicated 32 ways in 128 KiB of LDS:
+ *    entry x of table k for lane l lives at byte
+ *    (k >> 1) << 16 | x << 8 | (k & 1) << 7 | (l & 31) << 2, so the two
+ *    32-lane groups of a ds_read_b32 each hit 32 distinct banks --
+ *    conflict free for any data.
  *  * The LDS address of a lookup is ONE v_perm_b32: byte 1 <- the state byte,
- *    byte 0 <- lane*4, bytes 2..3 <- table select.  So a round costs per block
- *    16 ds_read_b32 + 16 v_perm + 12 v_alignbit + 8 v_xor3/v_bitop3.
- *  * Last round reuses T0: byte 1 of T0[x] is S[x]; two v_perm + one bitop3
- *    assemble a column.
+ *    bytes 0 and 2 <- a per-lane, per-table constant.  A round costs per block
+ *    16 ds_read_b32 + 16 v_perm + 8 v_xor3 (issued all lookups first).
+ *  * Last round reuses the T tables: S[x] is one byte of each T_k[x]; two
+ *    v_perm + one xor3 assemble a column with the last round key.
  *  * Round keys arrive BY VALUE in the kernel arguments (otc_aes_key), i.e.
  *    they are wave-uniform SGPR operands of the v_xor3s.
  *  * Each lane carries B independent blocks (ILP across LDS latency); block
  *    index = chunk + wave*64*B + b*64 + lane, so every global access is a
  *    fully coalesced 1 KiB dwordx4 wave access.  Persistent grid-stride loop
- *    amortises the 64 KiB table fill.
- *  * Decryption keeps Td0 (64 KiB) + the inverse S-box replicated as words
- *    (64 KiB) = 128 KiB, addressed with the same one-op v_perm (byte 2 selects
- *    the table).
+ *    amortises the table fill.
+ *  * CTR: counter-mode caching (k_aes_ctr_tt_cached): bytes 0..14 of a wave's
+ *    counters are uniform, so rounds 1-2 need 5 instead of 32 lookups/block.
+ *  * Decryption keeps Td0..Td3 (128 KiB) + the inverse S-box replicated as
+ *    words (32 KiB) = the whole 160 KiB LDS, same one-op v_perm addressing.
+ * Measurements and rejected variants (1-table layout, non-temporal accesses,
+ * other shapes): docs/PERF.md.
  */
 #include <hip/hip_runtime.h>
 
@@ -41,23 +45,12 @@ __device__ const AesTables g_tab = make_tables();
 
 
 
-constexpr uint32_t SEL(int k) { return 0x0c0c0000u | ((uint32_t)(4 + k) << 8); }
 /* second table (byte 2 of the address taken from lane word byte 2 = 1) */
 constexpr uint32_t SEL_HI(int k) { return 0x0c020000u | ((uint32_t)(4 + k) << 8); }
 
 __device__ __forceinline__ uint32_t lds_at(const uint32_t *tbl, uint32_t byte_addr)
 {
     return *(const uint32_t *)((const char *)tbl + byte_addr);
-}
-
-template <int THREADS>
-__device__ __forceinline__ void fill_rep64(uint32_t *lds, const uint32_t *src)
-{
-    uint4 *l4 = reinterpret_cast<uint4 *>(lds);
-    for (int q = threadIdx.x; q < 4096; q += THREADS) {
-        uint32_t v = src[q >> 4];
-        l4[q] = make_uint4(v, v, v, v);
-    }
 }
 
 /* 4-table layout (TBL4): T_k (k = 0..3, T_k = rotl(T0, 8k)) each replicated
@@ -86,45 +79,31 @@ __device__ __forceinline__ void tbl4_lane_consts(uint32_t lane, uint32_t (&lk)[4
     for (int k = 0; k < 4; ++k) lk[k] = ((uint32_t)(k >> 1) << 16) | ((uint32_t)(k & 1) << 7) | ((lane & 31u) << 2);
 }
 
-/* ISSUE_ALL: per round, issue every lookup of all B blocks before combining
- * any of them.  hipcc otherwise consumes each ds_read right away (1-3 LDS ops
+/* Per round, issue every lookup of all B blocks before combining any of
+ * them (+0..1.6%, profiles/r1/otbench_issue_all_ab.jsonl).  hipcc otherwise consumes each ds_read right away (1-3 LDS ops
  * in flight per wave); with at most 16 waves per CU (the 128 KiB table allows
  * one workgroup) that starves the LDS pipe.  gfx9 lgkmcnt still caps a wave at
  * 15 outstanding LDS ops. */
-template <int R0, int NR, int B, bool ISSUE_ALL = true>
+template <int R0, int NR, int B>
 __device__ __forceinline__ void enc_rounds4_from(const uint32_t *tbl, const uint32_t (&lk)[4], const otc_aes_key &K,
                                                  uint32_t (&s)[B][4])
 {
 #pragma unroll
     for (int r = R0; r < NR; ++r) {
         uint32_t t[B][4];
-        if (ISSUE_ALL) {
-            uint32_t a[B][4][4];
+        uint32_t a[B][4][4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int b = 0; b < B; ++b)
+            for (int b = 0; b < B; ++b)
 #pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        a[b][j][k] = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + k) & 3], lk[k], SEL_HI(k)));
+                for (int k = 0; k < 4; ++k)
+                    a[b][j][k] = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + k) & 3], lk[k], SEL_HI(k)));
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int b = 0; b < B; ++b)
-                    t[b][j] = xor3(xor3(a[b][j][0], a[b][j][1], a[b][j][2]), a[b][j][3], K.rk[4 * r + j]);
-        } else {
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lk[0], SEL_HI(0)));
-                    uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lk[1], SEL_HI(1)));
-                    uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lk[2], SEL_HI(2)));
-                    uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lk[3], SEL_HI(3)));
-                    t[b][j] = xor3(xor3(a0, a1, a2), a3, K.rk[4 * r + j]);
-                }
-            }
-        }
+            for (int b = 0; b < B; ++b)
+                t[b][j] = xor3(xor3(a[b][j][0], a[b][j][1], a[b][j][2]), a[b][j][3], K.rk[4 * r + j]);
 #pragma unroll
         for (int b = 0; b < B; ++b)
 #pragma unroll
@@ -221,103 +200,6 @@ __device__ __forceinline__ void dec_rounds4(const uint32_t *tbl, const uint32_t 
         for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
 }
 
-/* ---------------------------------------------------------------------------
- * Round functions for B blocks at once (arrays are compile-time indexed)
- * ------------------------------------------------------------------------- */
-template <int R0, int NR, int B>
-__device__ __forceinline__ void enc_rounds_from(const uint32_t *tbl, uint32_t lane4, const otc_aes_key &K,
-                                                uint32_t (&s)[B][4])
-{
-#pragma unroll
-    for (int r = R0; r < NR; ++r) {
-        uint32_t t[B][4];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lane4, SEL(0)));
-                uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lane4, SEL(1)));
-                uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lane4, SEL(2)));
-                uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lane4, SEL(3)));
-                t[b][j] = xor3(xor3(a0, rotl8(a1), rotl16(a2)), rotl24(a3), K.rk[4 * r + j]);
-            }
-        }
-#pragma unroll
-        for (int b = 0; b < B; ++b)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
-    }
-    uint32_t t[B][4];
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lane4, SEL(0)));
-            uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lane4, SEL(1)));
-            uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lane4, SEL(2)));
-            uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lane4, SEL(3)));
-            /* byte 1 of T0[x] is S[x] */
-            uint32_t lo = __builtin_amdgcn_perm(a1, a0, 0x0c0c0501u);
-            uint32_t hi = __builtin_amdgcn_perm(a3, a2, 0x05010c0cu);
-            t[b][j] = xor3(lo, hi, K.rk[4 * NR + j]); /* lo, hi have disjoint bytes */
-        }
-    }
-#pragma unroll
-    for (int b = 0; b < B; ++b)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
-}
-
-template <int NR, int B>
-__device__ __forceinline__ void enc_rounds(const uint32_t *tbl, uint32_t lane4, const otc_aes_key &K,
-                                           uint32_t (&s)[B][4])
-{
-    enc_rounds_from<1, NR, B>(tbl, lane4, K, s);
-}
-
-template <int NR, int B>
-__device__ __forceinline__ void dec_rounds(const uint32_t *tbl, uint32_t lane4, uint32_t lane4_hi,
-                                           const otc_aes_key &K, uint32_t (&s)[B][4])
-{
-#pragma unroll
-    for (int r = 1; r < NR; ++r) {
-        uint32_t t[B][4];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lane4, SEL(0)));
-                uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lane4, SEL(1)));
-                uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lane4, SEL(2)));
-                uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lane4, SEL(3)));
-                t[b][j] = xor3(xor3(a0, rotl8(a1), rotl16(a2)), rotl24(a3), K.rk[4 * r + j]);
-            }
-        }
-#pragma unroll
-        for (int b = 0; b < B; ++b)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
-    }
-    uint32_t t[B][4];
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lane4_hi, SEL_HI(0)));
-            uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lane4_hi, SEL_HI(1)));
-            uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lane4_hi, SEL_HI(2)));
-            uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lane4_hi, SEL_HI(3)));
-            uint32_t lo = __builtin_amdgcn_perm(a1, a0, 0x0c0c0400u);
-            uint32_t hi = __builtin_amdgcn_perm(a3, a2, 0x04000c0cu);
-            t[b][j] = xor3(lo, hi, K.rk[4 * NR + j]); /* lo, hi have disjoint bytes */
-        }
-    }
-#pragma unroll
-    for (int b = 0; b < B; ++b)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
-}
-
 __device__ __forceinline__ uint4 ld16(const uint8_t *p, uint64_t blk)
 {
     return *reinterpret_cast<const uint4 *>(p + 16 * blk);
@@ -326,34 +208,14 @@ __device__ __forceinline__ void st16(uint8_t *p, uint64_t blk, uint4 v)
 {
     *reinterpret_cast<uint4 *>(p + 16 * blk) = v;
 }
-/* streaming (non-temporal) variants: every plaintext/ciphertext byte is
- * touched exactly once */
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-template <bool NT>
-__device__ __forceinline__ uint4 ld16s(const uint8_t *p, uint64_t blk)
-{
-    if (!NT) return ld16(p, blk);
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p + 16 * blk));
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-template <bool NT>
-__device__ __forceinline__ void st16s(uint8_t *p, uint64_t blk, uint4 v)
-{
-    if (!NT) return st16(p, blk, v);
-    const u32x4 w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p + 16 * blk));
-}
-
-enum : int { E_ECB = 0, E_CTR = 1, E_CFB_DEC = 2, E_CFB_DEC_SEG = 3 };
+enum : int { E_ECB = 0, E_CFB_DEC = 2, E_CFB_DEC_SEG = 3 };
 enum : int { D_ECB = 0, D_CBC = 1, D_CBC_SEG = 2 };
 
 struct EncParams {
     const uint8_t *in;
     uint8_t *out;
     uint64_t nfull;   /* full 16-byte blocks */
-    uint32_t tail;    /* bytes of a trailing partial block (CTR) */
-    uint32_t wrap64;  /* CTR: 64-bit (RFC 3686) increment */
-    Ctr128 ctr;       /* CTR: counter; CFB_DEC_SEG: IV of segment 0 (IV_s = ctr + s) */
+    Ctr128 ctr;       /* CFB_DEC_SEG: IV of segment 0 (IV_s = ctr + s) */
     uint32_t iv[4];   /* CFB: IV as LE words */
     uint64_t seg_blocks; /* CFB_DEC_SEG: blocks per segment */
     uint32_t seg_shift;  /* CFB_DEC_SEG: log2(seg_blocks), or 64 if not a power of two */
@@ -370,7 +232,8 @@ struct DecParams {
 };
 
 /* ---------------------------------------------------------------------------
- * Encryption-direction kernel: ECB-enc, CTR, CFB128-dec
+ * Encryption-direction kernel: ECB-enc, CFB128-dec (CTR has its own
+ * counter-caching kernel below)
  * ------------------------------------------------------------------------- */
 template <int NR, int MODE, int B, int THREADS>
 __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key K)
@@ -384,9 +247,8 @@ __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key
     uint32_t lk[4];
     tbl4_lane_consts(lane, lk);
     constexpr uint64_t PER = (uint64_t)THREADS * B;
-    const uint64_t ntotal = P.nfull + (P.tail ? 1u : 0u);
 
-    for (uint64_t base = (uint64_t)blockIdx.x * PER; base < ntotal; base += (uint64_t)gridDim.x * PER) {
+    for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nfull; base += (uint64_t)gridDim.x * PER) {
         const bool full = base + PER <= P.nfull; /* wave-uniform */
         const uint64_t i0 = base + (uint64_t)wave * 64u * B + lane;
         uint32_t s[B][4];
@@ -395,10 +257,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key
         for (int b = 0; b < B; ++b) {
             const uint64_t i = i0 + 64u * b;
             const bool ok = full || i < P.nfull;
-            if (MODE == E_CTR) {
-                ctr_words(P.ctr, i, P.wrap64 != 0, s[b][0], s[b][1], s[b][2], s[b][3]);
-                x[b] = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
-            } else if (MODE == E_ECB) {
+            if (MODE == E_ECB) {
                 uint4 v = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
                 s[b][0] = v.x; s[b][1] = v.y; s[b][2] = v.z; s[b][3] = v.w;
             } else if (MODE == E_CFB_DEC) { /* cipher input is the previous ciphertext */
@@ -431,13 +290,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key
             } else {
                 o = make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]);
             }
-            if (full || i < P.nfull) {
-                st16(P.out, i, o);
-            } else if (MODE == E_CTR && i == P.nfull && P.tail) {
-                const uint32_t ks[4] = {s[b][0], s[b][1], s[b][2], s[b][3]};
-                for (uint32_t n = 0; n < P.tail; ++n)
-                    P.out[16 * i + n] = P.in[16 * i + n] ^ (uint8_t)(ks[n >> 2] >> (8 * (n & 3)));
-            }
+            if (full || i < P.nfull) st16(P.out, i, o);
         }
     }
 }
@@ -467,19 +320,15 @@ struct CtrParams {
 
 __device__ __forceinline__ uint32_t te_u(uint32_t idx) { return g_tab.te0[idx & 0xFFu]; } /* uniform lookup */
 
-template <int NR, int B, int THREADS, bool TBL4, bool ISSUE_ALL = true, bool NT = false>
+template <int NR, int B, int THREADS>
 __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_aes_key K)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t tbl[TBL4 ? 2 * 256 * 64 : 256 * 64];
-    if (TBL4)
-        fill_tbl4<THREADS>(tbl, g_tab.te0);
-    else
-        fill_rep64<THREADS>(tbl, g_tab.te0);
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
+    fill_tbl4<THREADS>(tbl, g_tab.te0);
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane4 = lane << 2;
     uint32_t lk[4];
     tbl4_lane_consts(lane, lk);
     constexpr uint64_t PER = (uint64_t)THREADS * B;
@@ -515,38 +364,26 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_
         for (int b = 0; b < B; ++b) {
             const int64_t i = i0 + 64 * b;
             const bool ok = full || (i >= 0 && (uint64_t)i < P.nfull);
-            x[b] = ok ? ld16s<NT>(P.in, (uint64_t)i) : make_uint4(0, 0, 0, 0);
+            x[b] = ok ? ld16(P.in, (uint64_t)i) : make_uint4(0, 0, 0, 0);
             /* round 1: only T3[byte 15] varies */
             const uint32_t c15 = (b15 | (uint32_t)(64 * b) | lane) ^ (K.rk[3] >> 24);
-            if (TBL4) {
-                const uint32_t s0 = U0 ^ lds_at(tbl, (c15 << 8) | lk[3]);
-                s[b][0] = V0 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[0], SEL_HI(0)));
-                s[b][1] = V1 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[3], SEL_HI(3)));
-                s[b][2] = V2 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[2], SEL_HI(2)));
-                s[b][3] = V3 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[1], SEL_HI(1)));
-            } else {
-                const uint32_t a = lds_at(tbl, (c15 << 8) | lane4);
-                const uint32_t s0 = U0 ^ rotl24(a);
-                /* round 2: the four lookups fed by s0 */
-                s[b][0] = V0 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lane4, SEL(0)));
-                s[b][1] = V1 ^ rotl24(lds_at(tbl, __builtin_amdgcn_perm(s0, lane4, SEL(3))));
-                s[b][2] = V2 ^ rotl16(lds_at(tbl, __builtin_amdgcn_perm(s0, lane4, SEL(2))));
-                s[b][3] = V3 ^ rotl8(lds_at(tbl, __builtin_amdgcn_perm(s0, lane4, SEL(1))));
-            }
+            const uint32_t s0 = U0 ^ lds_at(tbl, (c15 << 8) | lk[3]);
+            /* round 2: the four lookups fed by s0 */
+            s[b][0] = V0 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[0], SEL_HI(0)));
+            s[b][1] = V1 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[3], SEL_HI(3)));
+            s[b][2] = V2 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[2], SEL_HI(2)));
+            s[b][3] = V3 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[1], SEL_HI(1)));
         }
         /* rounds 3..NR */
-        if (TBL4)
-            enc_rounds4_from<3, NR, B, ISSUE_ALL>(tbl, lk, K, s);
-        else
-            enc_rounds_from<3, NR, B>(tbl, lane4, K, s);
+        enc_rounds4_from<3, NR, B>(tbl, lk, K, s);
 
 #pragma unroll
         for (int b = 0; b < B; ++b) {
             const int64_t i = i0 + 64 * b;
             const bool ok = full || (i >= 0 && (uint64_t)i < P.nfull);
             if (ok) {
-                st16s<NT>(P.out, (uint64_t)i,
-                          make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
+                st16(P.out, (uint64_t)i,
+                     make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
             } else if (i >= 0 && (uint64_t)i == P.nfull && P.tail) {
                 const uint32_t ks[4] = {s[b][0], s[b][1], s[b][2], s[b][3]};
                 for (uint32_t n = 0; n < P.tail; ++n)
@@ -935,6 +772,7 @@ __device__ __forceinline__ uint64_t cld64(const uint64_t *p) { return *(cptr64)p
 /* message buffers come from descriptors as plain addresses: access them as
  * GLOBAL memory, or hipcc emits flat_* ops, which count against lgkmcnt and
  * make every LDS wait also wait for HBM */
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 typedef __attribute__((address_space(1))) uint8_t g_u8;
 __device__ __forceinline__ uint4 gld16(const uint8_t *p, uint64_t blk)
@@ -1088,12 +926,9 @@ inline uint64_t busiest_cu_blocks(uint64_t nblocks, uint64_t step)
 }
 inline SmallShape small_shape(uint64_t nblocks)
 {
-    static const bool off = getenv("OTC_TT_NOSMALL") != nullptr; /* A/B */
-    static const bool nomid = getenv("OTC_TT_NOMID") != nullptr;  /* A/B */
-    if (off) return SHAPE_BULK;
     if (nblocks <= 256ull * 256) return SHAPE_256x1;
     if (nblocks <= 256ull * 1024) return SHAPE_1024x1;
-    if (!nomid && busiest_cu_blocks(nblocks, 1024) * 20 <= busiest_cu_blocks(nblocks, 4096) * 19)
+    if (busiest_cu_blocks(nblocks, 1024) * 20 <= busiest_cu_blocks(nblocks, 4096) * 19)
         return SHAPE_1024x1;
     return SHAPE_BULK;
 }
@@ -1105,30 +940,10 @@ constexpr int DEC_B = 4;
 constexpr int SEG_THREADS = 1024;
 constexpr int SEG_B = 2;
 
-/* Tuning variants (threads per workgroup x blocks per lane), selectable with
- * OTC_TT_VARIANT=<threads>x<B> for A/B measurements in one binary. */
-struct TTVariant {
-    int threads, b;
-};
-TTVariant tt_variant()
-{
-    static TTVariant v = [] {
-        TTVariant d{ENC_THREADS, ENC_B};
-        const char *e = getenv("OTC_TT_VARIANT");
-        if (e) {
-            int t = 0, b = 0;
-            if (sscanf(e, "%dx%d", &t, &b) == 2) d = TTVariant{t, b};
-        }
-        return d;
-    }();
-    return v;
-}
-
 template <int NR, int MODE, int T, int B>
 hipError_t launch_enc_tb(const EncParams &P, const otc_aes_key &K, hipStream_t st)
 {
-    const uint64_t nt = P.nfull + (P.tail ? 1 : 0);
-    int grid = grid_for(nt, (uint64_t)T * B, 1); /* 128 KiB LDS: one workgroup per CU */
+    int grid = grid_for(P.nfull, (uint64_t)T * B, 1); /* 128 KiB LDS: one workgroup per CU */
     hipLaunchKernelGGL((k_aes_enc_tt<NR, MODE, B, T>), dim3(grid), dim3(T), 0, st, P, K);
     return hipGetLastError();
 }
@@ -1136,10 +951,7 @@ hipError_t launch_enc_tb(const EncParams &P, const otc_aes_key &K, hipStream_t s
 template <int NR, int MODE>
 hipError_t launch_enc_nr(const EncParams &P, const otc_aes_key &K, hipStream_t st)
 {
-    const TTVariant v = tt_variant();
-    if (v.threads == 1024 && v.b == 2) return launch_enc_tb<NR, MODE, 1024, 2>(P, K, st);
-    if (v.threads == 512 && v.b == 4) return launch_enc_tb<NR, MODE, 512, 4>(P, K, st);
-    switch (small_shape(P.nfull + (P.tail ? 1 : 0))) {
+    switch (small_shape(P.nfull)) {
     case SHAPE_256x1: return launch_enc_tb<NR, MODE, 256, 1>(P, K, st);
     case SHAPE_1024x1: return launch_enc_tb<NR, MODE, 1024, 1>(P, K, st);
     default: return launch_enc_tb<NR, MODE, ENC_THREADS, ENC_B>(P, K, st);
@@ -1190,12 +1002,11 @@ template <int NR, bool CFB>
 hipError_t launch_seg_nr(const CbcSegParams &P, const otc_aes_key &K, hipStream_t st)
 {
     int grid = grid_for(P.nseg, (uint64_t)SEG_THREADS * SEG_B, 1);
-    /* OTC_CBC_GROUP: blocks per load/store burst (1 = the per-block kernel) */
-    static const int grp = getenv("OTC_CBC_GROUP") ? atoi(getenv("OTC_CBC_GROUP")) : 8;
-    if (grp == 4 && P.seg_blocks >= 4)
-        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, SEG_B, SEG_THREADS, 4, CFB>), dim3(grid), dim3(SEG_THREADS), 0, st,
-                           P, K);
-    else if (grp == 8 && P.seg_blocks >= 8) /* B = 1: two 8-block buffers per segment fit without spills */
+    /* 8-block load/store bursts per segment (+119% over one block at a time,
+     * profiles/r1/otbench_cbcenc_group_ab.jsonl); B = 1: two 8-block buffers
+     * per segment fit without spills.  Segments shorter than 8 blocks take the
+     * per-block kernel. */
+    if (P.seg_blocks >= 8)
         hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, 1, SEG_THREADS, 8, CFB>),
                            dim3(grid_for(P.nseg, (uint64_t)SEG_THREADS, 1)), dim3(SEG_THREADS), 0, st, P, K);
     else
@@ -1250,69 +1061,44 @@ hipError_t tt_ecb_encrypt(const void *in, void *out, uint64_t nblocks, const otc
     return launch_enc<E_ECB>(P, K, st);
 }
 
-/* wg_per_cu: resident workgroups per CU of the 1-table layouts (2; 1 while a
- * co-resident bitsliced kernel runs, hybrid impl).  A launch parameter, not
- * process state: the multi-GPU paths launch from one host thread per GPU. */
-template <int NR, int T, int B, bool TBL4 = false, bool ISSUE_ALL = true, bool NT = false>
-hipError_t launch_ctr_cached_tb(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo, int wg_per_cu, hipStream_t st)
+/* one 1024- or 256-thread workgroup per CU (the 128 KiB 4-table image) */
+template <int NR, int T, int B>
+hipError_t launch_ctr_cached_tb(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo, hipStream_t st)
 {
     constexpr uint64_t PER = (uint64_t)T * B;
     P.shift = ctr_lo & (PER - 1);
     P.cbase.lo = ctr_lo - P.shift;
     const uint64_t vt = P.nfull + (P.tail ? 1 : 0) + P.shift;
-    int grid = grid_for(vt, PER, TBL4 ? 1 : wg_per_cu);
-    hipLaunchKernelGGL((k_aes_ctr_tt_cached<NR, B, T, TBL4, ISSUE_ALL, NT>), dim3(grid), dim3(T), 0, st, P, K);
+    hipLaunchKernelGGL((k_aes_ctr_tt_cached<NR, B, T>), dim3(grid_for(vt, PER, 1)), dim3(T), 0, st, P, K);
     return hipGetLastError();
 }
 
 template <int NR>
-hipError_t launch_ctr_cached(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo, int wpc, hipStream_t st)
+hipError_t launch_ctr_cached(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo, hipStream_t st)
 {
-    /* OTC_TT_VARIANT=<threads>x<B>: negative threads = 1-table layout (A/B
-     * measurements); default = 4-table layout, 1024 threads x 4 blocks/lane */
-    const TTVariant v = tt_variant();
-    /* OTC_TT_NT=1: non-temporal plaintext loads / ciphertext stores (A/B) */
-    static const bool nt = getenv("OTC_TT_NT") && atoi(getenv("OTC_TT_NT")) != 0;
-    if (nt) return launch_ctr_cached_tb<NR, 1024, 4, true, true, true>(P, K, ctr_lo, wpc, st);
-    if (v.threads == 1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, true>(P, K, ctr_lo, wpc, st);
-    if (v.threads == 2 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, true, false>(P, K, ctr_lo, wpc, st);
-    if (v.threads == 512 && v.b == 4) return launch_ctr_cached_tb<NR, 512, 4, true>(P, K, ctr_lo, wpc, st);
-    if (v.threads == -1024 && v.b == 4) return launch_ctr_cached_tb<NR, 1024, 4, false>(P, K, ctr_lo, wpc, st);
-    if (v.threads == -1024 && v.b == 2) return launch_ctr_cached_tb<NR, 1024, 2, false>(P, K, ctr_lo, wpc, st);
     switch (small_shape(P.nfull + (P.tail ? 1 : 0))) {
-    case SHAPE_256x1: return launch_ctr_cached_tb<NR, 256, 1, true>(P, K, ctr_lo, wpc, st);
-    case SHAPE_1024x1: return launch_ctr_cached_tb<NR, 1024, 1, true>(P, K, ctr_lo, wpc, st);
-    default: return launch_ctr_cached_tb<NR, 1024, 4, true>(P, K, ctr_lo, wpc, st);
+    case SHAPE_256x1: return launch_ctr_cached_tb<NR, 256, 1>(P, K, ctr_lo, st);
+    case SHAPE_1024x1: return launch_ctr_cached_tb<NR, 1024, 1>(P, K, ctr_lo, st);
+    default: return launch_ctr_cached_tb<NR, 1024, 4>(P, K, ctr_lo, st);
     }
 }
 
 hipError_t tt_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
-                  hipStream_t st, int wg_per_cu)
+                  hipStream_t st)
 {
-    const int wpc = wg_per_cu < 1 ? 1 : wg_per_cu;
-    if (getenv("OTC_TT_NOCACHE") == nullptr) {
-        CtrParams P{};
-        P.in = (const uint8_t *)in;
-        P.out = (uint8_t *)out;
-        P.nfull = nbytes / 16;
-        P.tail = (uint32_t)(nbytes % 16);
-        P.wrap64 = wrap64 ? 1u : 0u;
-        P.cbase.hi = c.hi;
-        switch (K.nr) {
-        case 10: return launch_ctr_cached<10>(P, K, c.lo, wpc, st);
-        case 12: return launch_ctr_cached<12>(P, K, c.lo, wpc, st);
-        case 14: return launch_ctr_cached<14>(P, K, c.lo, wpc, st);
-        default: return hipErrorInvalidValue;
-        }
-    }
-    EncParams P{};
+    CtrParams P{};
     P.in = (const uint8_t *)in;
     P.out = (uint8_t *)out;
     P.nfull = nbytes / 16;
     P.tail = (uint32_t)(nbytes % 16);
     P.wrap64 = wrap64 ? 1u : 0u;
-    P.ctr = c;
-    return launch_enc<E_CTR>(P, K, st);
+    P.cbase.hi = c.hi;
+    switch (K.nr) {
+    case 10: return launch_ctr_cached<10>(P, K, c.lo, st);
+    case 12: return launch_ctr_cached<12>(P, K, c.lo, st);
+    case 14: return launch_ctr_cached<14>(P, K, c.lo, st);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t tt_cfb_decrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K,

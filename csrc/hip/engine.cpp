@@ -41,7 +41,7 @@ using otc_dev::Ctr128;
 namespace otc_impl {
 hipError_t tt_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
 hipError_t tt_ecb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
-hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t, int wg_per_cu = 2);
+hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
 hipError_t tt_cfb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, hipStream_t);
 hipError_t tt_cbc_decrypt(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t tt_cbc_decrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
@@ -59,6 +59,7 @@ hipError_t k_fill_random(void *, size_t, uint64_t, hipStream_t);
 hipError_t k_checksum(const void *, size_t, uint64_t *, hipStream_t);
 hipError_t k_clock(uint64_t *, uint64_t, uint64_t, hipStream_t);
 hipError_t k_rc4_multi(const uint8_t *, int, size_t, size_t, size_t, const void *, void *, hipStream_t);
+hipError_t k_rc4_states(void *, size_t, size_t, const void *, void *, hipStream_t);
 } // namespace otc_impl
 
 /* ------------------------------------------------------------------------- */
@@ -127,28 +128,38 @@ using namespace otc_rt;
 
 namespace {
 
-/* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  CTR over >= 4 GiB with
- * AES-192/256 runs bitsliced (64 GiB in place: AES-256 1165-1168 vs 1119-1121
- * GB/s, AES-192 1317-1321 vs 1311-1312; 4 GiB: 1101 vs 1046-1053 and 1251 vs
- * 1235; at 2 GiB AES-192 and at 1 GiB both still favour the T-table, whose
- * persistent grid has no per-call table kernels); AES-128 CTR (the two kernels at
- * parity; the hybrid split measured +0.5..1.3% on one box and -0.3..+1.3% on
- * another, within box noise, so the single T-table kernel stays), every
- * other mode and smaller calls (the bitsliced grid needs ~768 workgroups of
- * 128 KiB to fill the chip, plus two table kernels per call) take the
- * T-table.  ctr_bytes = 0 for non-CTR calls. */
+/* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  Bulk CTR with
+ * AES-192/256 runs bitsliced: AES-256 from 2 GiB (2 GiB: 1074 vs 1066 GB/s in
+ * both reps, profiles/r2/auto_impl/ab_ctr192_256_2g_4g.txt; 64 GiB: 1165-1168
+ * vs 1119-1121), AES-192 from 4 GiB (2 GiB still favours the T-table, 1247 vs
+ * 1206; 64 GiB 1317-1321 vs 1311-1312).  AES-128 CTR (the two kernels at
+ * parity), every other mode and smaller calls (the bitsliced grid needs ~768
+ * workgroups to fill the chip, plus two table kernels per call) take the
+ * T-table.  ctr_bytes = 0 for non-CTR calls.  OTC_IMPL=ttable|bitslice
+ * overrides "auto" for the whole process. */
 int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
 {
-    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_HYBRID) return impl;
-    const char *env = getenv("OTC_IMPL");
-    if (env) {
-        if (!strcmp(env, "ttable")) return OTC_IMPL_TTABLE;
-        if (!strcmp(env, "bitslice")) return OTC_IMPL_BITSLICE;
-        if (!strcmp(env, "hybrid")) return OTC_IMPL_HYBRID;
-    }
-    if (bits >= 192 && ctr_bytes >= ((size_t)4 << 30)) return OTC_IMPL_BITSLICE;
+    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE) return impl;
+    static const int env = [] {
+        const char *e = getenv("OTC_IMPL");
+        if (e && !strcmp(e, "ttable")) return OTC_IMPL_TTABLE;
+        if (e && !strcmp(e, "bitslice")) return OTC_IMPL_BITSLICE;
+        return OTC_IMPL_AUTO;
+    }();
+    if (env != OTC_IMPL_AUTO) return env;
+    if (bits == 256 && ctr_bytes >= ((size_t)2 << 30)) return OTC_IMPL_BITSLICE;
+    if (bits == 192 && ctr_bytes >= ((size_t)4 << 30)) return OTC_IMPL_BITSLICE;
     return OTC_IMPL_TTABLE;
 }
+
+int check_impl(int impl)
+{
+    if (impl == OTC_IMPL_AUTO || impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE) return OTC_OK;
+    return set_err(OTC_ERR_ARG, "impl must be OTC_IMPL_AUTO, OTC_IMPL_TTABLE or OTC_IMPL_BITSLICE");
+}
+
+/* the kernel family the calling thread's last AES call ran (otc_last_impl) */
+thread_local int g_last_impl = OTC_IMPL_AUTO;
 
 /* Device buffers of the cipher ops: non-null, 16-byte aligned (every kernel
  * moves 16 B per lane with global_load/store_dwordx4), and either the same
@@ -195,6 +206,14 @@ extern "C" int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, in
     return OTC_OK;
 }
 
+extern "C" int otc_pick_impl(int impl, int bits, int mode_ctr, uint64_t nbytes)
+{
+    if (check_impl(impl)) return -1;
+    return pick_impl(impl, bits, mode_ctr ? (size_t)nbytes : 0);
+}
+
+extern "C" int otc_last_impl(void) { return g_last_impl; }
+
 /* ---- device ops --------------------------------------------------------- */
 extern "C" int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_aes_key *k, int impl,
                            void *stream)
@@ -203,132 +222,20 @@ extern "C" int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_a
     if (nbytes % 16) return set_err(OTC_ERR_ARG, "ECB length must be a multiple of 16");
     if (!k) return set_err(OTC_ERR_ARG, "null key");
     if (int r = check_bufs(in, out, nbytes, true, "aes_ecb")) return r;
+    if (int r = check_impl(impl)) return r;
     if (nbytes == 0) return OTC_OK;
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     if (k->dir == OTC_DIR_ENCRYPT) {
-        e = (pick_impl(impl, k->bits) == OTC_IMPL_BITSLICE) ? otc_impl::bs_ecb_encrypt(in, out, nbytes / 16, *k, st)
-                                                            : otc_impl::tt_ecb_encrypt(in, out, nbytes / 16, *k, st);
+        g_last_impl = pick_impl(impl, k->bits);
+        e = g_last_impl == OTC_IMPL_BITSLICE ? otc_impl::bs_ecb_encrypt(in, out, nbytes / 16, *k, st)
+                                             : otc_impl::tt_ecb_encrypt(in, out, nbytes / 16, *k, st);
     } else {
+        g_last_impl = OTC_IMPL_TTABLE;
         e = otc_impl::tt_ecb_decrypt(in, out, nbytes / 16, *k, st);
     }
     if (e != hipSuccess) return hip_fail(e, "aes_ecb launch");
     return OTC_OK;
-}
-
-/* Hybrid CTR: the T-table kernel (LDS-bound, ~40% VALU) and the bitsliced
- * kernel (VALU-only) run CONCURRENTLY on two streams over disjoint ranges.
- * With OTC_TT_VARIANT=1024x2 (64 VGPRs x 4 waves) or 512x4 (112 x 2) each CU
- * hosts one T-table workgroup beside one 256-VGPR bitsliced wave per SIMD.
- * OTC_HYBRID_TT = fraction of blocks given to the T-table kernel.  Measured
- * slower than the T-table alone (docs/PERF.md): kept as an option. */
-struct AuxStream {
-    int dev = -1;
-    hipStream_t s = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-};
-
-/* Auxiliary streams for the hybrid split, pooled per device: a call takes one
- * (creating it on first use), enqueues, and returns it -- so concurrent
- * callers (one host thread per GPU in otc_multi_run) never share the events
- * they order on.  otc_release_resources() destroys the pool. */
-std::mutex g_aux_mu;
-std::vector<AuxStream> g_aux_free;
-
-static hipError_t aux_take(int dev, AuxStream &out)
-{
-    {
-        std::lock_guard<std::mutex> lk(g_aux_mu);
-        for (size_t i = 0; i < g_aux_free.size(); ++i)
-            if (g_aux_free[i].dev == dev) {
-                out = g_aux_free[i];
-                g_aux_free.erase(g_aux_free.begin() + (long)i);
-                return hipSuccess;
-            }
-    }
-    AuxStream a;
-    hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&a.e0, hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&a.e1, hipEventDisableTiming)) != hipSuccess) return e;
-    a.dev = dev;
-    out = a;
-    return hipSuccess;
-}
-
-static void aux_give(const AuxStream &a)
-{
-    std::lock_guard<std::mutex> lk(g_aux_mu);
-    g_aux_free.push_back(a);
-}
-
-void otc_rt::aux_release_all()
-{
-    std::lock_guard<std::mutex> lk(g_aux_mu);
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    for (AuxStream &a : g_aux_free) {
-        (void)hipSetDevice(a.dev);
-        if (a.s) (void)hipStreamSynchronize(a.s);
-        if (a.e0) (void)hipEventDestroy(a.e0);
-        if (a.e1) (void)hipEventDestroy(a.e1);
-        if (a.s) (void)hipStreamDestroy(a.s);
-    }
-    g_aux_free.clear();
-    (void)hipSetDevice(cur);
-}
-
-static hipError_t hybrid_ctr_on(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
-                                hipStream_t st, AuxStream &a);
-
-hipError_t hybrid_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
-                      hipStream_t st)
-{
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    AuxStream a;
-    if ((e = aux_take(dev, a)) != hipSuccess) return e;
-    e = hybrid_ctr_on(in, out, nbytes, K, c, wrap64, st, a);
-    aux_give(a); /* reusable as soon as the work is enqueued: stream order */
-    return e;
-}
-
-static hipError_t hybrid_ctr_on(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
-                                hipStream_t st, AuxStream &a)
-{
-    hipError_t e;
-    /* T-table share of the blocks (64 GiB AES-128 in place, 2 reps each:
-     * 0.75 1547/1558, 0.8 1556/1556, 0.85 1564/1565, 0.9 1564/1553 GB/s;
-     * T-table alone 1544/1548); OTC_HYBRID_TT overrides */
-    double frac = 0.85;
-    if (const char *f = getenv("OTC_HYBRID_TT")) frac = atof(f);
-    const uint64_t nblk = nbytes / 16;
-    uint64_t ntt = (uint64_t)(nblk * frac);
-    ntt -= ntt % 2048;
-    if (ntt > nblk) ntt = nblk;
-    const size_t tt_bytes = ntt * 16;
-    /* order the aux stream after prior work on st */
-    if ((e = hipEventRecord(a.e0, st)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(a.s, a.e0, 0)) != hipSuccess) return e;
-    Ctr128 c2 = c;
-    c2.lo = c.lo + ntt;
-    if (!wrap64 && c2.lo < c.lo) c2.hi += 1;
-    /* persistent T-table grid (1 workgroup per CU) first, so its workgroups
-     * are resident before the bitsliced waves fill the remaining VGPRs */
-    if (tt_bytes) {
-        /* the T-table variant for co-residency is chosen by OTC_TT_VARIANT
-         * (B=2 keeps it at <= 64 VGPRs so a 256-VGPR bitsliced wave fits) */
-        e = otc_impl::tt_ctr(in, out, tt_bytes, K, c, wrap64, st, 1);
-        if (e != hipSuccess) return e;
-    }
-    if (nbytes > tt_bytes) {
-        e = otc_impl::bs_ctr((const uint8_t *)in + tt_bytes, (uint8_t *)out + tt_bytes, nbytes - tt_bytes, K, c2,
-                             wrap64, a.s);
-        if (e != hipSuccess) return e;
-    }
-    if ((e = hipEventRecord(a.e1, a.s)) != hipSuccess) return e;
-    return hipStreamWaitEvent(st, a.e1, 0);
 }
 
 static int ctr_common(const void *in, void *out, size_t nbytes, const otc_aes_key *k, Ctr128 c, bool wrap64,
@@ -338,10 +245,11 @@ static int ctr_common(const void *in, void *out, size_t nbytes, const otc_aes_ke
     if (r) return r;
     if ((r = check_bufs(in, out, nbytes, true, "aes_ctr"))) return r;
     if (nbytes == 0) return OTC_OK;
+    if ((r = check_impl(impl))) return r;
     hipStream_t st = (hipStream_t)stream;
     const int im = pick_impl(impl, k->bits, nbytes);
+    g_last_impl = im;
     hipError_t e = im == OTC_IMPL_BITSLICE ? otc_impl::bs_ctr(in, out, nbytes, *k, c, wrap64, st)
-                   : im == OTC_IMPL_HYBRID ? hybrid_ctr(in, out, nbytes, *k, c, wrap64, st)
                                            : otc_impl::tt_ctr(in, out, nbytes, *k, c, wrap64, st);
     if (e != hipSuccess) return hip_fail(e, "aes_ctr launch");
     return OTC_OK;
@@ -604,6 +512,23 @@ extern "C" int otc_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, s
     }
     hipError_t e = otc_impl::k_rc4_multi(keys, keylen, nstreams, len, drop, in, out, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "rc4_multi launch");
+    return OTC_OK;
+}
+
+extern "C" int otc_rc4_crypt_batch(void *states, size_t nstreams, size_t len, const void *in, void *out,
+                                   void *stream)
+{
+    Range rg("otc_rc4_crypt_batch");
+    if (nstreams == 0 || len == 0) return OTC_OK;
+    if (!states || !in || !out) return set_err(OTC_ERR_ARG, "rc4_crypt_batch: null buffer");
+    if ((uintptr_t)states & 3u) return set_err(OTC_ERR_ARG, "rc4_crypt_batch: states must be 4-byte aligned");
+    if (len > SIZE_MAX / nstreams) return set_err(OTC_ERR_ARG, "size overflow");
+    if (in != out) {
+        const uintptr_t a = (uintptr_t)in, b = (uintptr_t)out, n = nstreams * len;
+        if (a < b + n && b < a + n) return set_err(OTC_ERR_ARG, "rc4_crypt_batch: input and output overlap partially");
+    }
+    hipError_t e = otc_impl::k_rc4_states(states, nstreams, len, in, out, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "rc4_crypt_batch launch");
     return OTC_OK;
 }
 

@@ -43,9 +43,6 @@ inline hipError_t dev_alloc(void **p, size_t n)
     return hipMalloc(p, n);
 }
 
-/* releases the hybrid-CTR auxiliary stream pool (engine.cpp) */
-void aux_release_all();
-
 } // namespace otc_rt
 
 #define HIPCHK(expr)                                                  \

@@ -258,6 +258,22 @@ extern "C" int otc_engine_run(otc_engine *e, int mode, const void *host_in, void
     if (int r = check_stream_args(mode, host_in, host_out, nbytes, k, ivc)) return r;
     if (mode == OTC_MODE_CBC_DEC && block_offset) return set_err(OTC_ERR_ARG, "CBC: pass the halo as iv instead");
     HIPCHK(hipSetDevice(e->device));
+    /* Every error return below leaves earlier H2D / kernel / D2H work queued
+     * on the engine's streams, and with a pinned host_out those D2H copies
+     * would land in caller memory after the error is reported (a caller that
+     * frees the buffer on error: use after free).  Drain the streams on any
+     * early return; the success path has retired every chunk already. */
+    struct DrainOnError {
+        otc_engine *e;
+        bool armed = true;
+        ~DrainOnError()
+        {
+            if (!armed) return;
+            for (hipStream_t s : {e->s_h2d, e->s_k, e->s_d2h})
+                if (s) (void)hipStreamSynchronize(s);
+            (void)hipGetLastError();
+        }
+    } drain{e};
     auto t0 = std::chrono::steady_clock::now();
     const bool pin_in = is_pinned(host_in), pin_out = is_pinned(host_out);
     for (int i = 0; i < e->depth; ++i) {
@@ -332,6 +348,7 @@ extern "C" int otc_engine_run(otc_engine *e, int mode, const void *host_in, void
         stats->chunks = (int)nchunks;
         stats->numa_node = e->numa_node;
     }
+    drain.armed = false;
     return OTC_OK;
 }
 
@@ -569,6 +586,15 @@ static int rccl_scatter_gather(int ngpus, int mode, const uint8_t *hin, uint8_t 
 {
     const char *to = getenv("OTC_RCCL_TIMEOUT_S");
     const double timeout_s = to ? atof(to) : 600.0;
+    /* every H2D / D2H of this job is enqueued from this one thread: with
+     * pageable host memory each copy blocks it and the pipeline serialises */
+    if (otc_ptr_kind(hin) == OTC_PTR_HOST || otc_ptr_kind(hout) == OTC_PTR_HOST) {
+        static std::once_flag once;
+        std::call_once(once, [] {
+            fprintf(stderr, "otc_multi_run(strategy 1): pageable host buffers -- the root's copies block and the "
+                            "pipeline serialises; pin them (otc_host_alloc_pinned / otc_host_register)\n");
+        });
+    }
     size_t S = chunk_bytes ? chunk_bytes : (size_t)64 << 20; /* per-GPU bytes per round */
     S = (S + 15) & ~(size_t)15;
     std::lock_guard<std::mutex> lk(g_rccl_mu);
@@ -610,7 +636,6 @@ extern "C" void otc_multi_release(void)
 extern "C" void otc_release_resources(void)
 {
     otc_multi_release();
-    aux_release_all();
 }
 
 /* Logical shards -> devices: shard g runs on device g, or g % ndev when

@@ -24,25 +24,12 @@
 
 namespace {
 
-/* U independent 16-byte loads per lane per trip (all issued before any
- * store) keep more HBM requests in flight per wave than one; NT selects
- * non-temporal loads/stores (once-touched data).  The variant is chosen at
- * run time by k_xor() (A/B: profiles/r1/otbench_xor_variants.jsonl). */
+/* One 16-byte load of each input per lane per trip: the stream already runs
+ * at the HBM rate a read-read-write stream reaches here (~5 TB/s of traffic);
+ * 2-8 loads per trip, 4-32 workgroups per CU and non-temporal accesses all
+ * measured within noise (profiles/r1/otbench_xor_variants.jsonl). */
 typedef uint32_t xu32x4 __attribute__((ext_vector_type(4)));
-template <bool NT>
-__device__ __forceinline__ xu32x4 xor_ld(const xu32x4 *p)
-{
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-template <bool NT>
-__device__ __forceinline__ void xor_st(xu32x4 v, xu32x4 *p)
-{
-    if constexpr (NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
 
-template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_xor_kernel(const uint8_t *a, const uint8_t *b, uint8_t *o, uint64_t n)
 {
     const uint64_t n16 = n / 16;
@@ -50,19 +37,7 @@ __global__ __launch_bounds__(256) void k_xor_kernel(const uint8_t *a, const uint
     const xu32x4 *B = reinterpret_cast<const xu32x4 *>(b);
     xu32x4 *O = reinterpret_cast<xu32x4 *>(o);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    /* full trips: U strided elements per lane, all in range */
-    for (; i + (U - 1) * stride < n16; i += U * stride) {
-        xu32x4 x[U], y[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            x[u] = xor_ld<NT>(A + i + u * stride);
-            y[u] = xor_ld<NT>(B + i + u * stride);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) xor_st<NT>(x[u] ^ y[u], O + i + u * stride);
-    }
-    for (; i < n16; i += stride) xor_st<NT>(xor_ld<NT>(A + i) ^ xor_ld<NT>(B + i), O + i);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) O[i] = A[i] ^ B[i];
     if (blockIdx.x == 0 && threadIdx.x < (n & 15)) {
         const uint64_t j = n16 * 16 + threadIdx.x;
         o[j] = a[j] ^ b[j];
@@ -111,18 +86,11 @@ __device__ __forceinline__ uint32_t sbox_addr(uint32_t x, uint32_t lane4)
     return t | (x & 3u) | lane4;
 }
 
-/* RC4 S-box address, two layouts (kernel template AL >= 3 selects BL):
- *   BL = false: byte x of lane l at ((x>>2)<<8) | l<<2 | (x&3) -- every lane
- *               owns a bank (conflict-free), 3 VALU per address;
- *   BL = true:  byte x of lane l at (x<<6) | l -- 1-2 VALU per address; the 4
- *               lanes of a dword share a bank, so equal x&3 with different
- *               rows conflict (~2-way on random data).
- * `lt` is the lane term (l<<2 or l). */
-template <bool BL>
-__device__ __forceinline__ uint32_t rc4_addr(uint32_t x, uint32_t lt)
-{
-    return BL ? (((x & 0xFFu) << 6) | lt) : sbox_addr(x, lt);
-}
+/* RC4 S-box address: byte x of lane l at ((x>>2)<<8) | l<<2 | (x&3) -- every
+ * lane owns a bank (conflict-free for any data).  A byte-interleaved layout
+ * ((x<<6) | l, fewer VALU per address, ~2-way conflicts) measured slower
+ * (profiles/r1/otbench_rc4_bytelayout_negative.jsonl). */
+__device__ __forceinline__ uint32_t rc4_addr(uint32_t x, uint32_t lane4) { return sbox_addr(x, lane4); }
 
 /* Output modes: RC4_KS = keystream only (no input); RC4_VEC = input, in/out
  * 16-byte aligned and len a multiple of 16 (host-checked), so every lane
@@ -207,28 +175,25 @@ __device__ __forceinline__ void rc4_store16_any(const uint8_t *in, uint8_t *out,
  * offset from one per-chunk lane address -- the i side of every step becomes a
  * ds_read_u8 / ds_write_b8 immediate offset, with no SALU index arithmetic and
  * no VALU address op (the loop is issue-bound at ~2 waves per SIMD). */
-template <bool BL>
-__device__ __forceinline__ constexpr uint32_t rc4_ioff(int m)
-{
-    return BL ? (uint32_t)m << 6 : ((uint32_t)(m >> 2) << 8) | (uint32_t)(m & 3);
-}
+__device__ __forceinline__ constexpr uint32_t rc4_ioff(int m) { return ((uint32_t)(m >> 2) << 8) | (uint32_t)(m & 3); }
 
-template <int MODE, int AL>
-__device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i, uint32_t j, uint64_t len,
+/* AL: i-aligned loops with the S[i+1] read-ahead (drop % 16 == 0, the
+ * default; +5-7% over the generic loop, profiles/r1/otbench_rc4_readahead_ab.jsonl) */
+template <int MODE, bool AL>
+__device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t &i, uint32_t &j, uint64_t len,
                                                const uint8_t *in, uint8_t *out, uint64_t base, bool live)
 {
-    constexpr bool BL = AL >= 3;
 #define RC4_STEP(O)                                                                                            \
     do {                                                                                                       \
         i = (i + 1) & 0xFFu;                                                                                   \
-        const uint32_t ai_ = rc4_addr<BL>(i, lane4);                                                              \
+        const uint32_t ai_ = rc4_addr(i, lane4);                                                              \
         const uint32_t a_ = S[ai_];                                                                            \
         j = (j + a_) & 0xFFu;                                                                                  \
-        const uint32_t aj_ = rc4_addr<BL>(j, lane4);                                                              \
+        const uint32_t aj_ = rc4_addr(j, lane4);                                                              \
         const uint32_t b_ = S[aj_];                                                                            \
         S[ai_] = (uint8_t)b_;                                                                                  \
         S[aj_] = (uint8_t)a_;                                                                                  \
-        O = S[rc4_addr<BL>(a_ + b_, lane4)];                                                                      \
+        O = S[rc4_addr(a_ + b_, lane4)];                                                                      \
     } while (0)
 #define RC4_GEN16(w)                                                                                           \
     _Pragma("unroll") for (int q = 0; q < 16; ++q)                                                             \
@@ -237,34 +202,9 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i,
         RC4_STEP(o);                                                                                           \
         w[q >> 2] |= o << (8 * (q & 3));                                                                       \
     }
-#define RC4_STEP_AT(O, SI, OFF)                                                                                \
-    do {                                                                                                       \
-        const uint32_t a_ = (SI)[OFF];                                                                         \
-        j = (j + a_) & 0xFFu;                                                                                  \
-        const uint32_t aj_ = rc4_addr<BL>(j, lane4);                                                              \
-        const uint32_t b_ = S[aj_];                                                                            \
-        (SI)[OFF] = (uint8_t)b_;                                                                               \
-        S[aj_] = (uint8_t)a_;                                                                                  \
-        O = S[rc4_addr<BL>(a_ + b_, lane4)];                                                                      \
-    } while (0)
-#define RC4_GEN16A(w)                                                                                          \
-    {                                                                                                          \
-        uint8_t *Sk = S + ((k << 10) | lane4);                                                                 \
-        k = (k + 1) & 15u;                                                                                     \
-        uint8_t *Sn = S + ((k << 10) | lane4);                                                                 \
-        _Pragma("unroll") for (int q = 0; q < 15; ++q)                                                         \
-        {                                                                                                      \
-            uint32_t o;                                                                                        \
-            RC4_STEP_AT(o, Sk, rc4_ioff<BL>(q + 1));                                                               \
-            w[q >> 2] |= o << (8 * (q & 3));                                                                   \
-        }                                                                                                      \
-        uint32_t o15;                                                                                          \
-        RC4_STEP_AT(o15, Sn, 0);                                                                               \
-        w[3] |= o15 << 24;                                                                                     \
-    }
-    /* AL == 2 (default): S[i+1] read ahead together with S[j], before the swap
- * writes, and corrected when the swap moved it (i + 1 == j -> a), so the j
- * chain carries one LDS round trip per byte instead of two. */
+    /* AL: S[i+1] read ahead together with S[j], before the swap writes, and
+     * corrected when the swap moved it (i + 1 == j -> a), so the j chain
+     * carries one LDS round trip per byte instead of two. */
 #define RC4_GEN16P(w)                                                                                          \
     {                                                                                                          \
         uint8_t *Sk = S + ((k << 10) | lane4);                                                                 \
@@ -274,29 +214,25 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i,
         const uint32_t nb = k << 4;                                                                            \
         _Pragma("unroll") for (int q = 0; q < 16; ++q)                                                         \
         {                                                                                                      \
-            uint8_t *si_ = q < 15 ? Sk + rc4_ioff<BL>(q + 1) : Sn;                                                 \
-            uint8_t *sp_ = q < 14 ? Sk + rc4_ioff<BL>(q + 2) : (q == 14 ? Sn : Sn + rc4_ioff<BL>(1));                            \
+            uint8_t *si_ = q < 15 ? Sk + rc4_ioff(q + 1) : Sn;                                                 \
+            uint8_t *sp_ = q < 14 ? Sk + rc4_ioff(q + 2) : (q == 14 ? Sn : Sn + rc4_ioff(1));                            \
             const uint32_t a_ = an;                                                                            \
             j = (j + a_) & 0xFFu;                                                                              \
-            const uint32_t aj_ = rc4_addr<BL>(j, lane4);                                                          \
+            const uint32_t aj_ = rc4_addr(j, lane4);                                                          \
             const uint32_t b_ = S[aj_];                                                                        \
             const uint32_t pn_ = *sp_;                                                                         \
             const uint32_t inx_ = q < 14 ? ib + (uint32_t)(q + 2) : nb + (uint32_t)(q - 14);                   \
             an = (j == inx_) ? a_ : pn_;                                                                       \
             *si_ = (uint8_t)b_;                                                                                \
             S[aj_] = (uint8_t)a_;                                                                              \
-            const uint32_t o_ = S[rc4_addr<BL>(a_ + b_, lane4)];                                                  \
+            const uint32_t o_ = S[rc4_addr(a_ + b_, lane4)];                                                  \
             w[q >> 2] |= o_ << (8 * (q & 3));                                                                  \
         }                                                                                                      \
     }
     uint64_t m = 0;
-    if constexpr (AL == 1) {
+    if constexpr (AL) {
         uint32_t k = (i >> 4) & 15u; /* i % 16 == 0 here (host checks drop % 16) */
-        RC4_MAIN_LOOP(16, RC4_GEN16A)
-        i = k << 4;
-    } else if constexpr (AL >= 2) {
-        uint32_t k = (i >> 4) & 15u;
-        uint32_t an = S[((k << 10) | lane4) + rc4_ioff<BL>(1)]; /* S[i + 1] */
+        uint32_t an = S[((k << 10) | lane4) + rc4_ioff(1)]; /* S[i + 1] */
         RC4_MAIN_LOOP(16, RC4_GEN16P)
         i = k << 4;
     } else {
@@ -308,44 +244,35 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t i,
         rc4_emit(in, out, base + m, o, live);
     }
 #undef RC4_GEN16P
-#undef RC4_GEN16A
-#undef RC4_STEP_AT
 #undef RC4_GEN16
 #undef RC4_STEP
 }
 
 #undef RC4_MAIN_LOOP
 
-template <int MODE, int AL>
+template <int MODE, bool AL>
 __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keylen, uint64_t nstreams, uint64_t len,
-                                                   uint64_t drop, const uint8_t *in, uint8_t *out, int ksa16)
+                                                   uint64_t drop, const uint8_t *in, uint8_t *out)
 {
     __shared__ __attribute__((aligned(16))) uint8_t S[64 * 256];
     const uint32_t lane = threadIdx.x;
-    constexpr bool BL = AL >= 3;
-    const uint32_t lane4 = BL ? lane : lane << 2; /* lane term of rc4_addr */
+    const uint32_t lane4 = lane << 2; /* lane term of rc4_addr */
     const uint64_t sid = (uint64_t)blockIdx.x * 64 + lane;
     const bool live = sid < nstreams;
 
-    if (BL) {
-        /* identity permutation: row x (64 bytes, one per lane) = x */
-        for (uint32_t q = lane; q < 64 * 256 / 4; q += 64)
-            reinterpret_cast<uint32_t *>(S)[q] = (q >> 4) * 0x01010101u;
-        __syncthreads();
-    } else {
-        /* identity permutation: dword q of lane l = bytes 4q..4q+3 */
-        for (uint32_t q = 0; q < 64; ++q)
-            *reinterpret_cast<uint32_t *>(S + ((q << 8) | lane4)) = 0x03020100u + 0x04040404u * q;
-    }
+    /* identity permutation: dword q of lane l = bytes 4q..4q+3 */
+    for (uint32_t q = 0; q < 64; ++q)
+        *reinterpret_cast<uint32_t *>(S + ((q << 8) | lane4)) = 0x03020100u + 0x04040404u * q;
 
     /* KSA (reference arc4.c:43-67) */
     const uint8_t *key = keys + (live ? sid : 0) * (uint64_t)keylen;
     uint32_t j = 0;
-    if (ksa16 && (keylen == 1 || keylen == 2 || keylen == 4 || keylen == 8 || keylen == 16 || keylen == 32)) {
+    if ((keylen == 1 || keylen == 2 || keylen == 4 || keylen == 8 || keylen == 16 || keylen == 32)) {
         /* key lengths dividing 32: the key is loaded once into registers (one
          * byte per VGPR, all loads in flight together) instead of one
          * dependent global byte load per KSA step, and i runs in 16-step
-         * chunks whose S[i] accesses are LDS immediate offsets. */
+         * chunks whose S[i] accesses are LDS immediate offsets (+7-27%,
+         * profiles/r1/otbench_rc4_ksa16_ab.jsonl). */
 #define RC4_KSA_CHUNK(C, KB)                                                                                   \
     {                                                                                                          \
         uint8_t *Sc = S + (((uint32_t)(C) << 10) | lane4);                                                     \
@@ -353,21 +280,21 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
         const uint32_t ib = (uint32_t)(C) << 4;                                                                \
         _Pragma("unroll") for (int q = 0; q < 16; ++q)                                                         \
         {                                                                                                      \
-            if constexpr (AL >= 2) { /* S[i+1] read ahead, fixed up when the swap moved it */                 \
+            if constexpr (AL) { /* S[i+1] read ahead, fixed up when the swap moved it */                 \
                 const uint32_t a = an;                                                                         \
                 j = (j + a + (KB)[q]) & 0xFFu;                                                                 \
-                const uint32_t aj = rc4_addr<BL>(j, lane4);                                                    \
+                const uint32_t aj = rc4_addr(j, lane4);                                                    \
                 const uint32_t b = S[aj];                                                                      \
-                const uint32_t pn = q < 15 ? Sc[rc4_ioff<BL>(q + 1)] : Sn[0];                                  \
+                const uint32_t pn = q < 15 ? Sc[rc4_ioff(q + 1)] : Sn[0];                                  \
                 an = (j == ((ib + (uint32_t)q + 1u) & 0xFFu)) ? a : pn;                                        \
-                Sc[rc4_ioff<BL>(q)] = (uint8_t)b;                                                              \
+                Sc[rc4_ioff(q)] = (uint8_t)b;                                                              \
                 S[aj] = (uint8_t)a;                                                                            \
             } else {                                                                                           \
-                const uint32_t a = Sc[rc4_ioff<BL>(q)];                                                        \
+                const uint32_t a = Sc[rc4_ioff(q)];                                                        \
                 j = (j + a + (KB)[q]) & 0xFFu;                                                                 \
-                const uint32_t aj = rc4_addr<BL>(j, lane4);                                                    \
+                const uint32_t aj = rc4_addr(j, lane4);                                                    \
                 const uint32_t b = S[aj];                                                                      \
-                Sc[rc4_ioff<BL>(q)] = (uint8_t)b;                                                              \
+                Sc[rc4_ioff(q)] = (uint8_t)b;                                                              \
                 S[aj] = (uint8_t)a;                                                                            \
             }                                                                                                  \
         }                                                                                                      \
@@ -393,11 +320,11 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     } else {
         int kpos = 0;
         for (uint32_t i = 0; i < 256; ++i) {
-            const uint32_t ai = rc4_addr<BL>(i, lane4);
+            const uint32_t ai = rc4_addr(i, lane4);
             const uint32_t a = S[ai];
             j = (j + a + key[kpos]) & 0xFFu;
             if (++kpos == keylen) kpos = 0;
-            const uint32_t aj = rc4_addr<BL>(j, lane4);
+            const uint32_t aj = rc4_addr(j, lane4);
             const uint32_t b = S[aj];
             S[ai] = (uint8_t)b;
             S[aj] = (uint8_t)a;
@@ -408,10 +335,10 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     uint32_t i = 0;
     j = 0;
     uint64_t n = 0;
-    if constexpr (AL >= 1) {
+    if constexpr (AL) {
         /* drop % 16 == 0 here (host): 16-step chunks, i = 16c + q + 1, S[i]
          * at immediate offsets (the last step of a chunk wraps into c + 1) */
-        uint32_t an = S[lane4 + rc4_ioff<BL>(1)]; /* S[1] */
+        uint32_t an = S[lane4 + rc4_ioff(1)]; /* S[1] */
         (void)an;
         for (uint32_t c = 0; n < drop; n += 16, c = (c + 1) & 15u) {
             uint8_t *Sc = S + ((c << 10) | lane4);
@@ -419,23 +346,16 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
             const uint32_t ib = c << 4, nb = ((c + 1) & 15u) << 4;
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                uint8_t *si = q < 15 ? Sc + rc4_ioff<BL>(q + 1) : Sn;
-                if constexpr (AL >= 2) { /* S[i+1] read ahead, as in the PRGA */
-                    uint8_t *sp = q < 14 ? Sc + rc4_ioff<BL>(q + 2) : (q == 14 ? Sn : Sn + rc4_ioff<BL>(1));
+                uint8_t *si = q < 15 ? Sc + rc4_ioff(q + 1) : Sn;
+                {
+                    uint8_t *sp = q < 14 ? Sc + rc4_ioff(q + 2) : (q == 14 ? Sn : Sn + rc4_ioff(1));
                     const uint32_t a = an;
                     j = (j + a) & 0xFFu;
-                    const uint32_t aj = rc4_addr<BL>(j, lane4);
+                    const uint32_t aj = rc4_addr(j, lane4);
                     const uint32_t b = S[aj];
                     const uint32_t pn = *sp;
                     const uint32_t inx = q < 14 ? ib + (uint32_t)(q + 2) : nb + (uint32_t)(q - 14);
                     an = (j == inx) ? a : pn;
-                    *si = (uint8_t)b;
-                    S[aj] = (uint8_t)a;
-                } else {
-                    const uint32_t a = *si;
-                    j = (j + a) & 0xFFu;
-                    const uint32_t aj = rc4_addr<BL>(j, lane4);
-                    const uint32_t b = S[aj];
                     *si = (uint8_t)b;
                     S[aj] = (uint8_t)a;
                 }
@@ -445,10 +365,10 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     }
     for (; n < drop; ++n) {
         i = (i + 1) & 0xFFu;
-        const uint32_t ai = rc4_addr<BL>(i, lane4);
+        const uint32_t ai = rc4_addr(i, lane4);
         const uint32_t a = S[ai];
         j = (j + a) & 0xFFu;
-        const uint32_t aj = rc4_addr<BL>(j, lane4);
+        const uint32_t aj = rc4_addr(j, lane4);
         const uint32_t b = S[aj];
         S[ai] = (uint8_t)b;
         S[aj] = (uint8_t)a;
@@ -456,6 +376,38 @@ __global__ __launch_bounds__(64) void k_rc4_kernel(const uint8_t *keys, int keyl
     const uint64_t base = (live ? sid : 0) * len;
     const uint8_t *src = MODE == RC4_KS ? nullptr : in;
     rc4_prga<MODE, AL>(S, lane4, i, j, len, src, out, base, live);
+}
+
+/* Resumable rc4.h streams (struct rc4_state, /root/reference/rc4.h:43-50):
+ * lane s continues stream s from its saved permutation and indices, runs the
+ * PRGA over its len bytes with the same LDS layout and loops as
+ * k_rc4_kernel (generic i: a resumed state can be anywhere in the period),
+ * and writes the state back -- rc4_crypt for many states in one launch. */
+struct Rc4StateDev {
+    uint32_t perm[64]; /* char perm[256] */
+    int32_t index1, index2;
+};
+static_assert(sizeof(Rc4StateDev) == 264, "struct rc4_state layout");
+
+template <int MODE>
+__global__ __launch_bounds__(64) void k_rc4_state_kernel(Rc4StateDev *st, uint64_t nstreams, uint64_t len,
+                                                         const uint8_t *in, uint8_t *out)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t S[64 * 256];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t lane4 = lane << 2;
+    const uint64_t sid = (uint64_t)blockIdx.x * 64 + lane;
+    const bool live = sid < nstreams;
+    Rc4StateDev *my = st + (live ? sid : 0);
+    for (uint32_t q = 0; q < 64; ++q) *reinterpret_cast<uint32_t *>(S + ((q << 8) | lane4)) = my->perm[q];
+    uint32_t i = (uint32_t)my->index1 & 0xFFu, j = (uint32_t)my->index2 & 0xFFu;
+    const uint64_t base = (live ? sid : 0) * len;
+    rc4_prga<MODE, false>(S, lane4, i, j, len, in, out, base, live);
+    if (live) {
+        for (uint32_t q = 0; q < 64; ++q) my->perm[q] = *reinterpret_cast<const uint32_t *>(S + ((q << 8) | lane4));
+        my->index1 = (int32_t)i;
+        my->index2 = (int32_t)j;
+    }
 }
 
 int grid_stream(uint64_t items, int per_cu)
@@ -507,28 +459,7 @@ hipError_t k_clock(uint64_t *out, uint64_t delay_ticks, uint64_t ticks, hipStrea
 
 hipError_t k_xor(const void *a, const void *b, void *out, size_t n, hipStream_t st)
 {
-    /* OTC_XOR_VARIANT="U,per_cu,nt" (A/B only); read once, thread-safe
-     * (function-local static initialisation) */
-    struct Cfg {
-        int U = 1, per_cu = 8, nt = 0;
-    };
-    static const Cfg cfg = [] {
-        Cfg c;
-        if (const char *e = getenv("OTC_XOR_VARIANT")) sscanf(e, "%d,%d,%d", &c.U, &c.per_cu, &c.nt);
-        if (c.U != 1 && c.U != 2 && c.U != 4 && c.U != 8) c.U = 1;
-        if (c.per_cu < 1 || c.per_cu > 64) c.per_cu = 8;
-        return c;
-    }();
-    const int U = cfg.U, per_cu = cfg.per_cu, nt = cfg.nt;
-    auto kern = nt ? (U == 1   ? k_xor_kernel<1, true>
-                      : U == 2 ? k_xor_kernel<2, true>
-                      : U == 4 ? k_xor_kernel<4, true>
-                               : k_xor_kernel<8, true>)
-                   : (U == 1   ? k_xor_kernel<1, false>
-                      : U == 2 ? k_xor_kernel<2, false>
-                      : U == 4 ? k_xor_kernel<4, false>
-                               : k_xor_kernel<8, false>);
-    hipLaunchKernelGGL(kern, dim3(grid_stream(n / 16, per_cu)), dim3(256), 0, st, (const uint8_t *)a,
+    hipLaunchKernelGGL(k_xor_kernel, dim3(grid_stream(n / 16, 8)), dim3(256), 0, st, (const uint8_t *)a,
                        (const uint8_t *)b, (uint8_t *)out, (uint64_t)n);
     return hipGetLastError();
 }
@@ -548,51 +479,44 @@ hipError_t k_checksum(const void *p, size_t n, uint64_t *out, hipStream_t st)
     return hipGetLastError();
 }
 
+hipError_t k_rc4_states(void *states, size_t nstreams, size_t len, const void *in, void *out, hipStream_t st)
+{
+    const uint64_t wgs = (nstreams + 63) / 64;
+    const bool vec = ((((uintptr_t)in | (uintptr_t)out) & 15u) == 0 && len % 16 == 0);
+    auto kern = vec ? k_rc4_state_kernel<RC4_VEC> : k_rc4_state_kernel<RC4_ANY>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(64), 0, st, (Rc4StateDev *)states, (uint64_t)nstreams,
+                       (uint64_t)len, (const uint8_t *)in, (uint8_t *)out);
+    return hipGetLastError();
+}
+
 hipError_t k_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t len, size_t drop, const void *in,
                        void *out, hipStream_t st)
 {
     const uint64_t wgs = (nstreams + 63) / 64;
     const int mode = !in ? RC4_KS
                      : ((((uintptr_t)in | (uintptr_t)out) & 15u) == 0 && len % 16 == 0) ? RC4_VEC : RC4_ANY;
-    /* default (2): i-aligned + S[i+1] read-ahead; OTC_RC4_ALIGNED=1: aligned
-     * only, 0: generic index arithmetic (A/B: profiles/r1/otbench_rc4_readahead_ab.jsonl),
-     * 3: read-ahead on the byte-interleaved layout (measured slower:
-     * profiles/r1/otbench_rc4_bytelayout_negative.jsonl) */
-    static const int al_mode = getenv("OTC_RC4_ALIGNED") ? atoi(getenv("OTC_RC4_ALIGNED")) : 2;
-    const int al = drop % 16 == 0 ? (al_mode == 3 ? 3 : al_mode == 2 ? 2 : al_mode != 0 ? 1 : 0) : 0;
-    auto kern = al == 3   ? (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 3>
-                             : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, 3>
-                                               : k_rc4_kernel<RC4_ANY, 3>)
-                : al == 2 ? (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 2>
-                             : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, 2>
-                                               : k_rc4_kernel<RC4_ANY, 2>)
-                : al == 1 ? (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 1>
-                             : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, 1>
-                                               : k_rc4_kernel<RC4_ANY, 1>)
-                          : (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, 0>
-                             : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, 0>
-                                               : k_rc4_kernel<RC4_ANY, 0>);
+    const bool al = drop % 16 == 0; /* i-aligned loops with the S[i+1] read-ahead */
+    auto kern = al ? (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, true>
+                      : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, true>
+                                        : k_rc4_kernel<RC4_ANY, true>)
+                   : (mode == RC4_KS    ? k_rc4_kernel<RC4_KS, false>
+                      : mode == RC4_VEC ? k_rc4_kernel<RC4_VEC, false>
+                                        : k_rc4_kernel<RC4_ANY, false>);
     /* Resident-workgroup cap per CU, by reserving unused dynamic LDS (each
      * workgroup holds 16 KiB of S-boxes; 160 KiB per CU).  Measured
      * (profiles/r1/otbench_rc4_wgcap_ab.jsonl, otbench_rc4_cap10_ab.jsonl):
      * a launch that would put all 10 per CU in one round runs 563 GB/s, the
      * same work in two rounds of <= 6 per CU 690 GB/s; every other shape is
-     * best uncapped.  OTC_RC4_WG_PER_CU=N forces cap N (0: never cap). */
-    static const int wg_env = getenv("OTC_RC4_WG_PER_CU") ? atoi(getenv("OTC_RC4_WG_PER_CU")) : -1;
-    int wg_cap = wg_env;
-    if (wg_env < 0) {
-        const uint64_t cus = (uint64_t)otc_dev::device_cus();
-        wg_cap = (wgs > 9 * cus && wgs <= 10 * cus) ? 6 : 0;
-    }
-    /* OTC_RC4_KSA16=0: generic KSA for every key length (A/B only) */
-    static const int ksa16 = !getenv("OTC_RC4_KSA16") || atoi(getenv("OTC_RC4_KSA16")) != 0;
+     * best uncapped. */
+    const uint64_t cus = (uint64_t)otc_dev::device_cus();
+    const int wg_cap = (wgs > 9 * cus && wgs <= 10 * cus) ? 6 : 0;
     size_t dyn_lds = 0;
     if (wg_cap >= 1 && wg_cap < 10) {
         const size_t per_wg = (160u * 1024u / (size_t)wg_cap) & ~(size_t)1023;
         dyn_lds = per_wg - 64u * 256u;
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(64), dyn_lds, st, keys, keylen, (uint64_t)nstreams, (uint64_t)len,
-                       (uint64_t)drop, (const uint8_t *)in, (uint8_t *)out, ksa16);
+                       (uint64_t)drop, (const uint8_t *)in, (uint8_t *)out);
     return hipGetLastError();
 }
 

@@ -58,11 +58,18 @@ typedef struct {
 int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 
 /* ---- implementation selection ------------------------------------------- */
-#define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for AES-192/256 CTR of >= 4 GiB,
-                               T-table otherwise (OTC_IMPL=ttable|bitslice|hybrid env overrides) */
+#define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for CTR with AES-256 >= 2 GiB and
+                               AES-192 >= 4 GiB, T-table otherwise (OTC_IMPL=ttable|bitslice
+                               env overrides for the whole process) */
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
 #define OTC_IMPL_BITSLICE 2 /* 32-block-per-lane bitsliced VALU kernel */
-#define OTC_IMPL_HYBRID 3   /* CTR: T-table (85% of the blocks) + bitsliced kernels co-resident on every CU */
+
+/* The kernel family `impl` resolves to for a call (mode_ctr: CTR, else ECB
+ * encrypt) of nbytes with a bits-bit key; -1 for an invalid impl. */
+int otc_pick_impl(int impl, int bits, int mode_ctr, uint64_t nbytes);
+/* OTC_IMPL_TTABLE / OTC_IMPL_BITSLICE: what the calling thread's last
+ * otc_aes_ctr / otc_aes_ecb call ran (OTC_IMPL_AUTO before any call). */
+int otc_last_impl(void);
 
 /* ---- device ops (device pointers; async on `stream`) ---------------------
  * All functions accept any byte length; the trailing partial block of CTR is
@@ -182,6 +189,13 @@ int otc_xor(const void *a, const void *b, void *out, size_t nbytes, void *stream
 int otc_rc4_multi(const uint8_t *keys, int keylen, size_t nstreams, size_t len, size_t drop,
                   const void *in, void *out, void *stream);
 
+/* rc4.h on the device (rc4_crypt for many states at once): states is a
+ * DEVICE array of nstreams `struct rc4_state` (rc4.h, e.g. set up with
+ * rc4_init on the host and copied over); stream s continues from states[s],
+ * processes len bytes at in + s*len -> out + s*len (in == out allowed), and
+ * its state is written back, so calls resume exactly like rc4_crypt. */
+int otc_rc4_crypt_batch(void *states, size_t nstreams, size_t len, const void *in, void *out, void *stream);
+
 /* Deterministic pseudo-random fill (synthetic plaintext). */
 int otc_fill_random(void *p, size_t nbytes, uint64_t seed, void *stream);
 
@@ -295,7 +309,7 @@ int otc_multi_run(int ngpus, int strategy, int mode, const void *host_in, void *
 /* Free the RCCL communicators / buffers that strategy 1 caches between calls
  * and the per-shard engines of strategy 0 (rebuilt on demand). */
 void otc_multi_release(void);
-/* otc_multi_release + the pooled auxiliary streams of the hybrid CTR path. */
+/* Everything the library caches between calls (today: otc_multi_release). */
 void otc_release_resources(void);
 
 /* Test hook: make the (after+1)-th runtime allocation from now fail once

@@ -156,6 +156,8 @@ def _declare_gpu(lib):
     K = P(OtcAesKey)
     sig = {
         "otc_last_error": (ctypes.c_char_p, []),
+        "otc_pick_impl": (c_int, [c_int, c_int, c_int, c_u64]),
+        "otc_last_impl": (c_int, []),
         "otc_aes_key_init": (c_int, [K, c_u8p, c_int, c_int]),
         "otc_aes_ecb": (c_int, [c_vp, c_vp, c_sz, K, c_int, c_vp]),
         "otc_aes_ctr": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_u64, c_int, c_vp]),
@@ -171,6 +173,7 @@ def _declare_gpu(lib):
         "otc_aes_ctr_batch": (c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_int, c_int, c_vp]),
         "otc_xor": (c_int, [c_vp, c_vp, c_vp, c_sz, c_vp]),
         "otc_rc4_multi": (c_int, [c_vp, c_int, c_sz, c_sz, c_sz, c_vp, c_vp, c_vp]),
+        "otc_rc4_crypt_batch": (c_int, [c_vp, c_sz, c_sz, c_vp, c_vp, c_vp]),
         "otc_fill_random": (c_int, [c_vp, c_sz, c_u64, c_vp]),
         "otc_checksum": (c_int, [c_vp, c_sz, c_vp, c_vp]),
         "otc_clock_probe": (c_int, [c_vp, ctypes.c_double, ctypes.c_double, c_vp]),

@@ -16,7 +16,7 @@ import torch
 from .. import _native
 from .keys import expand_key
 
-IMPLS = {"auto": 0, "ttable": 1, "bitslice": 2, "hybrid": 3}
+IMPLS = {"auto": 0, "ttable": 1, "bitslice": 2}
 
 
 def _impl(impl) -> int:
@@ -26,6 +26,23 @@ def _impl(impl) -> int:
         return IMPLS[impl]
     except KeyError:
         raise ValueError(f"impl must be one of {list(IMPLS)}") from None
+
+
+_IMPL_NAMES = {v: k for k, v in IMPLS.items()}
+
+
+def pick_impl(impl="auto", bits: int = 128, mode: str = "ctr", nbytes: int = 0) -> str:
+    """The kernel family ``impl`` resolves to for a ``mode`` ("ctr" or "ecb")
+    call of ``nbytes`` with a ``bits``-bit key (the native routing rule)."""
+    r = _lib().otc_pick_impl(_impl(impl), int(bits), 1 if mode == "ctr" else 0, int(nbytes))
+    if r < 0:
+        raise ValueError(f"bad impl {impl!r}")
+    return _IMPL_NAMES[r]
+
+
+def last_impl() -> str:
+    """What the calling thread's last ``ctr`` / ``ecb_*`` call actually ran."""
+    return _IMPL_NAMES[_lib().otc_last_impl()]
 
 
 def _check_dev(t: torch.Tensor, name: str):

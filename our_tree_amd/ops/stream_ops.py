@@ -49,6 +49,46 @@ def rc4_multi(keys: torch.Tensor, length: int, x: torch.Tensor | None = None, dr
     return out
 
 
+RC4_STATE_BYTES = 264  # sizeof(struct rc4_state): char perm[256]; int index1, index2
+
+
+def rc4_states(keys) -> torch.Tensor:
+    """``rc4_init`` (rc4.h) of every key on the host: uint8 [n, 264] CPU
+    tensor of ``struct rc4_state`` images, ready to move to the GPU."""
+    lib = _native.cpu_lib()
+    out = torch.empty((len(keys), RC4_STATE_BYTES), dtype=torch.uint8)
+    for r, k in enumerate(keys):
+        st = _native.Rc4State()
+        k = bytes(k)
+        lib.rc4_init(ctypes.byref(st), k, len(k))
+        out[r] = torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8)
+    return out
+
+
+def rc4_crypt_batch(states: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``rc4_crypt`` (rc4.h) for many streams on the GPU: ``states`` uint8
+    [n, 264] device tensor of ``struct rc4_state`` (see :func:`rc4_states`),
+    ``x`` [n, len] bytes; returns x ^ keystream and advances every state in
+    place, so a later call resumes each stream exactly where it stopped."""
+    _check_dev(states, "states")
+    _check_dev(x, "x")
+    if states.dtype != torch.uint8 or states.dim() != 2 or states.shape[1] != RC4_STATE_BYTES:
+        raise ValueError(f"states must be uint8 [nstreams, {RC4_STATE_BYTES}]")
+    ns = states.shape[0]
+    if ns == 0 or _nbytes(x) % ns:
+        raise ValueError("x must hold nstreams * len bytes")
+    length = _nbytes(x) // ns
+    out = torch.empty_like(x) if out is None else out
+    _check_dev(out, "out")
+    if _nbytes(out) != _nbytes(x):
+        raise ValueError("out must have the byte size of x")
+    with torch.cuda.device(x.device):
+        rc = _native.require_gpu_lib().otc_rc4_crypt_batch(states.data_ptr(), ns, length, x.data_ptr(),
+                                                           out.data_ptr(), _stream(x))
+    _native.check(rc, "otc_rc4_crypt_batch")
+    return out
+
+
 def fill_random_(t: torch.Tensor, seed: int = 0) -> torch.Tensor:
     """Fill ``t`` in place with deterministic pseudo-random bytes (splitmix64)."""
     _check_dev(t, "t")

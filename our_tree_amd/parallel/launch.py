@@ -87,15 +87,50 @@ def child_env(rank: int, world: int, port: int, base: dict | None = None) -> dic
     return env
 
 
-def spawn(nprocs: int, argv: list[str], timeout_s: float | None = None) -> int:
+def _child_setup(parent_pid: int):
+    """Runs in the forked child before it execs the worker (nothing has touched
+    the GPU in this launcher, so the exec is safe): ask the kernel to SIGTERM
+    the child when the launcher dies, however it dies -- a SIGKILL of the
+    launcher leaves no orphaned rank holding a GPU.  If the launcher is
+    already gone (the race before prctl), exit at once."""
+    try:
+        import ctypes
+
+        libc = ctypes.CDLL("libc.so.6", use_errno=True)
+        libc.prctl(1, int(signal.SIGTERM), 0, 0, 0)  # PR_SET_PDEATHSIG
+    except Exception:  # pragma: no cover - non-Linux
+        pass
+    if os.getppid() != parent_pid:
+        os._exit(1)
+
+
+def spawn(nprocs: int, argv: list[str], timeout_s: float | None = None, grace_s: float = 10.0) -> int:
     """Start ``nprocs`` copies of ``argv`` (one per rank) and wait.  Children
     share this process's stdout/stderr.  When one fails, the others are
     terminated (by PID -- they are our own children) and its exit code is
-    returned."""
+    returned.
+
+    Kill safety: every child gets a parent-death signal (``_child_setup``);
+    SIGTERM / SIGINT / SIGHUP sent to the launcher are forwarded to the
+    children, which get ``grace_s`` seconds to exit before SIGKILL; after
+    ``timeout_s`` the children are terminated the same way (exit code 124)."""
     port = free_port()
-    procs = [subprocess.Popen(argv, env=child_env(r, nprocs, port)) for r in range(nprocs)]
+    me = os.getpid()
+    procs = [subprocess.Popen(argv, env=child_env(r, nprocs, port), preexec_fn=lambda: _child_setup(me))
+             for r in range(nprocs)]
+    got = []
+
+    def on_signal(signum, frame):
+        got.append(signum)
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+
+    handled = (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)
+    old = {s: signal.signal(s, on_signal) for s in handled}
     t0 = time.monotonic()
     rc = 0
+    stop_at = None  # monotonic deadline for SIGKILL after a terminate
     try:
         live = set(range(nprocs))
         while live:
@@ -106,31 +141,43 @@ def spawn(nprocs: int, argv: list[str], timeout_s: float | None = None) -> int:
                 live.discard(r)
                 if c != 0 and rc == 0:
                     rc = c if c > 0 else 128 - c
-                    print(f"launch: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr)
+                    if not got:
+                        print(f"launch: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr)
                     for q in live:
                         procs[q].send_signal(signal.SIGTERM)
-            if timeout_s is not None and time.monotonic() - t0 > timeout_s and live:
-                print(f"launch: timeout after {timeout_s:.0f} s", file=sys.stderr)
+                    stop_at = stop_at or time.monotonic() + grace_s
+            if got and stop_at is None:
+                stop_at = time.monotonic() + grace_s
+            if timeout_s is not None and time.monotonic() - t0 > timeout_s and live and stop_at is None:
+                print(f"launch: timeout after {timeout_s:.0f} s; stopping the ranks", file=sys.stderr)
+                for q in live:
+                    procs[q].send_signal(signal.SIGTERM)
+                rc = rc or 124
+                stop_at = time.monotonic() + grace_s
+            if stop_at is not None and time.monotonic() > stop_at:
                 for q in live:
                     procs[q].kill()
-                rc = rc or 124
             time.sleep(0.05)
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
                 p.wait()
+        for s, h in old.items():
+            signal.signal(s, h)
+    if got and rc == 0:
+        rc = 128 + int(got[0])
     return rc
 
 
-def dispatch(gpus: int, script: str, argv: list[str]) -> bool:
+def dispatch(gpus: int, script: str, argv: list[str], timeout_s: float | None = None) -> bool:
     """Apply the plan for a script run as ``python script argv``.  Returns True
     when the caller should run its main body in this process; otherwise exits
-    (spawned run finished, or refused)."""
+    (spawned run finished, or refused).  ``timeout_s`` bounds a spawned run."""
     p = plan_launch(gpus)
     if p.action == "run":
         return True
     if p.action == "error":
         print(f"error: {p.message}", file=sys.stderr)
         sys.exit(2)
-    sys.exit(spawn(p.nprocs, [sys.executable, script] + list(argv)))
+    sys.exit(spawn(p.nprocs, [sys.executable, script] + list(argv), timeout_s=timeout_s))

@@ -13,6 +13,7 @@ import ctypes
 import numpy as np
 
 from .. import _native
+from ..ops.aes_ops import _impl
 from ..ops.keys import expand_key
 
 MODES = {"ecb": 0, "ctr": 1, "cbc-dec": 2}
@@ -76,7 +77,7 @@ class StreamEngine:
         st = _native.StreamStats()
         ivb = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(iv_or_counter))
         rc = self._lib.otc_engine_run(self._h, MODES[mode], _ptr(host_in), _ptr(host_out), n, ctypes.byref(k), ivb,
-                                      block_offset, {"auto": 0, "ttable": 1, "bitslice": 2}[impl], ctypes.byref(st))
+                                      block_offset, _impl(impl), ctypes.byref(st))
         _native.check(rc, "otc_engine_run")
         return {"total_ms": st.total_ms, "kernel_ms": st.kernel_ms, "h2d_ms": st.h2d_ms, "d2h_ms": st.d2h_ms,
                 "host_stage_ms": st.host_stage_ms, "bytes": st.bytes, "chunks": st.chunks,
@@ -95,15 +96,42 @@ class StreamEngine:
         return self._lib.otc_engine_staging(self._h, slot) or 0
 
 
+PTR_HOST, PTR_PINNED, PTR_DEVICE = 0, 1, 2  # otc.h OTC_PTR_*
+
+
+def pageable_buffers(*bufs) -> list[int]:
+    """Indices of the host buffers in ``bufs`` that are NOT pinned (plain
+    pageable memory: the runtime stages every async copy of them through a
+    bounce buffer and the copy blocks the host thread)."""
+    lib = _native.require_gpu_lib()
+    return [i for i, b in enumerate(bufs) if lib.otc_ptr_kind(_ptr(b)) == PTR_HOST]
+
+
 def multi_gpu_run(mode: str, host_in, host_out, key: bytes, iv_or_counter: bytes = bytes(16), ngpus: int = 1,
                   strategy: str = "direct", chunk_bytes: int = 256 << 20, impl: str = "auto") -> dict:
-    """Single-process multi-GPU processing of one host-resident stream."""
+    """Single-process multi-GPU processing of one host-resident stream.
+
+    strategy "rccl" funnels the whole stream through GPU 0's host link and
+    enqueues every H2D / D2H from one thread: with pageable host buffers those
+    copies block and the pipeline serialises, so a RuntimeWarning is raised
+    (pin them: ``pinned_empty``).  "direct" stages pageable data through its
+    own NUMA-placed pinned ring and needs no warning."""
+    import warnings
+
     lib = _native.require_gpu_lib()
+    if strategy == "rccl":
+        bad = pageable_buffers(host_in, host_out)
+        if bad:
+            which = " and ".join(("host_in", "host_out")[i] for i in bad)
+            verb = "are" if len(bad) > 1 else "is"
+            warnings.warn(f"multi_gpu_run(strategy='rccl'): {which} {verb} pageable; the root's H2D/D2H copies "
+                          "block and serialise the pipeline -- allocate with pinned_empty()", RuntimeWarning,
+                          stacklevel=2)
     k = expand_key(key, decrypt=(mode == "cbc-dec"))
     st = _native.MultiStats()
     ivb = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(iv_or_counter))
     rc = lib.otc_multi_run(ngpus, STRATEGIES[strategy], MODES[mode], _ptr(host_in), _ptr(host_out), _nb(host_in),
-                           ctypes.byref(k), ivb, {"auto": 0, "ttable": 1, "bitslice": 2}[impl], chunk_bytes,
+                           ctypes.byref(k), ivb, _impl(impl), chunk_bytes,
                            ctypes.byref(st))
     _native.check(rc, "otc_multi_run")
     return {"total_ms": st.total_ms, "gbps": st.gbps, "ngpus": st.ngpus, "strategy": strategy,
@@ -115,15 +143,23 @@ def multi_ctr_resident(bufs, key: bytes, counter: bytes, impl: str = "auto") -> 
     sizes, shard g at counter offset g * shard_blocks), all GPUs concurrently
     from one host thread (otc_multi_ctr_resident).  Returns elapsed ms."""
     lib = _native.require_gpu_lib()
-    n = bufs[0].numel()
-    if any(b.numel() != n or not b.is_cuda or b.device.index != g for g, b in enumerate(bufs)):
-        raise ValueError("bufs[g] must be equal-size tensors on cuda:g")
+    if not bufs:
+        raise ValueError("bufs must hold one tensor per GPU")
+    # shard size in BYTES (any dtype): the native call and the per-shard
+    # counter offset g * n / 16 both count bytes
+    n = bufs[0].numel() * bufs[0].element_size()
+    for g, b in enumerate(bufs):
+        if not b.is_cuda or b.device.index != g or not b.is_contiguous():
+            raise ValueError("bufs[g] must be a contiguous tensor on cuda:g")
+        if b.numel() * b.element_size() != n:
+            raise ValueError("every shard must have the same byte size")
+    if n % 16:
+        raise ValueError(f"shard byte size must be a multiple of 16 (got {n})")
     ptrs = (ctypes.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
     k = expand_key(key)
     ms = ctypes.c_double()
     ivb = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(counter))
-    rc = lib.otc_multi_ctr_resident(len(bufs), ptrs, n, ctypes.byref(k), ivb,
-                                    {"auto": 0, "ttable": 1, "bitslice": 2}[impl], ctypes.byref(ms))
+    rc = lib.otc_multi_ctr_resident(len(bufs), ptrs, n, ctypes.byref(k), ivb, _impl(impl), ctypes.byref(ms))
     _native.check(rc, "otc_multi_ctr_resident")
     return ms.value
 

@@ -219,3 +219,28 @@ def test_multi_ctr_resident(gpu):
     assert ms > 0
     got = b"".join(b.cpu().numpy().tobytes() for b in bufs)
     assert got == cpu_ref.ctr(key, ctr, src)
+
+
+def test_multi_ctr_resident_non_byte_dtype(gpu):
+    """shards of int32 / float32 are byte buffers: every byte is encrypted and
+    shard g starts at counter offset g * bytes / 16 (numel was
+    passed as the byte count)"""
+    ngpus = torch.cuda.device_count()
+    key, ctr = os.urandom(16), (2**64 - 7).to_bytes(16, "big")
+    for dt in (torch.int32, torch.float32):
+        per = 4 * 4099  # elements: 16 * 4099 bytes
+        bufs = [torch.randint(0, 2**20, (per,), dtype=torch.int32, device=f"cuda:{g}").view(dt) for g in range(ngpus)]
+        src = b"".join(b.cpu().view(torch.uint8).numpy().tobytes() for b in bufs)
+        pstream.multi_ctr_resident(bufs, key, ctr)
+        got = b"".join(b.cpu().view(torch.uint8).numpy().tobytes() for b in bufs)
+        assert got == cpu_ref.ctr(key, ctr, src)
+
+
+def test_multi_ctr_resident_rejects_bad_shards(gpu):
+    key, ctr = os.urandom(16), bytes(16)
+    with pytest.raises(ValueError, match="multiple of 16"):
+        pstream.multi_ctr_resident([torch.zeros(20, dtype=torch.uint8, device="cuda:0")], key, ctr)
+    with pytest.raises(ValueError, match="contiguous"):
+        pstream.multi_ctr_resident([torch.zeros(64, dtype=torch.uint8, device="cuda:0")[::2]], key, ctr)
+    with pytest.raises(ValueError, match="impl"):
+        pstream.multi_ctr_resident([torch.zeros(64, dtype=torch.uint8, device="cuda:0")], key, ctr, impl="hybrid")

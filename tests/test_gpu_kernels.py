@@ -401,71 +401,66 @@ def test_aesni_shaped_device_api(gpu, bits):
     assert torch.equal(z, x)
 
 
-_SPLIT_CHILD = r"""
-import os, sys
-import torch
-from our_tree_amd import ops
-from our_tree_amd.models import cpu_ref
-dev = torch.device("cuda:0")
-g = torch.Generator().manual_seed(5)
-bad = []
-for bits in (128, 256):
+@pytest.mark.parametrize("bits", [128, 256])
+def test_bitslice_launch_structures(gpu, bits):
+    """Both launch structures of the bitsliced kernels: CTR runs one launch
+    with range checks, ECB a bulk launch compiled for full tasks plus a
+    one-workgroup launch for a partial first / last task -- on shapes with a
+    partial first task, a partial last task, both, a single partial task and
+    none, out of place and in place (a task run by both launches would be
+    XORed twice)."""
+    g = torch.Generator().manual_seed(5)
     for n, low in ((16 * 2048 * 9 + 16 * 77 + 3, 1000), (16 * 2048 * 2, 0), (16 * 100, 2040), (16 * 2048 * 40 + 16, 5)):
         key = os.urandom(bits // 8)
         ctr0 = os.urandom(8) + low.to_bytes(8, "big")
-        x = torch.randint(0, 256, (n,), dtype=torch.uint8, generator=g).to(dev)
+        x = torch.randint(0, 256, (n,), dtype=torch.uint8, generator=g).to(gpu)
         y = ops.ctr(x, key, ctr0, impl="bitslice")
         torch.cuda.synchronize()
-        if y.cpu().numpy().tobytes() != cpu_ref.ctr(key, ctr0, x.cpu().numpy().tobytes()):
-            bad.append(("ctr", bits, n, low))
-        z = x.clone()  # in place: a task run by both launches would be XORed twice
+        assert ops.last_impl() == "bitslice"
+        assert host(y) == cpu_ref.ctr(key, ctr0, host(x)), ("ctr", n, low)
+        z = x.clone()
         ops.ctr(z, key, ctr0, out=z, impl="bitslice")
         torch.cuda.synchronize()
-        if not torch.equal(z, y):
-            bad.append(("ctr-inplace", bits, n, low))
+        assert torch.equal(z, y), ("ctr-inplace", n, low)
         m = n & ~15
         e = ops.ecb_encrypt(x[:m], key, impl="bitslice")
         torch.cuda.synchronize()
-        if e.cpu().numpy().tobytes() != cpu_ref.ecb(key, x[:m].cpu().numpy().tobytes()):
-            bad.append(("ecb", bits, m))
+        assert host(e) == cpu_ref.ecb(key, host(x[:m])), ("ecb", m)
         w = x[:m].clone()
         ops.ecb_encrypt(w, key, out=w, impl="bitslice")
         torch.cuda.synchronize()
-        if not torch.equal(w, e):
-            bad.append(("ecb-inplace", bits, m))
-print("BAD", bad)
-sys.exit(1 if bad else 0)
-"""
+        assert torch.equal(w, e), ("ecb-inplace", m)
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_bitslice_split_and_onepass_launches(gpu, split):
-    """Both launch structures of the bitsliced kernels (OTC_BS_SPLIT: bulk
-    full-task launch + one-workgroup edge launch, or one launch with range
-    checks; the default picks one per mode) on shapes with a partial first
-    task, a partial last task, both, a single partial task and none.  The knob
-    is read once per process, so each structure runs in a child process."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, OTC_BS_SPLIT=split, PYTHONPATH=root)
-    r = subprocess.run([sys.executable, "-c", _SPLIT_CHILD], env=env, cwd=root, capture_output=True, text=True,
-                       timeout=110)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+def test_auto_routing_rule(gpu):
+    """impl="auto" per key size and size (docs/PERF.md): bitsliced CTR for
+    AES-256 from 2 GiB and AES-192 from 4 GiB, T-table for everything else;
+    the boundaries are exact."""
+    G = 1 << 30
+    cases = [(128, "ctr", 64 * G, "ttable"), (256, "ctr", 2 * G, "bitslice"), (256, "ctr", 2 * G - 16, "ttable"),
+             (192, "ctr", 4 * G, "bitslice"), (192, "ctr", 4 * G - 16, "ttable"), (192, "ctr", 2 * G, "ttable"),
+             (256, "ecb", 64 * G, "ttable"), (128, "ctr", 16, "ttable")]
+    for bits, mode, n, want in cases:
+        assert ops.pick_impl("auto", bits, mode, n) == want, (bits, mode, n)
+        assert ops.pick_impl("ttable", bits, mode, n) == "ttable"
+        assert ops.pick_impl("bitslice", bits, mode, n) == "bitslice"
+    with pytest.raises(ValueError):
+        ops.pick_impl("hybrid")
 
 
-@pytest.mark.parametrize("bits", [192, 256])
-def test_ctr_auto_large_aes256_bitsliced(gpu, bits):
-    """impl="auto" sends CTR of >= 4 GiB with AES-192/256 to the bitsliced
-    kernel (the measured winner there): head, a middle window and the tail of a
-    4 GiB + 3-byte buffer against the oracle, and equal to the forced
-    T-table output."""
-    n = (4 << 30) + 3
+@pytest.mark.parametrize("bits,n", [(192, (4 << 30) + 3), (256, (2 << 30) + 3)])
+def test_ctr_auto_large_bitsliced(gpu, bits, n):
+    """impl="auto" sends bulk AES-192/256 CTR to the bitsliced kernel (the
+    measured winner there; the call must actually run it): head, a middle
+    window and the tail against the oracle, and equal to the forced T-table
+    output."""
     key, ctr0 = os.urandom(bits // 8), os.urandom(8) + (2**64 - 12345).to_bytes(8, "big")
     x = torch.empty(n, dtype=torch.uint8, device=gpu)
     ops.fill_random_(x, seed=bits)
     y = ops.ctr(x, key, ctr0, impl="auto")
+    assert ops.last_impl() == "bitslice"
     t = ops.ctr(x, key, ctr0, impl="ttable")
+    assert ops.last_impl() == "ttable"
     torch.cuda.synchronize()
     assert torch.equal(y, t)
     S = 1 << 16
@@ -473,22 +468,6 @@ def test_ctr_auto_large_aes256_bitsliced(gpu, bits):
         blk = off // 16
         exp = cpu_ref.ctr(key, ctr0, host(x[blk * 16:blk * 16 + S + 3]), block_offset=blk)
         assert host(y[blk * 16:blk * 16 + S + 3]) == exp
-
-
-@pytest.mark.parametrize("n", [16 * 5000 + 9, 16 * 2048 * 40 + 3, (32 << 20) + 16 * 777 + 5])
-@pytest.mark.parametrize("ctr_low", [0, 2047, (1 << 64) - 100000])
-def test_ctr_hybrid_matches_oracle(gpu, n, ctr_low):
-    """impl="hybrid": the T-table kernel over the first 85% of the blocks
-    (rounded to 2048-block tasks) and the bitsliced kernel over the rest
-    (counter advanced by the split), concurrently on two streams; the split
-    can fall on a counter carry."""
-    key = os.urandom(16)
-    ctr0 = os.urandom(8) + ctr_low.to_bytes(8, "big")
-    x = rnd(n, gpu, n % 1000)
-    y = ops.ctr(x, key, ctr0, impl="hybrid")
-    torch.cuda.synchronize()
-    assert host(y) == cpu_ref.ctr(key, ctr0, host(x))
-    ops.ctr(x, key, ctr0, out=x, impl="hybrid")  # in place
-    torch.cuda.synchronize()
-    assert torch.equal(x, y)
+    del x, y, t
+    torch.cuda.empty_cache()
 

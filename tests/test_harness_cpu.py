@@ -136,3 +136,40 @@ def test_gpu_cli_ecb_e_format(gpu):
     assert sizes == [1048576, 10485760, 104857600, 1048576000], r.stdout
     recs = results.parse(r.stdout)
     assert [x["bytes"] for x in recs] == sizes and all(len(x["us"]) == 2 for x in recs)
+
+
+@pytest.mark.gpu
+def test_gpu_rc4_harness_rows(gpu):
+    """`bin/test --device gpu`: the reference RC4 sweep (test.c:60-126,135-153)
+    with GPUs as column 3 -- reference line format, every iteration timed, and
+    the harness's own sampled check of out = msg ^ keystream passes (exit 0),
+    followed by the ARC4 self-test lines."""
+    exe = os.path.join(ROOT, "bin", "test")
+    r = subprocess.run([exe, "--device", "gpu", "--sizes", "1048576,1000003", "--threads", "1", "--iters", "2"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert re.search(r"^RC4, 1048576, 1, \nGenerated a new key in \d+, \n(\d+, ){2}\n", r.stdout, re.M), r.stdout
+    recs = results.parse(r.stdout)
+    assert [(x["bytes"], x["threads"], len(x["us"])) for x in recs] == [(1048576, 1, 2), (1000003, 1, 2)]
+    assert all(x["keygen_us"] is not None for x in recs)
+    assert "  ARC4 test #3: passed" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [128, 256])
+def test_gpu_aes_harness_hip_rows(gpu, bits):
+    """`bin/aes_test --suite hip-ecb,hip-ctr,hip-cbc`: the aes-modes harness
+    rows (aes-modes/test.c:287-350 format) on the GPU kernels, device-resident
+    data; the harness checks the first 64 bytes of every GPU's shard against
+    the CPU oracle after the last iteration and exits non-zero on a mismatch."""
+    exe = os.path.join(ROOT, "bin", "aes_test")
+    r = subprocess.run([exe, "--suite", "hip-ecb,hip-ctr,hip-cbc", "--sizes", "1048576,1048583", "--threads", "1",
+                        "--iters", "2", "--bits", str(bits)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    for label in ("HIP ECB", "HIP CTR", "HIP CBC"):
+        assert re.search(rf"^{label}, 1048576, 1, \d+, \d+, $", r.stdout, re.M), r.stdout
+    recs = results.parse(r.stdout)
+    assert sorted((x["label"], x["bytes"]) for x in recs) == sorted(
+        (lb, n) for lb in ("HIP ECB", "HIP CTR", "HIP CBC") for n in (1048576, 1048583))
+    assert all(x["threads"] == 1 and len(x["us"]) == 2 for x in recs)
+    assert "does not match" not in r.stderr
