@@ -120,6 +120,15 @@ bin/bc_test: csrc/cli/bc_test.cpp csrc/include/otc_cipher.hpp $(LIBDIR)/libotc.s
 # the results.* logs (the -O2 builds above are the real CPU baseline).
 O0FLAGS := -g -Wall -pedantic -O0 -std=gnu99
 O0_OBJ  := $(patsubst csrc/cpu/%.c,$(OBJ)/o0/%.o,$(CPU_SRC)) $(OBJ)/o0/bs_selftest.o
+# --- A/B variant libraries ------------------------------------------------
+# make variant NAME=kt0 VFLAGS="-DOTC_BS_KT_PREFETCH=0"  ->  variants/kt0/libotc.so
+# (its own object dir; load it with OTC_LIB=variants/kt0/libotc.so).  A/B
+# switches are compile-time: the production library carries no env knobs.
+.PHONY: variant
+variant:
+	@test -n "$(NAME)" || (echo "NAME=... required" && false)
+	$(MAKE) OBJ=build/obj-$(NAME) LIBDIR=variants/$(NAME) HIPFLAGS="$(HIPFLAGS) $(VFLAGS)" variants/$(NAME)/libotc.so
+
 .PHONY: ref-o0
 ref-o0: bin/test_o0 bin/aes_test_o0
 

@@ -31,6 +31,13 @@
 #ifndef OTC_BS_FENCE_MC
 #define OTC_BS_FENCE_MC 0
 #endif
+/* 1: the key terms of the NEXT S-box of a round are loaded (scalar loads)
+ * before the current S-box runs, so their latency hides under its ~83 VALU
+ * ops instead of stalling every S-box (s_load; s_waitcnt lgkmcnt(0) in front
+ * of each one otherwise). */
+#ifndef OTC_BS_KT_PREFETCH
+#define OTC_BS_KT_PREFETCH 1
+#endif
 
 
 namespace otc_bs {
@@ -109,6 +116,21 @@ OTC_HD void pin8(W *x)
 OTC_HD void pin_n(W *x, int n)
 {
     for (int i = 0; i + 8 <= n; i += 8) pin8(x + i);
+}
+
+/* Wait for the current S-box's key terms BEFORE the next S-box's scalar
+ * loads are issued: scalar loads return out of order, so the only wait the
+ * compiler can emit for them is lgkmcnt(0) -- placed at their first use inside
+ * the S-box it would also wait for the prefetch just issued.  An empty asm
+ * reading the terms puts that wait here. */
+OTC_HD void kt_ready(const W *t)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" ::"s"(t[0]), "s"(t[1]), "s"(t[2]), "s"(t[3]), "s"(t[4]), "s"(t[5]), "s"(t[6]), "s"(t[7]),
+                 "s"(t[8]), "s"(t[9]), "s"(t[10]));
+#else
+    (void)t;
+#endif
 }
 
 /* 3-input XOR.  VEC: one v_bitop3_b32 on gfx950 (hipcc does not fuse pure
@@ -370,6 +392,10 @@ template <int MIX, class KT, int FENCE = 2>
 OTC_HD void round_step_kt(W *s, KT kt)
 {
     W ns[128];
+    /* S-box i of the round (streaming order) is byte r + 4((c + r) & 3) with
+     * c = i / 4, r = i % 4 */
+    W tn[OTC_SBOX_KEY_TERMS];
+    if (OTC_BS_KT_PREFETCH) kt(0, tn);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         W col[32];
@@ -378,7 +404,16 @@ OTC_HD void round_step_kt(W *s, KT kt)
             const int b = r + 4 * ((c + r) & 3);
             W *x = s + 8 * b;
             W t[OTC_SBOX_KEY_TERMS];
-            kt(b, t);
+            if (OTC_BS_KT_PREFETCH) {
+#pragma unroll
+                for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = tn[j];
+                kt_ready(t);
+                const int i = 4 * c + r + 1;
+                if (i < 16) kt((i & 3) + 4 * (((i >> 2) + (i & 3)) & 3), tn);
+                sched_fence(); /* the loads issue here, not next to their use */
+            } else {
+                kt(b, t);
+            }
             /* FENCE 3: every LUT output pinned in the low-pressure order of
              * tools/sbox_schedule.py; 2: pin + scheduling barrier per S-box;
              * 1: pin only; 0: the scheduler may interleave S-boxes (more ILP,
@@ -410,11 +445,21 @@ OTC_HD void round_step_kt(W *s, KT kt)
 template <class KT>
 OTC_HD void round_final_kt(W *s, KT kt)
 {
+    W tn[OTC_SBOX_KEY_TERMS];
+    if (OTC_BS_KT_PREFETCH) kt(0, tn);
 #pragma unroll
     for (int b = 0; b < 16; ++b) {
         W *x = s + 8 * b;
         W t[OTC_SBOX_KEY_TERMS];
-        kt(b, t);
+        if (OTC_BS_KT_PREFETCH) {
+#pragma unroll
+            for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = tn[j];
+            kt_ready(t);
+            if (b + 1 < 16) kt(b + 1, tn);
+            sched_fence();
+        } else {
+            kt(b, t);
+        }
         sbox_lut3_c(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7],
                     t[8], t[9], t[10]);
         pin8(x);
@@ -636,10 +681,20 @@ OTC_HD void ctr_rounds12(const W *s15, const W *s14, KT kt, W *s)
         e[6][p] = d14[p];
         e[7][p] = s14[p];
     }
+    W tn[OTC_SBOX_KEY_TERMS];
+    if (OTC_BS_KT_PREFETCH) kt(0, tn);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
         W t[OTC_SBOX_KEY_TERMS];
-        kt(b, t);
+        if (OTC_BS_KT_PREFETCH) {
+#pragma unroll
+            for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = tn[j];
+            kt_ready(t);
+            if (b + 1 < 8) kt(b + 1, tn);
+            sched_fence();
+        } else {
+            kt(b, t);
+        }
         W *x = e[b];
         sbox_lut3_c(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7],
                     t[8], t[9], t[10]);

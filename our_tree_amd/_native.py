@@ -21,7 +21,9 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
-GPU_LIB_PATH = os.path.join(LIB_DIR, "libotc.so")
+# OTC_LIB selects a variant build of the same library for A/B measurements
+# (``make variant NAME=x VFLAGS=-D...`` -> variants/x/libotc.so); default: the in-tree build
+GPU_LIB_PATH = os.environ.get("OTC_LIB") or os.path.join(LIB_DIR, "libotc.so")
 CPU_LIB_PATH = os.path.join(LIB_DIR, "libotc_cpu.so")
 
 _lock = threading.Lock()
