@@ -125,7 +125,8 @@ def main():
     ap.add_argument("--gib", type=float, default=64.0, help="per-GPU shard size in GiB")
     ap.add_argument("--impl", default=os.environ.get("OTC_BENCH_IMPL", "auto"))
     ap.add_argument("--no-aes256", action="store_true")
-    ap.add_argument("--no-bitslice", action="store_true")
+    ap.add_argument("--no-bitslice", "--no-other-impl", dest="no_other", action="store_true",
+                    help="skip timing the other AES-128 CTR kernel (T-table vs bitsliced) on the same shard")
     ap.add_argument("--no-clock", action="store_true")
     ap.add_argument("--no-scatter", action="store_true", help="skip the RCCL scatter/gather AES-256-CBC pass")
     ap.add_argument("--scatter-mib", type=int, default=512, help="per-rank bytes per scatter round (MiB)")
@@ -220,6 +221,7 @@ def main():
         el = time.perf_counter() - t0
         return pdist.allreduce_max(el)
 
+    resolved = ops.pick_impl(args.impl, 128, "ctr", nbytes)  # the kernel the headline runs
     elapsed = timed(args.steps, key)
     ms_per_step = elapsed / args.steps * 1e3
     total_bytes = nbytes * world * args.steps
@@ -243,12 +245,15 @@ def main():
     cpb_eff = (ms_per_step * 1e-3) * clk_ghz * 1e9 * info["cus"] / nbytes if clk_ghz else None
 
     extra = {}
-    if not args.no_bitslice and args.impl != "bitslice":
-        # BASELINE config 3 names the wave-bitsliced VALU kernel for this
-        # 64 GiB AES-128-CTR shard: time it too (same buffer, same protocol)
-        bs_steps = max(1, min(args.steps, 5))
-        el_bs = timed(bs_steps, key, impl="bitslice")
-        extra["bitsliced_ctr_gbps_whole_node"] = round(nbytes * world * bs_steps / el_bs / 1e9, 3)
+    if not args.no_other:
+        # the other AES-128 CTR kernel on the same shard, same protocol: the
+        # headline's "auto" runs the bitsliced VALU kernel at this size (BASELINE
+        # config 3 names it), the LDS T-table kernel is timed beside it
+        other = "ttable" if resolved == "bitslice" else "bitslice"
+        o_steps = max(1, min(args.steps, 5))
+        el_o = timed(o_steps, key, impl=other)
+        extra[("ttable" if other == "ttable" else "bitsliced") + "_ctr_gbps_whole_node"] = round(
+            nbytes * world * o_steps / el_o / 1e9, 3)
     if not args.no_aes256:
         k256_steps = max(1, min(args.steps, 5))
         el256 = timed(k256_steps, key256)
@@ -304,6 +309,7 @@ def main():
                 "per_gpu_bytes": nbytes,
                 "in_place": True,
                 "impl": args.impl,
+                "impl_resolved": resolved,
             },
             "cycles_per_byte_per_cu": round(cpb, 4),
             "cycles_per_byte_per_cu_at_held_clock": round(cpb_eff, 4) if cpb_eff else None,

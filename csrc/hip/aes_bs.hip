@@ -33,9 +33,10 @@
  *     DMA path (no VGPRs) once rounds 1-2 have consumed the counter-cache
  *     table loads, and lands while the other rounds run; the other slots are
  *     loaded 8 slots ahead of their use in groups of 4;
- *   - ECB: a bulk launch compiled for full tasks only, whose load / store phases are straight-line code with exact
- *     vmcnt waits, plus a one-workgroup launch for a partial first / last
- *     task (BS_FULL_ONLY / BS_EDGE_ONLY);
+ *   - a bulk launch compiled for full tasks only, whose load / store
+ *     phases are straight-line code with exact vmcnt waits, plus a
+ *     one-workgroup launch for a partial first / last task (BS_FULL_ONLY /
+ *     BS_EDGE_ONLY);
  *   - the last round key is folded into the output XOR (ks ^ rk ^ pt as one
  *     v_bitop3 per word) after the single output transpose.
  * Measurements (and the round-1 kernel this replaced): docs/PERF.md,
@@ -68,7 +69,7 @@ struct BsParams {
     const uint32_t *ktab; /* key-term table (key_term_table layout) */
     const uint32_t *ctab; /* CTR counter-caching tables (OTC_BS_CTR_*), or null */
     uint64_t tasks;       /* 2048-block tasks of the call */
-    uint32_t part;        /* BS_ALL, BS_FULL_ONLY or BS_EDGE_ONLY */
+    uint32_t part;        /* BS_FULL_ONLY or BS_EDGE_ONLY */
 };
 
 /* Which tasks a launch runs.  The bulk launch (BS_FULL_ONLY) takes only tasks
@@ -77,7 +78,7 @@ struct BsParams {
  * precise vmcnt(N) counts -- per-slot range branches made it fall back to
  * vmcnt(0) around nearly every slot.  A one-workgroup launch (BS_EDGE_ONLY)
  * runs the first and the last task (wave 0 / wave 1) if they are partial. */
-enum : uint32_t { BS_ALL = 0, BS_FULL_ONLY = 1, BS_EDGE_ONLY = 2 };
+enum : uint32_t { BS_FULL_ONLY = 1, BS_EDGE_ONLY = 2 };
 
 enum : int { BS_CTR = 0, BS_ECB = 1 };
 
@@ -394,6 +395,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
  * workgroups per CU); ECB loads its whole input before the rounds. */
 constexpr int BS_LS = 8;
 
+
 template <int NR, int MODE, int LS, bool CACHE, bool FO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_aes_bs_t3(BsParams P,
                                                                                              otc_aes_key K)
@@ -436,19 +438,15 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     Q.ktab = tab;
     Q.tasks = tasks;
     constexpr int LS = MODE == BS_CTR ? BS_LS : 0;
-    /* Split (bulk BS_FULL_ONLY launch + edge launch) or one launch with
-     * runtime range checks: ECB +5% split (1240 vs 1178 GB/s, 4 GiB), CTR
-     * -0.8% (its plaintext loads are mostly DMA'd, and the clock it holds
-     * decides), so the structure is per mode (profiles/r2/bitslice_out). */
-    const bool onepass = MODE == BS_CTR;
+    /* Split launch: a bulk launch compiled for full tasks only (straight-line
+     * load / store phases with exact vmcnt waits) + a one-workgroup launch
+     * for a partial first / last task.  One launch with per-slot range checks
+     * measured slower for both modes: ECB 1178 vs 1240 GB/s (4 GiB,
+     * profiles/r2/bitslice_out), CTR (64 GiB, with the key-term prefetch)
+     * 1547/1551 vs 1606/1606 (profiles/r3/split). */
     const bool edge = (MODE == BS_CTR && P.shift != 0) || vt % 2048 != 0;
     auto run = [&](auto cachec) {
         constexpr bool C = decltype(cachec)::value;
-        if (onepass) {
-            Q.part = BS_ALL;
-            hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, false>), g, b, 0, st, Q, K);
-            return;
-        }
         Q.part = BS_FULL_ONLY;
         hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, true>), g, b, 0, st, Q, K);
         if (edge) {

@@ -128,12 +128,13 @@ using namespace otc_rt;
 
 namespace {
 
-/* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  Bulk CTR with
- * AES-192/256 runs bitsliced: AES-256 from 2 GiB (2 GiB: 1074 vs 1066 GB/s in
- * both reps, profiles/r2/auto_impl/ab_ctr192_256_2g_4g.txt; 64 GiB: 1165-1168
- * vs 1119-1121), AES-192 from 4 GiB (2 GiB still favours the T-table, 1247 vs
- * 1206; 64 GiB 1317-1321 vs 1311-1312).  AES-128 CTR (the two kernels at
- * parity), every other mode and smaller calls (the bitsliced grid needs ~768
+/* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  Bulk CTR runs
+ * bitsliced: AES-128 from 4 GiB (64 GiB: 1606 vs ~1510-1550 GB/s for the
+ * T-table since the key-term prefetch and the split launch,
+ * profiles/r3/split), AES-256 from 2 GiB (2 GiB: 1074 vs 1066 GB/s in both
+ * reps, profiles/r2/auto_impl/ab_ctr192_256_2g_4g.txt; 64 GiB: 1165-1168 vs
+ * 1119-1121), AES-192 from 4 GiB (2 GiB still favours the T-table, 1247 vs
+ * 1206).  Every other mode and smaller calls (the bitsliced grid needs ~768
  * workgroups to fill the chip, plus two table kernels per call) take the
  * T-table.  ctr_bytes = 0 for non-CTR calls.  OTC_IMPL=ttable|bitslice
  * overrides "auto" for the whole process. */
@@ -147,9 +148,9 @@ int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
         return OTC_IMPL_AUTO;
     }();
     if (env != OTC_IMPL_AUTO) return env;
-    if (bits == 256 && ctr_bytes >= ((size_t)2 << 30)) return OTC_IMPL_BITSLICE;
-    if (bits == 192 && ctr_bytes >= ((size_t)4 << 30)) return OTC_IMPL_BITSLICE;
-    return OTC_IMPL_TTABLE;
+    const size_t GiB = (size_t)1 << 30;
+    const size_t from = bits == 256 ? 2 * GiB : 4 * GiB;
+    return ctr_bytes >= from ? OTC_IMPL_BITSLICE : OTC_IMPL_TTABLE;
 }
 
 int check_impl(int impl)

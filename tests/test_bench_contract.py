@@ -45,7 +45,7 @@ def test_bench_json_line(gpu):
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--gib", "0.25", "--no-clock", "--no-aes256", "--no-bitslice",
+                        "--gib", "0.25", "--no-clock", "--no-aes256", "--no-other-impl",
                         "--scatter-mib", "64", "--scatter-rounds", "2", "--stream-gib", "0.25",
                         "--stream-passes", "2"],
                        capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
@@ -61,6 +61,7 @@ def test_bench_json_line(gpu):
     assert d["higher_is_better"] is True and d["scaling"] == "weak"
     assert d["config"]["model"] == "AES-128-CTR" and d["config"]["parallelism"] == "dp1"
     assert d["verified_sample"] is True
+    assert d["config"]["impl_resolved"] == "ttable"  # 0.25 GiB: below the bitsliced threshold
     nbytes = d["config"]["per_gpu_bytes"]
     assert nbytes == int(0.25 * (1 << 30))
     # value (GB/s) and ms_per_step describe the same timed region
