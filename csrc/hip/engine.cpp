@@ -128,16 +128,17 @@ using namespace otc_rt;
 
 namespace {
 
-/* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  Bulk CTR runs
- * bitsliced: AES-128 from 4 GiB (64 GiB: 1606 vs ~1510-1550 GB/s for the
- * T-table since the key-term prefetch and the split launch,
- * profiles/r3/split), AES-256 from 2 GiB (2 GiB: 1074 vs 1066 GB/s in both
- * reps, profiles/r2/auto_impl/ab_ctr192_256_2g_4g.txt; 64 GiB: 1165-1168 vs
- * 1119-1121), AES-192 from 4 GiB (2 GiB still favours the T-table, 1247 vs
- * 1206).  Every other mode and smaller calls (the bitsliced grid needs ~768
- * workgroups to fill the chip, plus two table kernels per call) take the
- * T-table.  ctr_bytes = 0 for non-CTR calls.  OTC_IMPL=ttable|bitslice
- * overrides "auto" for the whole process. */
+/* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  CTR calls of >= 4 GiB
+ * run bitsliced at every key size; the crossover sweep
+ * (profiles/r3/auto_impl/xover_ctr_128_256.jsonl, 2 reps, in place) puts it
+ * between 2 and 4 GiB: AES-128 2 GiB 1443/1453 vs T-table 1480/1476 GB/s,
+ * 4 GiB 1542/1547 vs 1506/1509, 8 GiB 1580/1581 vs 1490/1497; AES-256 2 GiB
+ * 1103/1099 vs 1108/1124, 4 GiB 1148/1148 vs 1091/1076 (AES-192 at 4 GiB:
+ * 1251 vs 1235 in round 2).  64 GiB AES-128: 1607 vs 1533.  Every other mode
+ * and smaller calls (the bitsliced grid needs ~768 workgroups to fill the
+ * chip, plus two table kernels per call) take the T-table.  ctr_bytes = 0
+ * for non-CTR calls.  OTC_IMPL=ttable|bitslice overrides "auto" for the
+ * whole process. */
 int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
 {
     if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE) return impl;
@@ -148,9 +149,8 @@ int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
         return OTC_IMPL_AUTO;
     }();
     if (env != OTC_IMPL_AUTO) return env;
-    const size_t GiB = (size_t)1 << 30;
-    const size_t from = bits == 256 ? 2 * GiB : 4 * GiB;
-    return ctr_bytes >= from ? OTC_IMPL_BITSLICE : OTC_IMPL_TTABLE;
+    (void)bits;
+    return ctr_bytes >= ((size_t)4 << 30) ? OTC_IMPL_BITSLICE : OTC_IMPL_TTABLE;
 }
 
 int check_impl(int impl)

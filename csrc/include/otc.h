@@ -58,9 +58,9 @@ typedef struct {
 int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 
 /* ---- implementation selection ------------------------------------------- */
-#define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for CTR with AES-256 >= 2 GiB and
-                               AES-128/192 >= 4 GiB, T-table otherwise (OTC_IMPL=ttable|bitslice
-                               env overrides for the whole process) */
+#define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for CTR calls >= 4 GiB, T-table
+                               otherwise (OTC_IMPL=ttable|bitslice env overrides for the whole
+                               process) */
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
 #define OTC_IMPL_BITSLICE 2 /* 32-block-per-lane bitsliced VALU kernel */
 
