@@ -54,7 +54,7 @@ $(OBJ)/cpu/%.o: csrc/cpu/%.c $(wildcard csrc/include/*.h)
 	@mkdir -p $(dir $@)
 	$(CC) $(CFLAGS) $(INC) -c $< -o $@
 
-$(OBJ)/cpu/bs_selftest.o: csrc/cpu/bs_selftest.cpp csrc/include/otc_bitslice.h
+$(OBJ)/cpu/bs_selftest.o: csrc/cpu/bs_selftest.cpp $(wildcard csrc/include/*.h)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -Wno-unknown-pragmas $(INC) -c $< -o $@
 
@@ -63,7 +63,7 @@ $(OBJ)/cpu/bs_selftest.o: csrc/cpu/bs_selftest.cpp csrc/include/otc_bitslice.h
 # the live register set (1 wave/SIMD + AGPR spills).  See docs/PERF.md.
 $(OBJ)/hip/aes_bs.o: HIPFLAGS += -fno-slp-vectorize
 
-$(OBJ)/hip/%.o: csrc/hip/%.hip csrc/hip/otc_device.h csrc/include/otc.h csrc/include/otc_bitslice.h
+$(OBJ)/hip/%.o: csrc/hip/%.hip $(wildcard csrc/hip/*.h) $(wildcard csrc/include/*.h)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) $(INC) -c $< -o $@
 

@@ -246,7 +246,13 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
  * ops cover their latency.  D: the other register slots are loaded D slots
  * ahead of use, in groups of 4, as the keystream of consumed slots frees
  * registers (loading all of them up front spills at 3 waves). */
-template <int NR, int MODE, int LS, bool CACHE, bool FO, int MIX = 2, int PRE = 4, int D = 8>
+/* register plaintext slots issued before the output transposes (2: the
+ * 81-LUT S-box's schedule peaks at 27 live planes, and 4 early slots then
+ * spilled in the output phase) */
+#ifndef OTC_BS_PRE
+#define OTC_BS_PRE 2
+#endif
+template <int NR, int MODE, int LS, bool CACHE, bool FO, int MIX = 2, int PRE = OTC_BS_PRE, int D = 8>
 __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key &K, uint4 *stage)
 {
     Task t;
