@@ -25,10 +25,11 @@ for b in t.split("== ")[1:]:
     pw = re.search(r"SOCKET_POWER: (\S+) W", b)
     clks = [int(x) for x in re.findall(r"GFX_\d:\n\s+CLK: (\d+) MHz", b)]
     print(head, pw.group(1) + " W" if pw else "-", "gfx MHz %d-%d" % (min(clks), max(clks)) if clks else "-")
-    if pw and float(pw.group(1)) > 600:
+    if pw:
         loaded.setdefault(head.split()[-1], []).append(float(pw.group(1)))
 for impl, ws in loaded.items():
     gbps = json.load(open(f"gpurun_out/power/bench_{impl}.json"))["value"]
+    ws = [x for x in ws if x >= 0.9 * max(ws)]  # steady state: drop the ramp and idle samples
     w = sum(ws) / len(ws)
     print(f"{impl}: {gbps:.1f} GB/s at {w:.0f} W loaded socket power = {w / gbps:.3f} J/GB (nJ/B)")
 PY
