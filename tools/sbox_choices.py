@@ -491,3 +491,27 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def add_top_choices(net, env, max_per_form=40):
+    """Alternative XOR decompositions of every top-layer form (keyed: each
+    form is an XOR of (U_a ^ K_a) terms): F = A ^ B or A ^ B ^ C over the
+    existing keyed forms."""
+    names = ["U7k"] + [f"T{i}" for i in range(1, 28)]
+    pool = {nm: env[nm] for nm in names if nm in env}
+    vals = {nm: net.val(s) for nm, s in pool.items()}
+    added = 0
+    for tgt in names:
+        if tgt not in pool: continue
+        tv = vals[tgt]
+        cnt = 0
+        others = [n for n in pool if n != tgt]
+        for a, b in itertools.combinations(others, 2):
+            if vals[a] ^ vals[b] == tv:
+                net.defs.append((pool[tgt][0], 'xor', (pool[a][0], pool[b][0]))); cnt += 1
+        for a, b, c in itertools.combinations(others, 3):
+            if cnt >= max_per_form: break
+            if vals[a] ^ vals[b] ^ vals[c] == tv:
+                net.defs.append((pool[tgt][0], 'xor', (pool[a][0], pool[b][0], pool[c][0]))); cnt += 1
+        added += cnt
+    return added
