@@ -399,7 +399,10 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
 
 /* CTR: 8 LDS slots (4 waves x 8 x 1 KiB = 32 KiB per workgroup, 3
  * workgroups per CU); ECB loads its whole input before the rounds. */
-constexpr int BS_LS = 8;
+#ifndef OTC_BS_LS
+#define OTC_BS_LS 8
+#endif
+constexpr int BS_LS = OTC_BS_LS;
 
 
 template <int NR, int MODE, int LS, bool CACHE, bool FO>
