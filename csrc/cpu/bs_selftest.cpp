@@ -197,8 +197,9 @@ extern "C" int otc_bitslice_selftest(int verbose)
             fails += bad;
 
             /* counter-cached CTR task (the GPU kernel's default CTR path):
-             * group constants + per-call S15/S14 planes + rounds 3.. from the
-             * table, for a few lanes of tasks with different u5 / groups */
+             * round-3 key terms per group, E0 per (group, lane), E1 per task,
+             * rounds 4.. from the table, for a few lanes of tasks with
+             * different u5 / groups */
             bad = 0;
             for (int trial = 0; trial < 4; ++trial) {
                 uint64_t hi = ((uint64_t)rand() << 32) ^ (uint64_t)rand();
@@ -208,19 +209,27 @@ extern "C" int otc_bitslice_selftest(int verbose)
                 uint8_t ctr[16];
                 for (int b = 0; b < 8; ++b) ctr[b] = (uint8_t)(hi >> (8 * (7 - b)));
                 for (int b = 0; b < 8; ++b) ctr[8 + b] = (uint8_t)(lo >> (8 * (7 - b)));
+                /* the group prefix as the table kernel derives it (group 0 of
+                 * a call whose cbase is this counter) */
+                uint8_t pre[14];
+                ctr_group_prefix(lo, hi, false, 0, pre);
+                bad += memcmp(pre, ctr, 14) != 0;
                 static uint32_t grp[OTC_BS_CTR_GRP_WORDS];
-                ctr_group_terms(ctr, rk, grp);
-                const uint32_t *kt15 = tab + 15 * OTC_BS_KT_STRIDE, *kt14 = tab + 14 * OTC_BS_KT_STRIDE;
-                W s14[8];
-                ctr_s14_planes(u5, kt14, s14);
+                uint32_t c8[8], e1w[OTC_BS_CTR_E1_WORDS];
+                ctr_group_consts(pre, rk, sbox_value, c8, grp);
+                const uint32_t k14 = (rk[3] >> 16) & 0xFFu, k15 = rk[3] >> 24;
+                ctr_e1_task(c8, k14, u5, sbox_value, e1w);
                 for (int lane = 0; lane < 64; lane += 21) {
-                    W s15[8];
-                    ctr_s15_planes((uint32_t)lane, kt15, s15);
-                    ctr_rounds12(s15, s14, [&](int b, W *t) {
-                        for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = grp[b * OTC_BS_KT_STRIDE + j];
-                    }, s);
+                    uint32_t ent[8];
+                    ctr_e0_lane(c8, k15, (uint32_t)lane, sbox_value, ent);
+                    W e0[32], e1[32];
+                    for (int p = 0; p < 32; ++p) {
+                        e0[p] = rep_byte(ent[p >> 2], p & 3);
+                        e1[p] = e1w[p];
+                    }
+                    ctr_round2_mix(e0, e1, s);
                     round_step_kt<true>(s, [&](int b, W *t) {
-                        for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = grp[(8 + b) * OTC_BS_KT_STRIDE + j];
+                        for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = grp[b * OTC_BS_KT_STRIDE + j];
                     });
                     for (int r = 3; r + 1 < ctx.nr; ++r)
                         round_step_kt<true>(s, [&](int b, W *t) {

@@ -18,9 +18,10 @@
  *
  * Default kernel (k_aes_bs_t3), built for 3 waves per SIMD (<= 168 VGPRs):
  *   - CTR counter caching (otc_bitslice.h): bytes 0..13 of the 2048 counters
- *     of a task are constant, so rounds 1-2 reduce to 8 S-boxes on top of
- *     per-group constants (k_bs_ctr_table, one thread per 32 tasks) -- 24 of
- *     the 160 AES-128 S-boxes and 2 MixColumns rounds disappear;
+ *     of a task are constant, so rounds 1-2 reduce to table reads (round-2
+ *     S-box outputs per (group, lane) and per task, k_bs_ctr_table) and one
+ *     partial MixColumns -- 32 of the 160 AES-128 S-boxes and 2 MixColumns
+ *     rounds disappear;
  *   - the S-box's key-dependent terms (11 words per round byte, see
  *     sbox_key_terms) come from a per-call table written by k_bs_key_table
  *     and read with scalar loads next to each S-box: no SALU mask arithmetic
@@ -67,7 +68,9 @@ struct BsParams {
     uint64_t shift;       /* CTR: ctr0.lo mod 2048 (virtual index = i + shift) */
     Ctr128 cbase;         /* CTR: ctr0 with the low 11 bits cleared */
     const uint32_t *ktab; /* key-term table (key_term_table layout) */
-    const uint32_t *ctab; /* CTR counter-caching tables (OTC_BS_CTR_*), or null */
+    const uint32_t *ctab; /* CTR counter caching: round-3 key terms per group */
+    const uint32_t *e0tab; /* CTR counter caching: E0 words per (group, lane) */
+    const uint32_t *e1tab; /* CTR counter caching: E1 plane words per task */
     uint64_t tasks;       /* 2048-block tasks of the call */
     uint32_t part;        /* BS_FULL_ONLY or BS_EDGE_ONLY */
 };
@@ -181,8 +184,7 @@ struct TableTerms {
  * slower -- its back edge permutes 128 planes and spills), low-register
  * MixColumns, S-box fence level 2 (per-S-box fences: LUT-level pins cost an
  * s_nop per asm boundary). */
-/* key terms of the counter-cached rounds 2 (BASE 0, bytes 0..7) and 3
- * (BASE 8) from the task's group entry */
+/* key terms of the counter-cached round 3 from the task's group entry */
 template <int BASE>
 struct GroupTerms {
     ktab_ptr gp;
@@ -196,34 +198,50 @@ struct GroupTerms {
 };
 
 /* CTR counter-caching tables of one call (otc_bitslice.h, "CTR counter
- * caching"): threads 0..63 the S15 planes of each lane, 64..95 the S14 planes
- * of each u5, then one thread per group of 32 tasks.  Group g's counter
- * prefix is (cbase with bits 0-15 cleared) + g * 2^16, with the same carry
- * rule as the kernel (128-bit, or 64-bit wrap). */
+ * caching"), one thread per entry: threads [0, ngroups) the round-3 key terms
+ * of each group, then one per (group, lane) for E0, then one per task for E1.
+ * Group g's counter prefix is (cbase with bits 0-15 cleared) + g * 2^16 with
+ * the kernel's carry rule (128-bit, or 64-bit wrap); task t has group
+ * ((cbase >> 11 & 31) + t) >> 5 and u5 = (cbase >> 11) + t mod 32, as in the
+ * kernel.  The byte S-box comes from a 256-entry LDS table built per block. */
 __global__ __launch_bounds__(256) void k_bs_ctr_table(otc_aes_key K, Ctr128 cbase, uint32_t wrap64,
-                                                      uint64_t ngroups, uint32_t *ctab)
+                                                      uint64_t ngroups, uint64_t tasks, uint32_t *gtab,
+                                                      uint32_t *e0tab, uint32_t *e1tab)
 {
+    __shared__ uint32_t sbt[256];
+    sbt[threadIdx.x] = sbox_value(threadIdx.x);
+    __syncthreads();
+    const auto sb = [&](uint32_t v) { return sbt[v & 0xFFu]; };
     const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    auto rkb = [&](int r, int b) -> uint32_t { return (K.rk[4 * r + (b >> 2)] >> (8 * (b & 3))) & 0xFFu; };
-    if (i < 64) {
-        uint32_t kt[OTC_BS_KT_STRIDE];
-        key_terms_of_byte(rkb(0, 15), kt);
-        ctr_s15_planes((uint32_t)i, kt, ctab + i * 8);
-    } else if (i < 96) {
-        uint32_t kt[OTC_BS_KT_STRIDE];
-        key_terms_of_byte(rkb(0, 14), kt);
-        ctr_s14_planes((uint32_t)(i - 64), kt, ctab + OTC_BS_CTR_S14_OFF + (i - 64) * 8);
-    } else if (i - 96 < ngroups) {
-        const uint64_t g = i - 96;
-        const uint64_t base = cbase.lo & ~(uint64_t)0xFFFF;
-        const uint64_t lo = base + (g << 16);
-        const uint64_t hi = cbase.hi + ((!wrap64 && lo < base) ? 1u : 0u);
-        uint8_t pre[14];
-#pragma unroll
-        for (int b = 0; b < 8; ++b) pre[b] = (uint8_t)(hi >> (8 * (7 - b)));
-#pragma unroll
-        for (int b = 0; b < 6; ++b) pre[8 + b] = (uint8_t)(lo >> (8 * (7 - b)));
-        ctr_group_terms(pre, K.rk, ctab + OTC_BS_CTR_GRP_OFF + g * OTC_BS_CTR_GRP_WORDS);
+    auto rk0b = [&](int b) -> uint32_t { return (K.rk[b >> 2] >> (8 * (b & 3))) & 0xFFu; };
+    uint64_t g;
+    int kind;
+    if (i < ngroups) {
+        g = i;
+        kind = 0;
+    } else if (i < ngroups * 65) {
+        g = (i - ngroups) >> 6;
+        kind = 1;
+    } else if (i < ngroups * 65 + tasks) {
+        g = (((cbase.lo >> 11) & 31u) + (i - ngroups * 65)) >> 5;
+        kind = 2;
+    } else {
+        return;
+    }
+    uint8_t pre[14];
+    ctr_group_prefix(cbase.lo, cbase.hi, wrap64 != 0, g, pre);
+    uint32_t c8[8];
+    if (kind == 0) {
+        ctr_group_consts(pre, K.rk, sb, c8, gtab + g * OTC_BS_CTR_GRP_WORDS);
+    } else if (kind == 1) {
+        ctr_group_consts(pre, K.rk, sb, c8, (uint32_t *)nullptr);
+        const uint32_t lane = (uint32_t)(i - ngroups) & 63u;
+        ctr_e0_lane(c8, rk0b(15), lane, sb, e0tab + (g * 64 + lane) * 8);
+    } else {
+        ctr_group_consts(pre, K.rk, sb, c8, (uint32_t *)nullptr);
+        const uint64_t t = i - ngroups * 65;
+        const uint32_t u5 = (uint32_t)((cbase.lo >> 11) + t) & 31u;
+        ctr_e1_task(c8, rk0b(14), u5, sb, e1tab + t * OTC_BS_CTR_E1_WORDS);
     }
 }
 
@@ -285,24 +303,26 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
     };
     if (!(MODE == BS_CTR && CACHE)) prefetch();
     if (MODE == BS_CTR && CACHE) {
-        /* counter caching: rounds 1-2 from the per-call / per-group tables */
+        /* counter caching: rounds 1-2 from the per-group / per-task tables */
         const uint64_t task = t.vbase >> 11;
-        const uint32_t u5 = ((uint32_t)(P.cbase.lo >> 11) + (uint32_t)task) & 31u;
         const uint64_t g = (((P.cbase.lo >> 11) & 31u) + task) >> 5;
-        const uint4 *q15 = (const uint4 *)(P.ctab + lane * 8u);
-        const uint4 a = q15[0], b = q15[1];
-        const W s15[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        const ktab_ptr s14p = (ktab_ptr)P.ctab + OTC_BS_CTR_S14_OFF + u5 * 8u;
-        W s14[8];
+        const uint4 *q0 = (const uint4 *)(P.e0tab + (g * 64u + lane) * 8u);
+        const uint4 a = q0[0], b = q0[1];
+        const W ew[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        W e0[32];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) s14[i] = s14p[i];
-        const ktab_ptr gp = (ktab_ptr)P.ctab + OTC_BS_CTR_GRP_OFF + g * OTC_BS_CTR_GRP_WORDS;
-        ctr_rounds12(s15, s14, GroupTerms<0>{gp}, s);
+        for (int p = 0; p < 32; ++p) e0[p] = rep_byte(ew[p >> 2], p & 3);
+        const ktab_ptr e1p = (ktab_ptr)P.e1tab + task * OTC_BS_CTR_E1_WORDS;
+        W e1[32];
+#pragma unroll
+        for (int p = 0; p < 32; ++p) e1[p] = e1p[p];
+        const ktab_ptr gp = (ktab_ptr)P.ctab + g * OTC_BS_CTR_GRP_WORDS;
+        ctr_round2_mix(e0, e1, s);
         pin_n(s, 128);
         sched_fence();
         prefetch();
         sched_fence();
-        round_step_kt<MIX, GroupTerms<8>, 2>(s, GroupTerms<8>{gp});
+        round_step_kt<MIX, GroupTerms<0>, 2>(s, GroupTerms<0>{gp});
         pin_n(s, 128);
         sched_fence();
         rounds_table<3, NR, MIX>(s, (ktab_ptr)P.ktab);
@@ -425,16 +445,19 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     /* CTR counter caching (+34% over no caching, profiles/r2/bitslice) */
     bool cache = MODE == BS_CTR;
     const uint64_t ngroups = cache ? (((P.cbase.lo >> 11) & 31u) + tasks + 31) >> 5 : 0;
+    const size_t ctab_words =
+        cache ? ngroups * (OTC_BS_CTR_GRP_WORDS + OTC_BS_CTR_E0_WORDS) + tasks * OTC_BS_CTR_E1_WORDS : 0;
     const size_t kt_words = (size_t)NR * 16 * OTC_BS_KT_STRIDE;
     /* per-call tables, stream-ordered: written by small kernels, freed behind
-     * the main kernel (the pool recycles the memory).  The group table is
-     * ~3.4e-5 of the data; if even that does not fit beside a near-full HBM,
-     * CTR runs without counter caching rather than failing. */
+     * the main kernel (the pool recycles the memory).  The counter-caching
+     * tables are ~0.6% of the data (2.8 KiB per 1 MiB group + 128 B per
+     * 32 KiB task); if they do not fit beside a near-full HBM, CTR runs
+     * without counter caching rather than failing. */
     uint32_t *tab = nullptr;
     hipError_t e = hipErrorOutOfMemory;
     if (cache) {
         e = alloc_fault() ? hipErrorOutOfMemory
-                          : hipMallocAsync((void **)&tab, (kt_words + OTC_BS_CTR_GRP_OFF + ngroups * OTC_BS_CTR_GRP_WORDS) * 4, st);
+                          : hipMallocAsync((void **)&tab, (kt_words + ctab_words) * 4, st);
         if (e != hipSuccess) {
             (void)hipGetLastError();
             cache = false;
@@ -467,10 +490,14 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
      * with it */
     if constexpr (MODE == BS_CTR) {
         if (cache) {
-            Q.ctab = tab + kt_words;
-            const uint64_t n = 96 + ngroups;
+            uint32_t *gt = tab + kt_words, *e0 = gt + ngroups * OTC_BS_CTR_GRP_WORDS,
+                     *e1 = e0 + ngroups * OTC_BS_CTR_E0_WORDS;
+            Q.ctab = gt;
+            Q.e0tab = e0;
+            Q.e1tab = e1;
+            const uint64_t n = ngroups * 65 + tasks;
             hipLaunchKernelGGL(k_bs_ctr_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, P.cbase,
-                               P.wrap64, ngroups, (uint32_t *)Q.ctab);
+                               P.wrap64, ngroups, tasks, gt, e0, e1);
             run(std::true_type{});
         } else {
             run(std::false_type{});

@@ -517,22 +517,29 @@ OTC_HD void key_term_table(const uint32_t *rk, int nr, uint32_t *tab)
  * counter byte 15 (bits 0-7) = lane bits 0-5 + slot bits 0-1, byte 14 = slot
  * bits 2-4 + the task's counter bits 11-15 ("u5"), and bytes 0..13 (bits 16+)
  * are a prefix shared by a GROUP of 32 consecutive tasks.  Rounds 1 and 2
- * then split into a per-group constant part, precomputed once per group, and
- * a small varying part:
- *   round 1: only S(byte 15) (per lane) and S(byte 14) (wave-uniform) vary --
- *            both read from a per-call table.  ShiftRows/MixColumns take them
- *            into columns 0 and 1 as (1,1,3,2)*S15 and (1,3,2,1)*S14 on top of
- *            a group constant, and that constant becomes the round-2 S-box KEY
- *            of those 8 bytes;
- *   round 2: only those 8 S-boxes vary; the other 8 are group constants whose
- *            MixColumns contribution folds into the round-3 S-box key.
- * Rounds 1-2 thus cost 8 S-boxes + ~170 XORs instead of 32 S-boxes + 640.
- * Per group: key terms of the 8 varying round-2 bytes and of all 16 round-3
- * bytes (OTC_BS_CTR_GRP_WORDS words). */
-#define OTC_BS_CTR_GRP_WORDS (24 * OTC_BS_KT_STRIDE)
-/* per-call part: S15 planes [64 lanes][8], S14 planes [32 u5][8] */
-#define OTC_BS_CTR_S14_OFF (64 * 8)
-#define OTC_BS_CTR_GRP_OFF (64 * 8 + 32 * 8)
+ * then leave nothing per lane but table reads:
+ *   round 1: only S(byte 15) and S(byte 14) vary; ShiftRows/MixColumns take
+ *            them into columns 0 and 1 as (1,1,3,2)*S15 and (1,3,2,1)*S14 on
+ *            top of a group constant (c8: ctr_group_consts);
+ *   round 2: the S-box outputs of bytes 0..3 ("E0") are then a function of
+ *            the group and byte 15 alone: per (group, lane) 4 values per
+ *            plane (slot bits 0-1), stored as 32 bytes -- byte 8j+i = that
+ *            4-bit pattern of plane i of byte j, doubled to 8 bits -- which
+ *            the kernel widens to plane words with one v_perm_b32 each.  Those
+ *            of bytes 4..7 ("E1") are a function of the task alone (u5 + slot
+ *            bits 2-4): 32 wave-uniform plane words per task, read with scalar
+ *            loads.  Bytes 8..15 are group constants;
+ *   round 3: input = MixColumns of E0 / E1 (ctr_round2_mix) + a group
+ *            constant (round 2's constant bytes through MixColumns, plus rk2)
+ *            that becomes the round-3 S-box key: 16 key-term sets per group.
+ * Rounds 1-2 thus cost ~190 VALU ops (32 widenings + the MixColumns of the 8
+ * varying bytes) instead of 32 S-boxes + 4 MixColumns (round 2 of this
+ * scheme computed the 8 varying S-boxes in the kernel, +650 ops per task).
+ * Table layout of a call (aes_bs.hip): group terms [ngroups][GRP_WORDS], E0
+ * [ngroups][64 lanes][8 words], E1 [tasks][32 words]. */
+#define OTC_BS_CTR_GRP_WORDS (16 * OTC_BS_KT_STRIDE)
+#define OTC_BS_CTR_E0_WORDS (64 * 8)
+#define OTC_BS_CTR_E1_WORDS 32
 
 /* S-box of one byte value through the bitsliced circuit (table-free, so
  * the device precompute and the host tests share it) */
@@ -546,6 +553,8 @@ OTC_HD uint32_t sbox_value(uint32_t v)
     return r;
 }
 OTC_HD uint32_t xtime_value(uint32_t a) { return ((a << 1) ^ ((a & 0x80u) ? 0x1Bu : 0u)) & 0xFFu; }
+/* GF(2^8) product c * a for the MixColumns coefficients c = 1, 2, 3 */
+OTC_HD uint32_t gmul123(uint32_t c, uint32_t a) { return c == 1 ? a : c == 2 ? xtime_value(a) : xtime_value(a) ^ a; }
 
 /* MixColumns of one column of byte values a[row] */
 OTC_HD void mix_column_bytes(const uint32_t *a, uint32_t *o)
@@ -575,46 +584,102 @@ OTC_HD void key_terms_of_byte(uint32_t byte, uint32_t *t)
     t[OTC_SBOX_KEY_TERMS] = 0;
 }
 
-/* Group constants: pre[0..13] = counter bytes 0..13 of the group, rk = the
- * LE round-key words (aes_export_rk32).  out: OTC_BS_CTR_GRP_WORDS words --
- * terms of round-2 bytes 0..7, then of round-3 bytes 0..15. */
-OTC_HD void ctr_group_terms(const uint8_t *pre, const uint32_t *rk, uint32_t *out)
+/* Counter bytes 0..13 of group g: (cbase with bits 0-15 cleared) + g * 2^16,
+ * carried into the high word unless the counter wraps at 64 bits. */
+OTC_HD void ctr_group_prefix(uint64_t cbase_lo, uint64_t cbase_hi, bool wrap64, uint64_t g, uint8_t *pre)
 {
-    auto rkb = [&](int r, int b) -> uint32_t { return (rk[4 * r + (b >> 2)] >> (8 * (b & 3))) & 0xFFu; };
-    uint32_t a[16], B[16], d[16], Q[16];
-    for (int b = 0; b < 14; ++b) a[b] = sbox_value(pre[b] ^ rkb(0, b));
-    a[14] = a[15] = 0; /* varying: added by the kernel */
-    shift_mix_bytes(a, B);
-    for (int b = 0; b < 8; ++b) key_terms_of_byte(B[b] ^ rkb(1, b), out + b * OTC_BS_KT_STRIDE);
-    for (int b = 0; b < 8; ++b) d[b] = 0; /* varying: the kernel's 8 S-boxes */
-    for (int b = 8; b < 16; ++b) d[b] = sbox_value(B[b] ^ rkb(1, b));
-    shift_mix_bytes(d, Q);
-    for (int b = 0; b < 16; ++b) key_terms_of_byte(Q[b] ^ rkb(2, b), out + (8 + b) * OTC_BS_KT_STRIDE);
+    const uint64_t base = cbase_lo & ~(uint64_t)0xFFFF;
+    const uint64_t lo = base + (g << 16);
+    const uint64_t hi = cbase_hi + ((!wrap64 && lo < base) ? 1u : 0u);
+    for (int b = 0; b < 8; ++b) pre[b] = (uint8_t)(hi >> (8 * (7 - b)));
+    for (int b = 0; b < 6; ++b) pre[8 + b] = (uint8_t)(lo >> (8 * (7 - b)));
 }
 
-/* Round-1 S-box output planes of counter byte 15 in lane `lane` (bits 0-5 =
- * lane, bits 6-7 = slot pattern) and of byte 14 for task bits u5 (bits 0-2 =
- * slot pattern, bits 3-7 = u5); kt: the round-0 key terms of that byte. */
-OTC_HD void ctr_s15_planes(uint32_t lane, const uint32_t *kt, W *o)
+/* Group constants: pre[0..13] = counter bytes 0..13 of the group, rk = the
+ * LE round-key words (aes_export_rk32), sb = a byte S-box.  c8[b] (b < 8) =
+ * constant part of the round-2 S-box input of byte b (round 1 with S14 =
+ * S15 = 0, plus rk1).  terms (if non-null): OTC_BS_CTR_GRP_WORDS words, the
+ * key terms of the 16 round-3 bytes. */
+template <class SB>
+OTC_HD void ctr_group_consts(const uint8_t *pre, const uint32_t *rk, SB sb, uint32_t *c8, uint32_t *terms)
 {
-    W x[8];
-    for (int i = 0; i < 6; ++i) x[i] = ((lane >> i) & 1u) ? ~0u : 0u;
-    x[6] = 0xAAAAAAAAu;
-    x[7] = 0xCCCCCCCCu;
-    sbox_lut3_c(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kt[0], kt[1], kt[2], kt[3], kt[4], kt[5], kt[6], kt[7],
-                kt[8], kt[9], kt[10]);
-    for (int i = 0; i < 8; ++i) o[i] = x[i];
+    auto rkb = [&](int r, int b) -> uint32_t { return (rk[4 * r + (b >> 2)] >> (8 * (b & 3))) & 0xFFu; };
+    uint32_t a[16], B[16];
+    for (int b = 0; b < 14; ++b) a[b] = sb(pre[b] ^ rkb(0, b));
+    a[14] = a[15] = 0; /* varying */
+    shift_mix_bytes(a, B);
+    for (int b = 0; b < 8; ++b) c8[b] = B[b] ^ rkb(1, b);
+    if (terms) {
+        uint32_t d[16], Q[16];
+        for (int b = 0; b < 8; ++b) d[b] = 0; /* varying: E0 / E1 */
+        for (int b = 8; b < 16; ++b) d[b] = sb(B[b] ^ rkb(1, b));
+        shift_mix_bytes(d, Q);
+        for (int b = 0; b < 16; ++b) key_terms_of_byte(Q[b] ^ rkb(2, b), terms + b * OTC_BS_KT_STRIDE);
+    }
 }
-OTC_HD void ctr_s14_planes(uint32_t u5, const uint32_t *kt, W *o)
+
+/* E0 entry of (group, lane): out[8] words = 32 bytes, byte 8j+i (j < 4) has
+ * at bit q (and q + 4) bit i of the round-2 S-box output of byte j for the
+ * counter byte 15 = lane + 64q (slot bits 0-1 = q).  k15 = rk0 byte 15. */
+template <class SB>
+OTC_HD void ctr_e0_lane(const uint32_t *c8, uint32_t k15, uint32_t lane, SB sb, uint32_t *out)
 {
-    W x[8];
-    x[0] = 0xF0F0F0F0u;
-    x[1] = 0xFF00FF00u;
-    x[2] = 0xFFFF0000u;
-    for (int i = 0; i < 5; ++i) x[3 + i] = ((u5 >> i) & 1u) ? ~0u : 0u;
-    sbox_lut3_c(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kt[0], kt[1], kt[2], kt[3], kt[4], kt[5], kt[6], kt[7],
-                kt[8], kt[9], kt[10]);
-    for (int i = 0; i < 8; ++i) o[i] = x[i];
+    /* built in registers, stored once (out is global memory on the device) */
+    const uint32_t cf[4] = {1, 1, 3, 2};
+    uint32_t e[4][4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t s15 = sb((lane | (q << 6)) ^ k15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[q][j] = sb(c8[j] ^ gmul123(cf[j], s15));
+    }
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int p = 4 * w + b, j = p >> 3, i = p & 7;
+            uint32_t nib = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) nib |= ((e[q][j] >> i) & 1u) << q;
+            v |= (nib | (nib << 4)) << (8 * b);
+        }
+        out[w] = v;
+    }
+}
+
+/* E1 entry of a task with counter bits 11-15 = u5: out[32] plane words, bit k
+ * of word 8j+i = bit i of the round-2 S-box output of byte 4+j for counter
+ * byte 14 = (k >> 2) | u5 << 3.  k14 = rk0 byte 14. */
+template <class SB>
+OTC_HD void ctr_e1_task(const uint32_t *c8, uint32_t k14, uint32_t u5, SB sb, uint32_t *out)
+{
+    /* built in registers, stored once (out is global memory on the device) */
+    const uint32_t cf[4] = {1, 3, 2, 1};
+    uint32_t e[8][4];
+#pragma unroll
+    for (uint32_t w = 0; w < 8; ++w) {
+        const uint32_t s14 = sb((w | (u5 << 3)) ^ k14);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[w][j] = sb(c8[4 + j] ^ gmul123(cf[j], s14));
+    }
+#pragma unroll
+    for (int p = 0; p < 32; ++p) {
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 8; ++w) v |= ((e[w][p >> 3] >> (p & 7)) & 1u) * (0xFu << (4 * w));
+        out[p] = v;
+    }
+}
+
+/* plane word of E0 byte p: byte p & 3 of word x replicated (one v_perm_b32) */
+OTC_HD W rep_byte(W x, int b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_perm(x, x, 0x01010101u * (uint32_t)b);
+#else
+    return ((x >> (8 * b)) & 0xFFu) * 0x01010101u;
+#endif
 }
 
 /* xtime on 8 planes */
@@ -658,56 +723,17 @@ OTC_HD void mix_column2(const W *a, int i, const W *b, int j, W *out)
     }
 }
 
-/* Rounds 1 and 2 of a counter-cached CTR task: s15/s14 = round-1 S-box
- * planes (ctr_s15_planes / ctr_s14_planes), kt(b, t) = round-2 key terms of
- * bytes 0..7 (ctr_group_terms).  Result in s[128]: the round-3 S-box input
- * WITHOUT its key (that is folded into the group's round-3 terms). */
-template <class KT>
-OTC_HD void ctr_rounds12(const W *s15, const W *s14, KT kt, W *s)
+/* Round 2's ShiftRows + MixColumns on its 8 varying S-box outputs: e0[32] =
+ * planes of bytes 0..3, e1[32] = bytes 4..7.  Result in s[128]: the round-3
+ * S-box input WITHOUT its key (the group's round-3 terms carry that).  The
+ * varying bytes land at col0 rows 0,1 (bytes 0,5), col1 rows 0,3 (4,3), col2
+ * rows 2,3 (2,7), col3 rows 1,2 (1,6). */
+OTC_HD void ctr_round2_mix(const W *e0, const W *e1, W *s)
 {
-    /* round-2 S-box inputs: column 0 = (1,1,3,2) S15, column 1 = (1,3,2,1) S14 */
-    W e[8][8];
-    W d15[8], d14[8];
-    xt8(s15, d15);
-    xt8(s14, d14);
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-        e[0][p] = s15[p];
-        e[1][p] = s15[p];
-        e[2][p] = s15[p] ^ d15[p];
-        e[3][p] = d15[p];
-        e[4][p] = s14[p];
-        e[5][p] = s14[p] ^ d14[p];
-        e[6][p] = d14[p];
-        e[7][p] = s14[p];
-    }
-    W tn[OTC_SBOX_KEY_TERMS];
-    if (OTC_BS_KT_PREFETCH) kt(0, tn);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        W t[OTC_SBOX_KEY_TERMS];
-        if (OTC_BS_KT_PREFETCH) {
-#pragma unroll
-            for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = tn[j];
-            kt_ready(t);
-            if (b + 1 < 8) kt(b + 1, tn);
-            sched_fence();
-        } else {
-            kt(b, t);
-        }
-        W *x = e[b];
-        sbox_lut3_c(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7],
-                    t[8], t[9], t[10]);
-        pin8(x);
-        sched_fence();
-    }
-    /* ShiftRows: column c row r <- byte r + 4((c + r) & 3); the varying bytes
-     * 0..7 land at col0 rows 0,1 (bytes 0,5), col1 rows 0,3 (4,3), col2 rows
-     * 2,3 (2,7), col3 rows 1,2 (1,6) */
-    mix_column2(e[0], 0, e[5], 1, s);
-    mix_column2(e[4], 0, e[3], 3, s + 32);
-    mix_column2(e[2], 2, e[7], 3, s + 64);
-    mix_column2(e[1], 1, e[6], 2, s + 96);
+    mix_column2(e0 + 0, 0, e1 + 8, 1, s);
+    mix_column2(e1 + 0, 0, e0 + 24, 3, s + 32);
+    mix_column2(e0 + 16, 2, e1 + 24, 3, s + 64);
+    mix_column2(e0 + 8, 1, e1 + 16, 2, s + 96);
 }
 
 /* Rounds 1..NR of AES on bitsliced planes s[128] (AddRoundKey r folded into
@@ -782,7 +808,13 @@ OTC_HD W perm_b(W hi, W lo, uint32_t sel)
 OTC_HD W bsel(W m, W x, W y) { return (x & m) | (y & ~m); }
 
 /* one bit-level block-swap stage of transpose32 (J = 4, 2, 1; a template so
- * the stage is fully unrolled -- a rolled loop puts m[] in scratch) */
+ * the stage is fully unrolled -- a rolled loop puts m[] in scratch).  The
+ * selects compile to v_bfi_b32.  Measured alternatives (profiles/r3/
+ * round2_tables): the selects as v_bitop3_b32 -- which issue at ~0.65x the
+ * cost of v_bfi_b32 in tools/ubench/valu_ops.hip -- ran at the same speed
+ * (the kernel is power-, not issue-bound); two pairs per 64-bit shift made
+ * hipcc add a v_mov_b64 per shift (the operands are never in adjacent VGPRs)
+ * and spill. */
 template <int J>
 OTC_HD void transpose_bits(W *m, W mk)
 {
@@ -800,7 +832,7 @@ OTC_HD void transpose32(W *m)
     /* in-place 32x32 transpose: m[r] bit c  ->  m[c] bit r.  Classic 5-stage
      * block swap; the 16- and 8-bit stages only move bytes, so each output
      * word is one v_perm_b32 (2 ops per pair instead of 5); the 4/2/1-bit
-     * stages are a shift and a bit select per word (4 ops per pair). */
+     * stages are a shift and a bit select per word (transpose_bits). */
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const W a = m[k], b = m[k | 16];
