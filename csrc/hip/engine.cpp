@@ -149,8 +149,12 @@ int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
         return OTC_IMPL_AUTO;
     }();
     if (env != OTC_IMPL_AUTO) return env;
-    (void)bits;
-    return ctr_bytes >= ((size_t)4 << 30) ? OTC_IMPL_BITSLICE : OTC_IMPL_TTABLE;
+    /* measured crossover (profiles/r3/auto_impl/xover_after_round2_tables):
+     * AES-128 2 GiB 1520 vs 1506 GB/s, 1 GiB 1353 vs 1360; AES-256 1 GiB
+     * 1056 vs 1049.  AES-192 takes the AES-128 threshold (not measured at
+     * 1 GiB; its margin lies between the two). */
+    const size_t min_bs = bits == 256 ? ((size_t)1 << 30) : ((size_t)2 << 30);
+    return ctr_bytes >= min_bs ? OTC_IMPL_BITSLICE : OTC_IMPL_TTABLE;
 }
 
 int check_impl(int impl)

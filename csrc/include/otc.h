@@ -58,8 +58,8 @@ typedef struct {
 int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 
 /* ---- implementation selection ------------------------------------------- */
-#define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for CTR calls >= 4 GiB, T-table
-                               otherwise (OTC_IMPL=ttable|bitslice env overrides for the whole
+#define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for CTR calls >= 2 GiB (AES-256:
+                               >= 1 GiB), T-table otherwise (OTC_IMPL=ttable|bitslice env overrides for the whole
                                process) */
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
 #define OTC_IMPL_BITSLICE 2 /* 32-block-per-lane bitsliced VALU kernel */

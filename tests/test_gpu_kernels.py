@@ -434,12 +434,12 @@ def test_bitslice_launch_structures(gpu, bits):
 
 def test_auto_routing_rule(gpu):
     """impl="auto" by size (docs/PERF.md, profiles/r3/auto_impl): bitsliced
-    CTR from 4 GiB at every key size, T-table for everything else; the
-    boundaries are exact."""
+    CTR from 2 GiB (AES-128/192) or 1 GiB (AES-256), T-table for everything
+    else; the boundaries are exact."""
     G = 1 << 30
-    cases = [(128, "ctr", 64 * G, "bitslice"), (128, "ctr", 4 * G - 16, "ttable"), (128, "ctr", 4 * G, "bitslice"),
-             (256, "ctr", 4 * G, "bitslice"), (256, "ctr", 4 * G - 16, "ttable"), (256, "ctr", 2 * G, "ttable"),
-             (192, "ctr", 4 * G, "bitslice"), (192, "ctr", 4 * G - 16, "ttable"), (192, "ctr", 2 * G, "ttable"),
+    cases = [(128, "ctr", 64 * G, "bitslice"), (128, "ctr", 2 * G - 16, "ttable"), (128, "ctr", 2 * G, "bitslice"),
+             (256, "ctr", 1 * G, "bitslice"), (256, "ctr", 1 * G - 16, "ttable"), (256, "ctr", 4 * G, "bitslice"),
+             (192, "ctr", 2 * G, "bitslice"), (192, "ctr", 2 * G - 16, "ttable"), (192, "ctr", 1 * G, "ttable"),
              (256, "ecb", 64 * G, "ttable"), (128, "ctr", 16, "ttable")]
     for bits, mode, n, want in cases:
         assert ops.pick_impl("auto", bits, mode, n) == want, (bits, mode, n)
@@ -449,7 +449,7 @@ def test_auto_routing_rule(gpu):
         ops.pick_impl("hybrid")
 
 
-@pytest.mark.parametrize("bits,n", [(128, (4 << 30) + 3), (192, (4 << 30) + 3), (256, (4 << 30) + 3)])
+@pytest.mark.parametrize("bits,n", [(128, (2 << 30) + 3), (192, (2 << 30) + 3), (256, (1 << 30) + 3)])
 def test_ctr_auto_large_bitsliced(gpu, bits, n):
     """impl="auto" sends bulk AES CTR to the bitsliced kernel (the
     measured winner there; the call must actually run it): head, a middle
