@@ -7,7 +7,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 D=gpurun_out/energy
 mkdir -p $D
-ops=${1:-nop xor_vv and_vv bitop3_vvs bitop3_vvv bfi_vvv perm_vvv lshl_vi}
+ops=${1:-nop xor_vv and_vv bitop3_vvs bitop3_vvv bfi_vvv perm_vvv lshl_vi and_or_vvv ds_read_b32}
 echo "== idle" >> $D/smi.txt
 timeout 20 amd-smi metric -p -c -g 0 >> $D/smi.txt 2>&1
 for op in $ops; do

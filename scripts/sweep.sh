@@ -1,0 +1,30 @@
+#!/bin/bash
+# Mode x key-size sweep of the current build (through gpurun):
+#   gpurun --timeout 900 -- bash scripts/sweep.sh OUTNAME
+# every AES mode at 128/192/256 bits on a 4 GiB in-place buffer (impl auto),
+# CTR at 64 GiB with both kernels, then the J/GB power probe and a kernel trace
+# of a short bench.py run.  Output under gpurun_out/OUTNAME/.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+O=gpurun_out/${1:-sweep}; mkdir -p $O
+for m in ctr ecb ecb-dec cbc-dec cfb-dec cbc-enc-seg cfb-enc-seg; do for b in 128 192 256; do
+    timeout -k 10 120 ./bin/otbench --mode $m --bits $b --bytes 4G --inplace --iters 10 --warmup 2 --clock >> $O/sweep.jsonl || exit 1
+done; done
+for i in ttable bitslice; do for b in 128 256; do
+    timeout -k 10 120 ./bin/otbench --mode ctr --bits $b --bytes 64G --inplace --iters 10 --warmup 2 --impl $i --clock >> $O/ctr64g.jsonl || exit 1
+done; done
+bash scripts/power_probe.sh "bitslice" > $O/power.txt 2>&1 || { tail -5 $O/power.txt; exit 1; }
+cp -r gpurun_out/power $O/ 2>/dev/null
+mkdir -p $O/kt
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt/db -o run -- python3 bench.py --steps 5 --warmup 1 --no-scatter --no-stream > $O/kt/run.log 2>&1 || { tail -20 $O/kt/run.log; exit 1; }
+db=$(find $O/kt/db -name '*.db' | head -1)
+python3 tools/rocpd_summary.py "$db" > $O/kt/kernels.txt && head -12 $O/kt/kernels.txt
+python3 - "$O" <<'PY'
+import json, sys
+o = sys.argv[1]
+for f in ("sweep.jsonl", "ctr64g.jsonl"):
+    for l in open(f"{o}/{f}"):
+        d = json.loads(l)
+        print(f, d["mode"], d["bits"], d["bytes"] >> 30, "GiB", d["impl"], d["gbps"], d.get("held_clock_ghz"))
+PY
+cat $O/power.txt | tail -3

@@ -4,7 +4,7 @@
 // (amd-smi) while it runs and derive energy per wave-instruction.
 //
 //   valu_energy OP SECONDS      OP in: xor_vv bitop3_vvv bitop3_vvs and_vv
-//                               bfi_vvv perm_vvv lshl_vi nop
+//                               bfi_vvv perm_vvv lshl_vi and_or_vvv ds_read_b32 nop
 // Prints one JSON line: wave-instructions per second of the chip.
 // Question it answers for the bitsliced AES kernel (power-limited): does a
 // 3-VGPR-operand v_bitop3_b32 cost more energy than a 2-operand v_xor_b32,
@@ -15,8 +15,9 @@
 #include <cstdlib>
 #include <cstring>
 
-enum { XOR_VV, BITOP3_VVV, BITOP3_VVS, AND_VV, BFI_VVV, PERM_VVV, LSHL_VI, NOP, NOPS };
-static const char *names[NOPS] = {"xor_vv", "bitop3_vvv", "bitop3_vvs", "and_vv", "bfi_vvv", "perm_vvv", "lshl_vi", "nop"};
+enum { XOR_VV, BITOP3_VVV, BITOP3_VVS, AND_VV, BFI_VVV, PERM_VVV, LSHL_VI, AND_OR_VVV, DS_READ, NOP, NOPS };
+static const char *names[NOPS] = {"xor_vv",  "bitop3_vvv", "bitop3_vvs", "and_vv",      "bfi_vvv",
+                                  "perm_vvv", "lshl_vi",    "and_or_vvv", "ds_read_b32", "nop"};
 
 template <int OP>
 __global__ __launch_bounds__(256) void k_op(unsigned *out, int iters, unsigned sk)
@@ -25,6 +26,14 @@ __global__ __launch_bounds__(256) void k_op(unsigned *out, int iters, unsigned s
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] = threadIdx.x * (2 * j + 1) + blockIdx.x;
     const unsigned b = threadIdx.x ^ 0x1234u, c = threadIdx.x ^ 0x9876u;
+    /* ds_read_b32: 32 KiB per workgroup, lane l reads bank l mod 32 of a
+     * data-dependent row (conflict-free, like the T-table kernel's lookups) */
+    __shared__ unsigned lds[8192];
+    if (OP == DS_READ) {
+        for (int q = threadIdx.x; q < 8192; q += 256) lds[q] = q * 2654435761u;
+        __syncthreads();
+    }
+    const unsigned lane_off = threadIdx.x & 31u;
     for (int i = 0; i < iters; ++i) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -37,6 +46,9 @@ __global__ __launch_bounds__(256) void k_op(unsigned *out, int iters, unsigned s
                 if (OP == BFI_VVV) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(a[j]) : "v"(b), "v"(c));
                 if (OP == PERM_VVV) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b), "v"(c));
                 if (OP == LSHL_VI) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(a[j]));
+                if (OP == AND_OR_VVV) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b), "v"(c));
+                if (OP == DS_READ) /* 8 chains in flight, one wait per round of them (hipcc) */
+                    a[j] = lds[((a[j] & 0xFFu) << 5) | lane_off];
                 if (OP == NOP) asm volatile("s_nop 0" : "+v"(a[j]));
             }
         }
@@ -90,6 +102,8 @@ int main(int argc, char **argv)
     case BFI_VVV: r = run<BFI_VVV>(cus, out, secs); break;
     case PERM_VVV: r = run<PERM_VVV>(cus, out, secs); break;
     case LSHL_VI: r = run<LSHL_VI>(cus, out, secs); break;
+    case AND_OR_VVV: r = run<AND_OR_VVV>(cus, out, secs); break;
+    case DS_READ: r = run<DS_READ>(cus, out, secs); break;
     case NOP: r = run<NOP>(cus, out, secs); break;
     }
     if (r < 0) return 1;
