@@ -1,14 +1,17 @@
 #!/bin/bash
 # Mode x key-size sweep of the current build (through gpurun):
 #   gpurun --timeout 900 -- bash scripts/sweep.sh OUTNAME
-# every AES mode at 128/192/256 bits on a 4 GiB in-place buffer (impl auto),
+# every AES mode at 128/192/256 bits on a 4 GiB buffer (impl auto; in place
+# except the chained decrypts),
 # CTR at 64 GiB with both kernels, then the J/GB power probe and a kernel trace
 # of a short bench.py run.  Output under gpurun_out/OUTNAME/.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=gpurun_out/${1:-sweep}; mkdir -p $O
 for m in ctr ecb ecb-dec cbc-dec cfb-dec cbc-enc-seg cfb-enc-seg; do for b in 128 192 256; do
-    timeout -k 10 120 ./bin/otbench --mode $m --bits $b --bytes 4G --inplace --iters 10 --warmup 2 --clock >> $O/sweep.jsonl || exit 1
+    ip=--inplace  # the chained decrypts read the previous ciphertext block: out of place
+    case $m in cbc-dec|cfb-dec) ip= ;; esac
+    timeout -k 10 120 ./bin/otbench --mode $m --bits $b --bytes 4G $ip --iters 10 --warmup 2 --clock >> $O/sweep.jsonl || exit 1
 done; done
 for i in ttable bitslice; do for b in 128 256; do
     timeout -k 10 120 ./bin/otbench --mode ctr --bits $b --bytes 64G --inplace --iters 10 --warmup 2 --impl $i --clock >> $O/ctr64g.jsonl || exit 1
