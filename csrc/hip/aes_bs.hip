@@ -26,8 +26,8 @@
  *     sbox_key_terms) come from a per-call table written by k_bs_key_table
  *     and read with scalar loads next to each S-box: no SALU mask arithmetic
  *     and no round-key SGPRs live across the kernel;
- *   - an 83-LUT3 S-box (tools/sbox_lut3.py: ILP cover after re-synthesising
- *     the bottom linear layer) in minimum-live-plane order
+ *   - a 79-LUT3 S-box (tools/sbox_choices.py: ILP cover over structural
+ *     choices of the circuit) in minimum-live-plane order
  *     (tools/sbox_schedule.py) and a 55-node MixColumns column
  *     (tools/mixcol_search.py; the textbook forms take 76-80);
  *   - CTR: the plaintext of the first 8 slots goes straight to LDS by the
@@ -264,9 +264,10 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
  * ops cover their latency.  D: the other register slots are loaded D slots
  * ahead of use, in groups of 4, as the keystream of consumed slots frees
  * registers (loading all of them up front spills at 3 waves). */
-/* register plaintext slots issued before the output transposes (2: the
- * 81-LUT S-box's schedule peaks at 27 live planes, and 4 early slots then
- * spilled in the output phase) */
+/* register plaintext slots issued before the output transposes (2: with the
+ * 81-LUT S-box (27 live planes at its peak) 4 early slots spilled in the
+ * output phase; with the 79-LUT one (24) they no longer spill but measured
+ * 1-1.5% slower, profiles/r3/sbox79) */
 #ifndef OTC_BS_PRE
 #define OTC_BS_PRE 2
 #endif

@@ -15,13 +15,16 @@ and of its output), and a class may have several structural definitions:
   cancellation free), plus product pairs that share a factor regrouped as
   f & (g1 ^ g2);
 * every 2-LUT decomposition F(g(3 inputs), 2 inputs) of the four GF(2^4)
-  inversion outputs.
+  inversion outputs;
+* alternative XOR decompositions of the top-layer forms over other forms
+  (round 3, session 2; a fixed order keeps the definitions acyclic).
 
 Cuts are enumerated over all definitions (fixpoint), the cover ILP
 (scipy/HiGHS) picks one implementation per needed class and minimises LUTs;
 cycles through equivalent classes are removed lazily (a constraint per found
 cycle, re-solve).  The emitted program is checked against the AES S-box on
-all 2^16 (x, k).  Result: 81 LUTs (round 2: 83).
+all 2^16 (x, k).  Result: 79 LUTs (without the top-layer choices 81; round
+2: 83), in ~7 min.
 
     tools/sbox_choices.py            # ~5-10 min (ILP), rewrites the header body
 """
@@ -462,6 +465,45 @@ def check_program(net, stmts, names, out_cls, out_req):
     return all(env[f"S{j}"] == out_req[j] for j in range(8))
 
 
+def add_top_choices(net, env, max_per_form=40):
+    """Alternative XOR decompositions of the top-layer forms (each form is an
+    XOR of keyed (U_a ^ K_a) terms, so keys carry over): F = A ^ B or
+    A ^ B ^ C over other forms, restricted to forms earlier in a fixed order
+    (U-weight, then name) so the definitions form a DAG.  Unrestricted
+    choices give a smaller relaxation (75) whose solutions contain cycles
+    through equivalent classes; every lazy cycle cut costs a ~35 min re-solve."""
+    names = ["U7k"] + [f"T{i}" for i in range(1, 28)]
+    pool = {nm: env[nm] for nm in names if nm in env}
+    vals = {nm: net.val(s) for nm, s in pool.items()}
+    um = {f"U{a}": 1 << a for a in range(8)}
+    wmask = {}
+    for d in TOP:
+        m = 0
+        for i in d[2:]:
+            if i in um:
+                m ^= um[i]
+            elif i in wmask:
+                m ^= wmask[i]
+        wmask[d[0]] = m
+    order = sorted(pool, key=lambda n: (bin(wmask[n]).count('1'), n))
+    rank = {n: i for i, n in enumerate(order)}
+    added = 0
+    for tgt in names:
+        if tgt not in pool: continue
+        tv = vals[tgt]
+        cnt = 0
+        others = [n for n in pool if rank[n] < rank[tgt]]
+        for a, b in itertools.combinations(others, 2):
+            if vals[a] ^ vals[b] == tv:
+                net.defs.append((pool[tgt][0], 'xor', (pool[a][0], pool[b][0]))); cnt += 1
+        for a, b, c in itertools.combinations(others, 3):
+            if cnt >= max_per_form: break
+            if vals[a] ^ vals[b] ^ vals[c] == tv:
+                net.defs.append((pool[tgt][0], 'xor', (pool[a][0], pool[b][0], pool[c][0]))); cnt += 1
+        added += cnt
+    return added
+
+
 def main():
     net = Net()
     env = build_base(net, bottom='none')
@@ -472,6 +514,7 @@ def main():
         r = bottom_network(net, env, prods, forms, seed, prefer=prefer if seed % 2 else (),
                            temp=0.5 if seed < 20 else 1.5)
     add_inversion_choices(net, env)
+    add_top_choices(net, env)
     outs = [x[0] for x in r]
     print(f"classes {len(net.tt)}, definitions {len(net.defs)}", file=sys.stderr)
     cuts = enum_cuts(net)
@@ -492,26 +535,3 @@ def main():
 if __name__ == "__main__":
     main()
 
-
-def add_top_choices(net, env, max_per_form=40):
-    """Alternative XOR decompositions of every top-layer form (keyed: each
-    form is an XOR of (U_a ^ K_a) terms): F = A ^ B or A ^ B ^ C over the
-    existing keyed forms."""
-    names = ["U7k"] + [f"T{i}" for i in range(1, 28)]
-    pool = {nm: env[nm] for nm in names if nm in env}
-    vals = {nm: net.val(s) for nm, s in pool.items()}
-    added = 0
-    for tgt in names:
-        if tgt not in pool: continue
-        tv = vals[tgt]
-        cnt = 0
-        others = [n for n in pool if n != tgt]
-        for a, b in itertools.combinations(others, 2):
-            if vals[a] ^ vals[b] == tv:
-                net.defs.append((pool[tgt][0], 'xor', (pool[a][0], pool[b][0]))); cnt += 1
-        for a, b, c in itertools.combinations(others, 3):
-            if cnt >= max_per_form: break
-            if vals[a] ^ vals[b] ^ vals[c] == tv:
-                net.defs.append((pool[tgt][0], 'xor', (pool[a][0], pool[b][0], pool[c][0]))); cnt += 1
-        added += cnt
-    return added
