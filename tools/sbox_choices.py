@@ -170,17 +170,26 @@ def enum_cuts(net, cap=60):
                 changed = True
     return cuts
 
-def solve(net, outs, cuts, time_limit=600, verbose=True, max_iter=30):
+def solve(net, outs, cuts, time_limit=600, verbose=True, max_iter=30, order_cls=()):
+    """order_cls: classes whose selected implementations must be acyclic
+    among themselves, enforced inside the ILP by level variables
+    (Miller-Tucker-Zemlin: level(c) >= level(L) + 1 when the chosen cut of c
+    has leaf L) instead of lazy cycle cuts -- for the unrestricted top-layer
+    choices, whose cycles otherwise cost one full re-solve each."""
     impl_cls = sorted({d[0] for d in net.defs})
     var = []
     for c in impl_cls:
         for u in cuts[c]:
             if u != frozenset([c]):
                 var.append((c, u))
-    nv = len(var)
+    nx = len(var)
     vid = {v: i for i, v in enumerate(var)}
     idx_by_cls = {}
     for i, (c, u) in enumerate(var): idx_by_cls.setdefault(c, []).append(i)
+    order_cls = sorted(set(order_cls))
+    lvl = {c: nx + k for k, c in enumerate(order_cls)}
+    nv = nx + len(order_cls)
+    big = len(order_cls) + 1
     rows = []; lb = []; ub = []
     def add(coefs, lo, hi):
         rows.append(coefs); lb.append(lo); ub.append(hi)
@@ -193,18 +202,25 @@ def solve(net, outs, cuts, time_limit=600, verbose=True, max_iter=30):
             if L in net.pi: continue
             co = {j: 1 for j in idx_by_cls.get(L, [])}; co[i] = co.get(i, 0) - 1
             add(co, 0, np.inf)
+            if c in lvl and L in lvl:
+                # level(c) - level(L) - big * x_i >= 1 - big
+                add({lvl[c]: 1, lvl[L]: -1, i: -big}, 1 - big, np.inf)
+    cost = np.concatenate([np.ones(nx), np.zeros(nv - nx)])
+    integ = np.concatenate([np.ones(nx), np.zeros(nv - nx)])
+    upper = np.concatenate([np.ones(nx), np.full(nv - nx, float(big))])
     for it in range(max_iter):
         A = lil_matrix((len(rows), nv))
         for r, co in enumerate(rows):
             for j, v in co.items(): A[r, j] = v
         t0 = time.time()
-        res = milp(c=np.ones(nv), constraints=LinearConstraint(csr_matrix(A), lb, ub), integrality=np.ones(nv),
-                   bounds=Bounds(0, 1), options={"time_limit": time_limit, "disp": False})
+        res = milp(c=cost, constraints=LinearConstraint(csr_matrix(A), lb, ub), integrality=integ,
+                   bounds=Bounds(0, upper), options={"time_limit": time_limit, "disp": False})
         if verbose: print(f"vars {nv} rows {len(rows)} status {res.message} obj {res.fun} in {time.time()-t0:.1f}s", file=sys.stderr)
         if res.x is None: return None
         sel = {}
         for i, (c, u) in enumerate(var):
             if res.x[i] > 0.5: sel[c] = u
+        if verbose: print(f"  {len(sel)} LUTs selected (incl. unused)", file=sys.stderr)
         # cycle check among the classes needed by the outputs
         cyc = find_cycle(net, sel, outs)
         if cyc is None:
@@ -465,13 +481,15 @@ def check_program(net, stmts, names, out_cls, out_req):
     return all(env[f"S{j}"] == out_req[j] for j in range(8))
 
 
-def add_top_choices(net, env, max_per_form=40):
+def add_top_choices(net, env, max_per_form=40, restrict=True, order_seed=None):
     """Alternative XOR decompositions of the top-layer forms (each form is an
     XOR of keyed (U_a ^ K_a) terms, so keys carry over): F = A ^ B or
-    A ^ B ^ C over other forms, restricted to forms earlier in a fixed order
-    (U-weight, then name) so the definitions form a DAG.  Unrestricted
+    A ^ B ^ C over other forms.  restrict: only forms earlier in a fixed
+    order (U-weight, then name), so the definitions form a DAG.  Unrestricted
     choices give a smaller relaxation (75) whose solutions contain cycles
-    through equivalent classes; every lazy cycle cut costs a ~35 min re-solve."""
+    through equivalent classes; every lazy cycle cut costs a ~35 min re-solve,
+    so the unrestricted network is solved with level variables instead
+    (solve(order_cls=...)).  Returns (definitions added, top-form classes)."""
     names = ["U7k"] + [f"T{i}" for i in range(1, 28)]
     pool = {nm: env[nm] for nm in names if nm in env}
     vals = {nm: net.val(s) for nm, s in pool.items()}
@@ -485,14 +503,18 @@ def add_top_choices(net, env, max_per_form=40):
             elif i in wmask:
                 m ^= wmask[i]
         wmask[d[0]] = m
-    order = sorted(pool, key=lambda n: (bin(wmask[n]).count('1'), n))
+    tie = {n: n for n in pool}
+    if order_seed is not None:  # another DAG restriction: random ties within a U-weight
+        rr = random.Random(order_seed)
+        tie = {n: rr.random() for n in pool}
+    order = sorted(pool, key=lambda n: (bin(wmask[n]).count('1'), tie[n]))
     rank = {n: i for i, n in enumerate(order)}
     added = 0
     for tgt in names:
         if tgt not in pool: continue
         tv = vals[tgt]
         cnt = 0
-        others = [n for n in pool if rank[n] < rank[tgt]]
+        others = [n for n in pool if n != tgt and (not restrict or rank[n] < rank[tgt])]
         for a, b in itertools.combinations(others, 2):
             if vals[a] ^ vals[b] == tv:
                 net.defs.append((pool[tgt][0], 'xor', (pool[a][0], pool[b][0]))); cnt += 1
@@ -501,10 +523,18 @@ def add_top_choices(net, env, max_per_form=40):
             if vals[a] ^ vals[b] ^ vals[c] == tv:
                 net.defs.append((pool[tgt][0], 'xor', (pool[a][0], pool[b][0], pool[c][0]))); cnt += 1
         added += cnt
-    return added
+    return added, {s[0] for s in pool.values()}
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--unrestricted", action="store_true",
+                    help="top-layer choices over ALL other forms, acyclicity by level variables")
+    ap.add_argument("--order-seed", type=int, help="restricted choices under a random tie order")
+    ap.add_argument("--time-limit", type=float, default=1800)
+    ap.add_argument("--out", help="write the header here instead of csrc/include/otc_sbox_lut3.h")
+    a = ap.parse_args()
     net = Net()
     env = build_base(net, bottom='none')
     prods, forms = bottom_targets(env, net)
@@ -514,16 +544,20 @@ def main():
         r = bottom_network(net, env, prods, forms, seed, prefer=prefer if seed % 2 else (),
                            temp=0.5 if seed < 20 else 1.5)
     add_inversion_choices(net, env)
-    add_top_choices(net, env)
+    _, top_cls = add_top_choices(net, env, restrict=not a.unrestricted, order_seed=a.order_seed)
     outs = [x[0] for x in r]
     print(f"classes {len(net.tt)}, definitions {len(net.defs)}", file=sys.stderr)
     cuts = enum_cuts(net)
-    sel = solve(net, outs, cuts, time_limit=1800)
+    sel = solve(net, outs, cuts, time_limit=a.time_limit, order_cls=top_cls if a.unrestricted else ())
     o = out_tts()
     req = [o[7 - j] for j in range(8)]  # S_j (BP numbering, S0 = MSB) = bit 7-j
     stmts, names, _ = emit_body(net, sel, outs, req)
     assert check_program(net, stmts, names, outs, req), "emitted program does not compute the S-box"
     hdr = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "csrc", "include", "otc_sbox_lut3.h")
+    if a.out:
+        import shutil
+        shutil.copy(hdr, a.out)
+        hdr = a.out
     text = open(hdr).read()
     a = text.index("\n", text.index("    (void)K7; (void)K03;")) + 1
     b = text.index("    x7 = S0; x6 = S1;")
