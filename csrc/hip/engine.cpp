@@ -128,17 +128,13 @@ using namespace otc_rt;
 
 namespace {
 
-/* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  CTR calls of >= 4 GiB
- * run bitsliced at every key size; the crossover sweep
- * (profiles/r3/auto_impl/xover_ctr_128_256.jsonl, 2 reps, in place) puts it
- * between 2 and 4 GiB: AES-128 2 GiB 1443/1453 vs T-table 1480/1476 GB/s,
- * 4 GiB 1542/1547 vs 1506/1509, 8 GiB 1580/1581 vs 1490/1497; AES-256 2 GiB
- * 1103/1099 vs 1108/1124, 4 GiB 1148/1148 vs 1091/1076 (AES-192 at 4 GiB:
- * 1251 vs 1235 in round 2).  64 GiB AES-128: 1607 vs 1533.  Every other mode
- * and smaller calls (the bitsliced grid needs ~768 workgroups to fill the
- * chip, plus two table kernels per call) take the T-table.  ctr_bytes = 0
- * for non-CTR calls.  OTC_IMPL=ttable|bitslice overrides "auto" for the
- * whole process. */
+/* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  CTR calls of >= 2 GiB
+ * (AES-256: >= 1 GiB) run bitsliced, the thresholds below.  Every other mode
+ * (ECB encryption included: profiles/r3/ecb256/xover_ecb_s79.jsonl, T-table
+ * ahead at 1-64 GiB) and smaller calls (the bitsliced grid needs ~768
+ * workgroups to fill the chip, plus two table kernels per call) take the
+ * T-table.  ctr_bytes = 0 for non-CTR calls.  OTC_IMPL=ttable|bitslice
+ * overrides "auto" for the whole process. */
 int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
 {
     if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE) return impl;
