@@ -205,6 +205,13 @@ def solve(net, outs, cuts, time_limit=600, verbose=True, max_iter=30, order_cls=
             if c in lvl and L in lvl:
                 # level(c) - level(L) - big * x_i >= 1 - big
                 add({lvl[c]: 1, lvl[L]: -1, i: -big}, 1 - big, np.inf)
+    # every 2-cycle (c's cut has leaf L, L's cut has leaf c) excluded up front:
+    # the lazy cuts found nearly only those, at one full re-solve each
+    for i, (c, u) in enumerate(var):
+        for L in u:
+            for j in idx_by_cls.get(L, []):
+                if j > i and c in var[j][1]:
+                    add({i: 1, j: 1}, 0, 1)
     cost = np.concatenate([np.ones(nx), np.zeros(nv - nx)])
     integ = np.concatenate([np.ones(nx), np.zeros(nv - nx)])
     upper = np.concatenate([np.ones(nx), np.full(nv - nx, float(big))])

@@ -89,7 +89,8 @@ def schedule(stmts, outputs, seed):
 
 
 def main():
-    text = open(HDR).read()
+    hdr = sys.argv[1] if len(sys.argv) > 1 else HDR  # another header (e.g. an ILP run's --out)
+    text = open(hdr).read()
     lines, stmts, idx = parse(text)
     by = {s[0]: s for s in stmts}
     outputs = {"S%d" % i for i in range(8)}
@@ -105,7 +106,7 @@ def main():
     out = lines[:]
     for k, i in enumerate(idx):
         out[i] = new[k]
-    open(HDR, "w").write("\n".join(out))
+    open(hdr, "w").write("\n".join(out))
     print(f"peak live planes: {start_peak} -> {best_peak}", file=sys.stderr)
 
 
