@@ -26,7 +26,7 @@
  *     sbox_key_terms) come from a per-call table written by k_bs_key_table
  *     and read with scalar loads next to each S-box: no SALU mask arithmetic
  *     and no round-key SGPRs live across the kernel;
- *   - a 79-LUT3 S-box (tools/sbox_choices.py: ILP cover over structural
+ *   - a 77-LUT3 S-box (tools/sbox_choices.py: ILP cover over structural
  *     choices of the circuit) in minimum-live-plane order
  *     (tools/sbox_schedule.py) and a 55-node MixColumns column
  *     (tools/mixcol_search.py; the textbook forms take 76-80);
@@ -267,7 +267,7 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
 /* register plaintext slots issued before the output transposes (2: with the
  * 81-LUT S-box (27 live planes at its peak) 4 early slots spilled in the
  * output phase; with the 79-LUT one (24) they no longer spill but measured
- * 1-1.5% slower, profiles/r3/sbox79) */
+ * 1-1.5% slower, profiles/r3/sbox79; the 77-LUT one peaks at 23) */
 #ifndef OTC_BS_PRE
 #define OTC_BS_PRE 2
 #endif

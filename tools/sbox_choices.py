@@ -17,16 +17,20 @@ and of its output), and a class may have several structural definitions:
 * every 2-LUT decomposition F(g(3 inputs), 2 inputs) of the four GF(2^4)
   inversion outputs;
 * alternative XOR decompositions of the top-layer forms over other forms
-  (round 3, session 2; a fixed order keeps the definitions acyclic).
+  (round 3, session 2; a fixed order keeps the definitions acyclic --
+  --order-seed N breaks ties within a U-weight at random instead of by name,
+  a different DAG restriction each).
 
 Cuts are enumerated over all definitions (fixpoint), the cover ILP
 (scipy/HiGHS) picks one implementation per needed class and minimises LUTs;
-cycles through equivalent classes are removed lazily (a constraint per found
-cycle, re-solve).  The emitted program is checked against the AES S-box on
-all 2^16 (x, k).  Result: 79 LUTs (without the top-layer choices 81; round
-2: 83), in ~7 min.
+every 2-cycle between chosen cuts is excluded up front and longer cycles
+through equivalent classes lazily (a constraint per found cycle, re-solve).
+The emitted program is checked against the AES S-box on all 2^16 (x, k).
+Result: 79 LUTs with the name order (without the top-layer choices 81;
+round 2: 83); 77 with --order-seed 5 (seeds 1-4: 77-79,
+profiles/r3/sbox77/), ~10 min per solve.
 
-    tools/sbox_choices.py            # ~5-10 min (ILP), rewrites the header body
+    tools/sbox_choices.py --order-seed 5   # ~10 min (ILP), rewrites the header body
 """
 import itertools, os, random, sys, time
 import numpy as np
