@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Static instruction counts of the bitsliced bulk kernels in a built object.
+
+Extracts the gfx950 code object from a hipcc object's .hip_fatbin section
+(llvm-objcopy + clang-offload-bundler), disassembles it and prints, for every
+k_aes_bs_t3 instantiation compiled for full tasks only (the bulk launch: one
+2048-block task per wave, straight-line code), the VALU / SALU / SMEM /
+vector-memory instruction counts, VGPRs and scratch bytes.  The kernel has no
+loops, so the static VALU count is the VALU per task that rocprofv3's
+SQ_INSTS_VALU / SQ_WAVES reports (profiles/r3/sbox79: 13,058 vs 13,056.5).
+
+    tools/isa_count.py build/obj/hip/aes_bs.o [build/obj-VARIANT/hip/aes_bs.o ...]
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
+NAMES = {"Li10E": "AES-128", "Li12E": "AES-192", "Li14E": "AES-256"}
+
+
+def code_object(obj, tmp):
+    fat = os.path.join(tmp, "fatbin")
+    co = os.path.join(tmp, "co")
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", obj, os.path.join(tmp, "o")],
+                   check=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--targets={TARGET}",
+                    f"--input={fat}", f"--output={co}"], check=True)
+    return co
+
+
+def metadata(co):
+    """kernel symbol -> (vgpr_count, private_segment_fixed_size) from the notes"""
+    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True,
+                           text=True).stdout
+    out = {}
+    for blk in notes.split("  - .agpr_count:")[1:]:
+        name = re.search(r"\.name:\s+(\S+)", blk)
+        vg = re.search(r"\.vgpr_count:\s+(\d+)", blk)
+        pr = re.search(r"\.private_segment_fixed_size:\s+(\d+)", blk)
+        if name:
+            out[name.group(1)] = (int(vg.group(1)) if vg else -1, int(pr.group(1)) if pr else -1)
+    return out
+
+
+def main():
+    for obj in sys.argv[1:]:
+        with tempfile.TemporaryDirectory() as tmp:
+            co = code_object(obj, tmp)
+            asm = subprocess.run([f"{LLVM}/llvm-objdump", "-d", co], check=True, capture_output=True,
+                                 text=True).stdout
+            meta = metadata(co)
+        for f in re.split(r"\n(?=[0-9a-f]+ <)", asm):
+            m = re.match(r"[0-9a-f]+ <(.*?)>:", f)
+            if not m or "k_aes_bs_t3" not in m.group(1) or "Lb1ELb1E" not in m.group(1):
+                continue
+            name = m.group(1)
+            ins = re.findall(r"^\s+([a-z_0-9]+)", f, re.M)
+            cnt = lambda p: sum(1 for i in ins if i.startswith(p))
+            tm = re.search(r"t3ILi(\d+)ELi(\d)E", name)
+            mode = {"0": "CTR", "1": "ECB"}.get(tm.group(2), "?") if tm else "?"
+            bits = NAMES.get(f"Li{tm.group(1)}E", "?") if tm else "?"
+            vg, scr = meta.get(name + ".kd", meta.get(name, (-1, -1)))
+            print(f"{obj}: {mode} {bits} VALU {cnt('v_')} SALU {cnt('s_') - cnt('s_load') - cnt('s_buffer')} "
+                  f"SMEM {cnt('s_load') + cnt('s_buffer')} VMEM {cnt('global_') + cnt('buffer_')} "
+                  f"LDS {cnt('ds_')} VGPRs {vg} scratch {scr}")
+
+
+if __name__ == "__main__":
+    main()

@@ -543,6 +543,8 @@ def main():
     ap.add_argument("--unrestricted", action="store_true",
                     help="top-layer choices over ALL other forms, acyclicity by level variables")
     ap.add_argument("--order-seed", type=int, help="restricted choices under a random tie order")
+    ap.add_argument("--lazy", action="store_true",
+                    help="with --unrestricted: no level variables, cycles (beyond 2) cut lazily")
     ap.add_argument("--time-limit", type=float, default=1800)
     ap.add_argument("--out", help="write the header here instead of csrc/include/otc_sbox_lut3.h")
     a = ap.parse_args()
@@ -559,7 +561,7 @@ def main():
     outs = [x[0] for x in r]
     print(f"classes {len(net.tt)}, definitions {len(net.defs)}", file=sys.stderr)
     cuts = enum_cuts(net)
-    sel = solve(net, outs, cuts, time_limit=a.time_limit, order_cls=top_cls if a.unrestricted else ())
+    sel = solve(net, outs, cuts, time_limit=a.time_limit, order_cls=top_cls if a.unrestricted and not a.lazy else ())
     o = out_tts()
     req = [o[7 - j] for j in range(8)]  # S_j (BP numbering, S0 = MSB) = bit 7-j
     stmts, names, _ = emit_body(net, sel, outs, req)
