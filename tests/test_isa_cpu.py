@@ -1,0 +1,49 @@
+"""Static guards on the built gfx950 code (no GPU needed): the bitsliced bulk
+kernels stay spill-free and within their VALU budget per 2048-block task
+(tools/isa_count.py; profiles/r3/sbox77: 12,802 AES-128, 18,610 AES-256 --
+the counts rocprofv3 measures, profiles/r3/sbox79/pmc_ctr128_bulk.txt).  A
+register-pressure regression shows up here as scratch > 0 long before a GPU
+run, and a lost optimisation as a VALU jump."""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OBJ = os.path.join(ROOT, "build", "obj", "hip", "aes_bs.o")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+BUDGET = {("CTR", "AES-128"): 12900, ("CTR", "AES-192"): 15800, ("CTR", "AES-256"): 18700}
+
+
+@pytest.fixture(scope="module")
+def counts():
+    if not os.path.exists(OBJ) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):
+        pytest.skip("no built aes_bs.o (make) or no ROCm LLVM tools")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_count.py"), OBJ], check=True,
+                         capture_output=True, text=True).stdout
+    rows = {}
+    for line in out.splitlines():
+        m = re.search(r": (\w+) (AES-\d+) VALU (\d+) .* VGPRs (-?\d+) scratch (-?\d+)", line)
+        if m:
+            rows[(m.group(1), m.group(2))] = (int(m.group(3)), int(m.group(4)), int(m.group(5)))
+    return rows
+
+
+def test_every_bulk_kernel_found(counts):
+    for mode in ("CTR", "ECB"):
+        for bits in ("AES-128", "AES-192", "AES-256"):
+            assert (mode, bits) in counts, (mode, bits, sorted(counts))
+
+
+def test_bulk_kernels_spill_free(counts):
+    for key, (valu, vgprs, scratch) in counts.items():
+        assert scratch == 0, (key, scratch)
+        assert 0 < vgprs <= 168, (key, vgprs)  # 3 waves per SIMD
+
+
+def test_ctr_valu_budget(counts):
+    for key, budget in BUDGET.items():
+        assert counts[key][0] <= budget, (key, counts[key][0], budget)
