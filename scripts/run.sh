@@ -7,7 +7,7 @@
 #   validate            pytest -m gpu, smoke(), default bench.py   (round-end checks)
 #   test [pytest args]  pytest -m gpu (optionally a subset: test tests/test_gpu_engine.py -k cbc)
 #   bench [bench args]  bench.py with the given flags
-#   rehearse N [args]   bench.py --gpus N self-spawned, N ranks sharing the box's GPU (gloo)
+#   rehearse N [args]   bench.py --gpus N --gib 2 self-spawned, N ranks sharing the box's GPU (gloo)
 #   kt NAME -- CMD...   rocprofv3 kernel trace + stats of CMD, summarised to gpurun_out/NAME/kernels.txt
 #   pmc NAME "COUNTERS" -- CMD...   one counter pass (<= 8 SQ, 4 TCC, ...) of CMD, CSV in gpurun_out/NAME
 #   otbench [otbench args]          bin/otbench JSON lines
@@ -55,7 +55,8 @@ bench)
 rehearse)
     n=${1:-2}
     shift || true
-    OTC_DIST_BACKEND=gloo OTC_SHARE_GPUS=1 timeout -k 10 600 python bench.py --gpus "$n" --no-clock "$@" \
+    # N shards must fit ONE GPU: 2 GiB each unless the args say otherwise (argparse keeps the last --gib)
+    OTC_DIST_BACKEND=gloo OTC_SHARE_GPUS=1 timeout -k 10 600 python bench.py --gpus "$n" --no-clock --gib 2 "$@" \
         > $OUT/rehearse_dp$n.txt 2>&1 || { tail -30 $OUT/rehearse_dp$n.txt; exit 1; }
     grep '^{' $OUT/rehearse_dp$n.txt
     ;;
