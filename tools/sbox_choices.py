@@ -545,6 +545,8 @@ def main():
     ap.add_argument("--order-seed", type=int, help="restricted choices under a random tie order")
     ap.add_argument("--lazy", action="store_true",
                     help="with --unrestricted: no level variables, cycles (beyond 2) cut lazily")
+    ap.add_argument("--bottoms", type=int, default=40, help="randomised bottom linear layers offered")
+    ap.add_argument("--top-max", type=int, default=40, help="alternative decompositions per top-layer form")
     ap.add_argument("--time-limit", type=float, default=1800)
     ap.add_argument("--out", help="write the header here instead of csrc/include/otc_sbox_lut3.h")
     a = ap.parse_args()
@@ -553,11 +555,12 @@ def main():
     prods, forms = bottom_targets(env, net)
     made = add_grouped_products(net, env)
     prefer = [(a, b) for a, b, _ in made]
-    for seed in range(40):
+    for seed in range(a.bottoms):
         r = bottom_network(net, env, prods, forms, seed, prefer=prefer if seed % 2 else (),
-                           temp=0.5 if seed < 20 else 1.5)
+                           temp=0.5 if seed < a.bottoms // 2 else 1.5)
     add_inversion_choices(net, env)
-    _, top_cls = add_top_choices(net, env, restrict=not a.unrestricted, order_seed=a.order_seed)
+    _, top_cls = add_top_choices(net, env, max_per_form=a.top_max, restrict=not a.unrestricted,
+                                 order_seed=a.order_seed)
     outs = [x[0] for x in r]
     print(f"classes {len(net.tt)}, definitions {len(net.defs)}", file=sys.stderr)
     cuts = enum_cuts(net)
