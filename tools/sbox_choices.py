@@ -30,6 +30,10 @@ Result: 79 LUTs with the name order (without the top-layer choices 81;
 round 2: 83); 77 with --order-seed 5 (seeds 1-4: 77-79,
 profiles/r3/sbox77/), ~10 min per solve.
 
+Unrestricted choices with level-variable acyclicity (--unrestricted: 2237
+variables, 10552 rows) stopped at its 90-minute limit with a 79-LUT
+incumbent: the big-M rows leave HiGHS a weak relaxation.
+
     tools/sbox_choices.py --order-seed 5   # ~10 min (ILP), rewrites the header body
 """
 import itertools, os, random, sys, time
