@@ -53,6 +53,23 @@ __device__ __forceinline__ uint32_t lds_at(const uint32_t *tbl, uint32_t byte_ad
     return *(const uint32_t *)((const char *)tbl + byte_addr);
 }
 
+/* LDS address of table k's entry for byte k of state word w: byte 1 <- that
+ * byte, bytes 0 / 2 <- the per-lane, per-table constant lkk (whose bytes 1
+ * and 3 are zero).  For k = 1 the byte is already in place, so the address is
+ * one bit-field insert (v_bfi_b32, ~0.75 nJ per wave-instruction) instead of
+ * a v_perm_b32 (~1.03 nJ, profiles/r3/energy/): a quarter of all lookups. */
+__device__ __forceinline__ uint32_t tt_addr(uint32_t w, uint32_t lkk, int k)
+{
+    if (k == 1) {
+        /* written out: hipcc turns the C form into v_and_or_b32 (0.83 nJ,
+         * and a costlier VOP3 issue than v_perm) */
+        uint32_t r;
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x0000FF00u), "v"(w), "v"(lkk));
+        return r;
+    }
+    return __builtin_amdgcn_perm(w, lkk, SEL_HI(k));
+}
+
 /* 4-table layout (TBL4): T_k (k = 0..3, T_k = rotl(T0, 8k)) each replicated
  * 32 ways.  Row x of region r (r = k >> 1, 64 KiB each) holds T_{2r} for lanes
  * 0..31 in bytes 0..127 and T_{2r+1} in bytes 128..255:
@@ -98,7 +115,7 @@ __device__ __forceinline__ void enc_rounds4_from(const uint32_t *tbl, const uint
             for (int b = 0; b < B; ++b)
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    a[b][j][k] = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + k) & 3], lk[k], SEL_HI(k)));
+                    a[b][j][k] = lds_at(tbl, tt_addr(s[b][(j + k) & 3], lk[k], k));
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -117,7 +134,7 @@ __device__ __forceinline__ void enc_rounds4_from(const uint32_t *tbl, const uint
         for (int b = 0; b < B; ++b)
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                a[b][j][k] = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + k) & 3], lk[k], SEL_HI(k)));
+                a[b][j][k] = lds_at(tbl, tt_addr(s[b][(j + k) & 3], lk[k], k));
 #pragma unroll
     for (int b = 0; b < B; ++b) {
 #pragma unroll
@@ -168,10 +185,10 @@ __device__ __forceinline__ void dec_rounds4(const uint32_t *tbl, const uint32_t 
         for (int b = 0; b < B; ++b) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lk[0], SEL_HI(0)));
-                uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lk[1], SEL_HI(1)));
-                uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lk[2], SEL_HI(2)));
-                uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lk[3], SEL_HI(3)));
+                uint32_t a0 = lds_at(tbl, tt_addr(s[b][j], lk[0], 0));
+                uint32_t a1 = lds_at(tbl, tt_addr(s[b][(j + 3) & 3], lk[1], 1));
+                uint32_t a2 = lds_at(tbl, tt_addr(s[b][(j + 2) & 3], lk[2], 2));
+                uint32_t a3 = lds_at(tbl, tt_addr(s[b][(j + 1) & 3], lk[3], 3));
                 t[b][j] = xor3(xor3(a0, a1, a2), a3, K.rk[4 * r + j]);
             }
         }
@@ -185,10 +202,10 @@ __device__ __forceinline__ void dec_rounds4(const uint32_t *tbl, const uint32_t 
     for (int b = 0; b < B; ++b) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            uint32_t a0 = lds_at(tbl, __builtin_amdgcn_perm(s[b][j], lk_is2, SEL_HI(0)) >> 1);
-            uint32_t a1 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 3) & 3], lk_is2, SEL_HI(1)) >> 1);
-            uint32_t a2 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 2) & 3], lk_is2, SEL_HI(2)) >> 1);
-            uint32_t a3 = lds_at(tbl, __builtin_amdgcn_perm(s[b][(j + 1) & 3], lk_is2, SEL_HI(3)) >> 1);
+            uint32_t a0 = lds_at(tbl, tt_addr(s[b][j], lk_is2, 0) >> 1);
+            uint32_t a1 = lds_at(tbl, tt_addr(s[b][(j + 3) & 3], lk_is2, 1) >> 1);
+            uint32_t a2 = lds_at(tbl, tt_addr(s[b][(j + 2) & 3], lk_is2, 2) >> 1);
+            uint32_t a3 = lds_at(tbl, tt_addr(s[b][(j + 1) & 3], lk_is2, 3) >> 1);
             uint32_t lo = __builtin_amdgcn_perm(a1, a0, 0x0c0c0400u);
             uint32_t hi = __builtin_amdgcn_perm(a3, a2, 0x04000c0cu);
             t[b][j] = xor3(lo, hi, K.rk[4 * NR + j]);
@@ -369,10 +386,10 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_
             const uint32_t c15 = (b15 | (uint32_t)(64 * b) | lane) ^ (K.rk[3] >> 24);
             const uint32_t s0 = U0 ^ lds_at(tbl, (c15 << 8) | lk[3]);
             /* round 2: the four lookups fed by s0 */
-            s[b][0] = V0 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[0], SEL_HI(0)));
-            s[b][1] = V1 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[3], SEL_HI(3)));
-            s[b][2] = V2 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[2], SEL_HI(2)));
-            s[b][3] = V3 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[1], SEL_HI(1)));
+            s[b][0] = V0 ^ lds_at(tbl, tt_addr(s0, lk[0], 0));
+            s[b][1] = V1 ^ lds_at(tbl, tt_addr(s0, lk[3], 3));
+            s[b][2] = V2 ^ lds_at(tbl, tt_addr(s0, lk[2], 2));
+            s[b][3] = V3 ^ lds_at(tbl, tt_addr(s0, lk[1], 1));
         }
         /* rounds 3..NR */
         enc_rounds4_from<3, NR, B>(tbl, lk, K, s);
@@ -857,10 +874,10 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_batch_tt(BatchParams P)
                 x[b] = (i >= 0 && (uint64_t)i < nfull) ? gld16(in, (uint64_t)i) : make_uint4(0, 0, 0, 0);
                 const uint32_t c15 = (b15 | (uint32_t)(64 * b) | lane) ^ (K.rk[3] >> 24);
                 const uint32_t s0 = U0 ^ lds_at(tbl, (c15 << 8) | lk[3]);
-                s[b][0] = V0 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[0], SEL_HI(0)));
-                s[b][1] = V1 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[3], SEL_HI(3)));
-                s[b][2] = V2 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[2], SEL_HI(2)));
-                s[b][3] = V3 ^ lds_at(tbl, __builtin_amdgcn_perm(s0, lk[1], SEL_HI(1)));
+                s[b][0] = V0 ^ lds_at(tbl, tt_addr(s0, lk[0], 0));
+                s[b][1] = V1 ^ lds_at(tbl, tt_addr(s0, lk[3], 3));
+                s[b][2] = V2 ^ lds_at(tbl, tt_addr(s0, lk[2], 2));
+                s[b][3] = V3 ^ lds_at(tbl, tt_addr(s0, lk[1], 1));
             }
             enc_rounds4_from<3, NR, B>(tbl, lk, K, s);
         } else {
