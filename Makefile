@@ -43,8 +43,8 @@ HIP_OBJ := $(patsubst csrc/hip/%.hip,$(OBJ)/hip/%.o,$(HIP_SRC)) $(OBJ)/hip/engin
 BINS := bin/test bin/aes_test bin/aes_ecb_e bin/aes_ecb_d bin/otbench bin/bc_test
 
 .PHONY: all cpu clean
-all: $(LIBDIR)/libotc.so $(LIBDIR)/libotc_cpu.so $(BINS) bin/test_cpu bin/aes_test_cpu ref-o0
-cpu: $(LIBDIR)/libotc_cpu.so bin/test_cpu bin/aes_test_cpu ref-o0
+all: $(LIBDIR)/libotc.so $(LIBDIR)/libotc_cpu.so $(BINS) bin/test_cpu bin/aes_test_cpu bin/otbench_hostsim ref-o0
+cpu: $(LIBDIR)/libotc_cpu.so bin/test_cpu bin/aes_test_cpu bin/otbench_hostsim ref-o0
 
 $(OBJ)/cpu/aesni.o: csrc/cpu/aesni.c csrc/include/aesni.h
 	@mkdir -p $(dir $@)
@@ -108,6 +108,12 @@ bin/otbench: csrc/cli/otbench.cpp $(LIBDIR)/libotc.so
 	@mkdir -p bin
 	$(CXX) -O2 -std=c++17 $(INC) $< -o $@ -L$(LIBDIR) -lotc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
 
+# otbench over a host-memory double of the device API (CPU tests of its
+# argument / snapshot / verification logic, tests/test_otbench_cpu.py)
+bin/otbench_hostsim: csrc/cli/otbench.cpp csrc/cli/otc_hostsim.cpp $(CPU_OBJ)
+	@mkdir -p bin
+	$(CXX) -O2 -std=c++17 -Wall $(INC) csrc/cli/otbench.cpp csrc/cli/otc_hostsim.cpp $(CPU_OBJ) -o $@ -lpthread
+
 bin/bc_test: csrc/cli/bc_test.cpp csrc/include/otc_cipher.hpp $(LIBDIR)/libotc.so
 	@mkdir -p bin
 	$(CXX) -O2 -std=c++17 -Wall $(INC) $< -o $@ -L$(LIBDIR) -lotc -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
@@ -153,7 +159,7 @@ bin/aes_test_o0: csrc/cli/aes_test.c $(O0_OBJ)
 	$(CXX) -O0 -g $(INC) -x c -std=gnu99 $< -x none $(O0_OBJ) -o $@ -lpthread
 
 clean:
-	rm -rf build $(LIBDIR)/*.so $(BINS) bin/test_cpu bin/aes_test_cpu bin/test_o0 bin/aes_test_o0
+	rm -rf build $(LIBDIR)/*.so $(BINS) bin/otbench_hostsim bin/test_cpu bin/aes_test_cpu bin/test_o0 bin/aes_test_o0
 
 # Host sanitizers over the threaded CPU paths (also tests/test_sanitizers_cpu.py)
 SAN_SRC := csrc/cpu/aes.c csrc/cpu/arc4.c csrc/cli/san_driver.c

@@ -11,10 +11,21 @@ Timing: W untimed warmup steps, barrier + synchronize, K timed steps,
 synchronize + barrier, MAX over ranks.  Correctness is checked on a sample of
 every shard against the CPU oracle before timing.
 
+Per rank (``per_rank``): its own GB/s over the same steps, the clock it held,
+its verification, and -- the chip runs against its package power limit, so
+throughput follows energy per byte -- the socket energy over exactly the timed
+steps (amdsmi energy counter), average power, J/GB and the fraction of the
+window the PPT limit was active.  Whole node: ``joules_per_gb``,
+``avg_socket_w_per_gpu``, ``ppt_residency_max``.
+
 Multi-GPU: ``python bench.py --gpus N`` without a launcher spawns N fresh
 worker processes itself (parallel/launch.py) before anything touches the GPU;
 under torchrun WORLD_SIZE must equal --gpus.  Fewer visible GPUs than --gpus
 is an error (exit 2) -- a multi-GPU request is never measured on fewer GPUs.
+Before any large allocation a bounded preflight moves 16 MiB through a scatter
+and an all_gather and checks every byte (parallel/preflight.py): a broken
+peer transport ends the run with one error JSON line after --preflight-timeout
+seconds instead of hanging.
 
 Communication: the resident CTR step needs none (every rank owns its shard),
 so an extra, separately timed pass runs BASELINE config 4 in miniature -- an
@@ -25,26 +36,41 @@ of every rank's output is checked against the C oracle (``rccl_ranks_verified``)
 the xGMI bytes reported are those of the verified pieces.  A second extra
 streams a few GiB per rank from pinned, NUMA-placed host memory through the
 3-stream H2D | kernel | D2H pipeline (BASELINE config 5 in miniature) and
-reports every rank's NUMA node and per-direction PCIe rate.
+reports every rank's NUMA node and per-direction PCIe rate.  A third reruns
+the reference's own GPU measurement (AES-256 ECB, 1000 MiB, allocation and
+pageable copies inside the timer, main_ecb_e.cu:37-44) beside the pinned and
+kernel-only figures for the same buffer (utils/refmethod.py).
+
+``--device cpu`` rehearses the whole flow (launch, preflight, per-rank
+gather, JSON) on the host with gloo and the C oracle, tiny shards.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--gib 64]
         torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
 
-import argparse
-import json
 import os
-import sys
-import time
 
-import torch
+# Before torch / HIP load, for every way this script is started (self-spawned
+# ranks, torchrun, plain python): this host driver supports dmabuf IPC only,
+# and RCCL's peer transport fails (hipIpcGetMemHandle: invalid argument)
+# without it.  setdefault: an explicit value from the caller wins.
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import argparse  # noqa: E402
+import json  # noqa: E402
+import sys  # noqa: E402
+import time  # noqa: E402
+
+import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_GBPS = 0.519  # BASELINE.md headline CTR: AES-NI CTR-256, 1000 MiB, 8 threads (frankchn)
 BASELINE_GPU_GBPS = 2.41  # BASELINE.md repo headline: CUDA "AES ECB" 1000 MiB (baryon)
 AES128_EQUIV = 14 / 10  # AES-256 -> AES-128 round ratio (BASELINE.md caveat 5: derived, not published)
+RANK_KEYS = ("gbps", "held_clock_ghz", "verified", "joules", "avg_socket_w", "joules_per_gb", "ppt_residency",
+             "gfxclk_mhz_mean", "xgmi_read_kb", "xgmi_write_kb")
 
 
 def baseline_ratios(value: float) -> dict:
@@ -58,6 +84,40 @@ def baseline_ratios(value: float) -> dict:
         "vs_baseline_what": "AES-128-CTR GB/s / 0.519 GB/s AES-NI CTR-256 1000 MiB 8 threads "
                             "(aes-modes/results.frankchn.aesni:32; no AES-128 number is published)",
         "vs_baseline_aes128_equiv": round(value / (BASELINE_GBPS * AES128_EQUIV), 2),
+    }
+
+
+def per_rank_table(rows: list[list[float]]) -> list[dict]:
+    """Rows of floats in RANK_KEYS order (nan = not measured) -> one dict per
+    rank, ``verified`` as a bool, unmeasured values as None."""
+    out = []
+    for r, row in enumerate(rows):
+        d = {"rank": r}
+        for k, v in zip(RANK_KEYS, row):
+            if k == "verified":
+                d[k] = bool(v == 1.0)
+            elif v != v:  # nan
+                d[k] = None
+            elif k.startswith("xgmi"):
+                d[k] = int(v)
+            else:
+                d[k] = round(v, 4 if k in ("joules_per_gb", "ppt_residency", "held_clock_ghz") else 3)
+        out.append(d)
+    return out
+
+
+def node_energy(table: list[dict], total_bytes: int) -> dict:
+    """Whole-node energy keys from the per-rank table (None when no rank
+    could read its power counters)."""
+    js = [d["joules"] for d in table if d["joules"] is not None]
+    ws = [d["avg_socket_w"] for d in table if d["avg_socket_w"] is not None]
+    pp = [d["ppt_residency"] for d in table if d["ppt_residency"] is not None]
+    full = len(js) == len(table)
+    return {
+        "joules_per_gb": round(sum(js) / (total_bytes / 1e9), 4) if full and js else None,
+        "avg_socket_w_per_gpu": round(sum(ws) / len(ws), 1) if ws else None,
+        "ppt_residency_max": round(max(pp), 4) if pp else None,
+        "energy_ranks": len(js),
     }
 
 
@@ -99,14 +159,7 @@ def stream_pass(args, key, counter, rank, world, local, block0):
         numa = eng.numa_node
     el = pdist.allreduce_max(mine)
     ok_all = pdist.allreduce_max(0.0 if ok else 1.0) == 0.0
-    row = [float(rank), float(numa), h2d, d2h, win * args.stream_passes / mine / 1e9]
-    rows = [row]
-    if torch.distributed.is_initialized():
-        dev = torch.device("cuda", local) if torch.distributed.get_backend() == "nccl" else "cpu"
-        t = torch.tensor(row, dtype=torch.float64, device=dev)
-        outs = [torch.empty_like(t) for _ in range(world)]
-        torch.distributed.all_gather(outs, t)
-        rows = [o.cpu().tolist() for o in outs]
+    rows = pdist.gather_floats([float(rank), float(numa), h2d, d2h, win * args.stream_passes / mine / 1e9])
     del hin, hout
     return {
         "stream_ctr_gbps_whole_node": round(win * args.stream_passes * world / el / 1e9, 3),
@@ -124,19 +177,32 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--gib", type=float, default=64.0, help="per-GPU shard size in GiB")
     ap.add_argument("--impl", default=os.environ.get("OTC_BENCH_IMPL", "auto"))
+    ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
+                    help="cpu: rehearse the flow on the host (gloo, C oracle, tiny shards)")
     ap.add_argument("--no-aes256", action="store_true")
     ap.add_argument("--no-bitslice", "--no-other-impl", dest="no_other", action="store_true",
                     help="skip timing the other AES-128 CTR kernel (T-table vs bitsliced) on the same shard")
     ap.add_argument("--no-clock", action="store_true")
+    ap.add_argument("--no-power", action="store_true", help="skip the amdsmi energy / power / PPT counters")
     ap.add_argument("--no-scatter", action="store_true", help="skip the RCCL scatter/gather AES-256-CBC pass")
     ap.add_argument("--scatter-mib", type=int, default=512, help="per-rank bytes per scatter round (MiB)")
     ap.add_argument("--scatter-rounds", type=int, default=4)
     ap.add_argument("--no-stream", action="store_true", help="skip the host-streamed CTR pass")
     ap.add_argument("--stream-gib", type=float, default=2.0, help="pinned host window per rank (GiB)")
     ap.add_argument("--stream-passes", type=int, default=3)
+    ap.add_argument("--no-refmethod", action="store_true",
+                    help="skip the reference-methodology AES-256 ECB 1000 MiB rows")
     ap.add_argument("--timeout", type=float, default=1800.0,
                     help="seconds before a self-spawned multi-GPU run is stopped (all ranks)")
+    ap.add_argument("--preflight-timeout", type=float, default=120.0)
+    ap.add_argument("--preflight-fault-rank", type=int, default=None, help=argparse.SUPPRESS)  # test hook
+    ap.add_argument("--preflight-hang-rank", type=int, default=None, help=argparse.SUPPRESS)  # test hook
     args = ap.parse_args()
+    cpu = args.device == "cpu"
+    if cpu:
+        os.environ.setdefault("OTC_DIST_BACKEND", "gloo")
+        os.environ.setdefault("OTC_SHARE_GPUS", "1")  # ranks are host processes: no GPU count applies
+        args.no_clock = args.no_power = args.no_stream = args.no_refmethod = True
 
     # decide the launch before any HIP call (spawned ranks re-enter here with
     # RANK/WORLD_SIZE set); exits on error or when the spawned run finished
@@ -154,25 +220,43 @@ def main():
     def emit(obj):
         os.write(result_fd, (json.dumps(obj) + "\n").encode())
 
-    from our_tree_amd import ops
     from our_tree_amd.models import cpu_ref
     from our_tree_amd.parallel import dist as pdist
-    from our_tree_amd.utils import device as dinfo
+    from our_tree_amd.parallel import preflight
 
-    # The clock probe's stream is created before RCCL creates its streams: a
-    # later one shared a hardware queue with the compute stream (4 per process
-    # here), so the probe ran after the steps and read the idle clock (2.4 GHz
-    # instead of the ~2.0 held under load).
-    gpu = pdist.local_gpu()
-    torch.cuda.set_device(gpu)
-    probe_stream = torch.cuda.Stream(device=gpu, priority=-1)
+    probe_stream = None
+    if not cpu:
+        # The clock probe's stream is created before RCCL creates its streams: a
+        # later one shared a hardware queue with the compute stream (4 per process
+        # here), so the probe ran after the steps and read the idle clock (2.4 GHz
+        # instead of the ~2.0 held under load).
+        gpu = pdist.local_gpu()
+        torch.cuda.set_device(gpu)
+        probe_stream = torch.cuda.Stream(device=gpu, priority=-1)
 
     # a process group even at N=1 (a 1-rank RCCL group) so the scatter pass
     # always runs the collective code path
     rank, world, local = pdist.init_from_env(force=not args.no_scatter)
     assert world == args.gpus, (world, args.gpus)  # launch.dispatch guarantees it
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+
+    def on_timeout(r, t):
+        msg = {"error": f"preflight: scatter/all_gather did not finish within {t:.0f} s "
+                        "(peer transport / IPC failure?)", "rank": r}
+        if r == 0:
+            emit(msg)
+        print(json.dumps(msg), file=sys.stderr, flush=True)
+        os._exit(3)
+
+    pre = preflight.run(timeout_s=args.preflight_timeout, on_timeout=on_timeout,
+                        fault_rank=args.preflight_fault_rank, hang_rank=args.preflight_hang_rank)
+    if not pre["ok"]:
+        if rank == 0:
+            emit({"error": "preflight verification failed", "preflight": pre})
+        sys.exit(1)
+
+    dev = torch.device("cpu") if cpu else torch.device("cuda", local)
+    if not cpu:
+        torch.cuda.set_device(dev)
 
     nbytes = int(args.gib * (1 << 30))
     nbytes -= nbytes % 16
@@ -183,82 +267,139 @@ def main():
     shard_blocks = nbytes // 16
     my_block0 = rank * shard_blocks
 
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize()
+
     buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    ops.fill_random_(buf, seed=1000 + rank)
+    if cpu:
+        buf.copy_(torch.randint(0, 256, (nbytes,), generator=torch.Generator().manual_seed(1000 + rank),
+                                dtype=torch.uint8))
+        resolved = "cpu-oracle"
+    else:
+        from our_tree_amd import ops
+
+        ops.fill_random_(buf, seed=1000 + rank)
+        resolved = ops.pick_impl(args.impl, 128, "ctr", nbytes)  # the kernel the headline runs
+
+    def step(k=key, impl=args.impl):
+        if cpu:
+            pdist._ctr_local(buf, k, counter, my_block0)
+        else:
+            ops.ctr(buf, k, counter, out=buf, block_offset=my_block0, impl=impl)
 
     # ---- correctness on a sample (outside the timed region) ----------------
-    S = 1 << 16
-    head = buf[:S].cpu().numpy().tobytes()
-    tail_off = nbytes - S
-    tail = buf[tail_off:].cpu().numpy().tobytes()
-    ops.ctr(buf, key, counter, out=buf, block_offset=my_block0, impl=args.impl)
-    torch.cuda.synchronize()
-    ok = (buf[:S].cpu().numpy().tobytes() == cpu_ref.ctr(key, counter, head, my_block0)
-          and buf[tail_off:].cpu().numpy().tobytes()
-          == cpu_ref.ctr(key, counter, tail, my_block0 + tail_off // 16))
+    S = min(1 << 16, nbytes // 2 - (nbytes // 2) % 16)
+
+    def verify_once(k, impl=args.impl) -> bool:
+        """one untimed step on the live (in-place) buffer, head and tail
+        samples checked against the oracle -- run before each timed config"""
+        head = buf[:S].cpu().numpy().tobytes()
+        tail = buf[nbytes - S:].cpu().numpy().tobytes()
+        step(k, impl)
+        sync()
+        return (buf[:S].cpu().numpy().tobytes() == cpu_ref.ctr(k, counter, head, my_block0)
+                and buf[nbytes - S:].cpu().numpy().tobytes()
+                == cpu_ref.ctr(k, counter, tail, my_block0 + (nbytes - S) // 16))
+
+    ok = verify_once(key)
     ok_all = pdist.allreduce_max(0.0 if ok else 1.0) == 0.0
     if not ok_all:
         if rank == 0:
             emit({"error": "verification failed"})
         sys.exit(1)
 
-    def step(k=key, impl=args.impl):
-        ops.ctr(buf, k, counter, out=buf, block_offset=my_block0, impl=impl)
+    meter = None
+    if not args.no_power:
+        from our_tree_amd.utils.power import PowerMeter
 
-    def timed(nsteps, k, impl=args.impl):
+        meter = PowerMeter(local)
+
+    def timed(nsteps, k, impl=args.impl, measure=False):
+        """returns (MAX over ranks of the barrier-to-barrier time, this rank's
+        own time to its last synchronize, power stats of this rank or None)"""
         for _ in range(args.warmup):
             step(k, impl)
-        torch.cuda.synchronize()
+        sync()
         if torch.distributed.is_initialized():
             torch.distributed.barrier()
-        torch.cuda.synchronize()
+        sync()
+        if measure and meter is not None:
+            meter.start()
         t0 = time.perf_counter()
         for _ in range(nsteps):
             step(k, impl)
-        torch.cuda.synchronize()
+        sync()
+        mine = time.perf_counter() - t0
+        pw = meter.stop(nbytes * nsteps) if measure and meter is not None else None
         if torch.distributed.is_initialized():
             torch.distributed.barrier()
         el = time.perf_counter() - t0
-        return pdist.allreduce_max(el)
+        return pdist.allreduce_max(el), mine, pw
 
-    resolved = ops.pick_impl(args.impl, 128, "ctr", nbytes)  # the kernel the headline runs
-    elapsed = timed(args.steps, key)
+    elapsed, mine, pw = timed(args.steps, key, measure=True)
     ms_per_step = elapsed / args.steps * 1e3
     total_bytes = nbytes * world * args.steps
     value = total_bytes / elapsed / 1e9
 
-    info = dinfo.info(local)
-    cpb = (ms_per_step * 1e-3) * info["clock_hz"] * info["cus"] / nbytes
-
-    # Clock the chip holds under this load (untimed extra steps with the
-    # one-wave probe beside them): cycles/byte/CU at the nominal clock
-    # overstates the cycle count when the chip lowers its clock.
     clk_ghz = None
-    if not args.no_clock:
-        n_clk = max(3, int(0.3 / max(ms_per_step * 1e-3, 1e-6)) + 1)
-        window = 0.6 * n_clk * ms_per_step * 1e-3
-        probe = ops.clock_probe(0.2 * n_clk * ms_per_step * 1e-3, window, device=dev, stream=probe_stream)
-        for _ in range(n_clk):
-            step()
-        torch.cuda.synchronize()
-        clk_ghz = ops.clock_ghz(probe)
-    cpb_eff = (ms_per_step * 1e-3) * clk_ghz * 1e9 * info["cus"] / nbytes if clk_ghz else None
+    cus, clock_hz = 256, 2.4e9
+    if not cpu:
+        from our_tree_amd.utils import device as dinfo
+
+        info = dinfo.info(local)
+        cus, clock_hz = info["cus"], info["clock_hz"]
+        # Clock the chip holds under this load (untimed extra steps with the
+        # one-wave probe beside them): cycles/byte/CU at the nominal clock
+        # overstates the cycle count when the chip lowers its clock.
+        if not args.no_clock:
+            n_clk = max(3, int(0.3 / max(ms_per_step * 1e-3, 1e-6)) + 1)
+            window = 0.6 * n_clk * ms_per_step * 1e-3
+            probe = ops.clock_probe(0.2 * n_clk * ms_per_step * 1e-3, window, device=dev, stream=probe_stream)
+            for _ in range(n_clk):
+                step()
+            torch.cuda.synchronize()
+            clk_ghz = ops.clock_ghz(probe)
+    cpb = (ms_per_step * 1e-3) * clock_hz * cus / nbytes
+    cpb_eff = (ms_per_step * 1e-3) * clk_ghz * 1e9 * cus / nbytes if clk_ghz else None
+
+    nan = float("nan")
+    pwv = pw if pw and pw.get("available") else {}
+    row = [nbytes * args.steps / mine / 1e9, clk_ghz if clk_ghz else nan, 1.0 if ok else 0.0]
+    row += [float(pwv[k]) if pwv.get(k) is not None else nan
+            for k in ("joules", "avg_socket_w", "joules_per_gb", "ppt_residency", "gfxclk_mhz_mean",
+                      "xgmi_read_kb", "xgmi_write_kb")]
+    table = per_rank_table(pdist.gather_floats(row))
+    energy = node_energy(table, total_bytes)
+    if meter is not None and not pwv:
+        energy["energy_unavailable"] = pw.get("reason") if pw else "no window"
 
     extra = {}
-    if not args.no_other:
+    if not args.no_other and not cpu:
         # the other AES-128 CTR kernel on the same shard, same protocol: the
         # headline's "auto" runs the bitsliced VALU kernel at this size (BASELINE
         # config 3 names it), the LDS T-table kernel is timed beside it
         other = "ttable" if resolved == "bitslice" else "bitslice"
+        name = "ttable" if other == "ttable" else "bitsliced"
+        v_ok = pdist.allreduce_max(0.0 if verify_once(key, other) else 1.0) == 0.0
         o_steps = max(1, min(args.steps, 5))
-        el_o = timed(o_steps, key, impl=other)
-        extra[("ttable" if other == "ttable" else "bitsliced") + "_ctr_gbps_whole_node"] = round(
-            nbytes * world * o_steps / el_o / 1e9, 3)
+        el_o, _, _ = timed(o_steps, key, impl=other)
+        extra[name + "_ctr_gbps_whole_node"] = round(nbytes * world * o_steps / el_o / 1e9, 3)
+        extra[name + "_ctr_verified"] = v_ok
     if not args.no_aes256:
+        v_ok = pdist.allreduce_max(0.0 if verify_once(key256) else 1.0) == 0.0
         k256_steps = max(1, min(args.steps, 5))
-        el256 = timed(k256_steps, key256)
+        el256, _, _ = timed(k256_steps, key256)
         extra["aes256_ctr_gbps_whole_node"] = round(nbytes * world * k256_steps / el256 / 1e9, 3)
+        extra["aes256_ctr_verified"] = v_ok
         extra["aes256_vs_cpu_aesni_ctr256"] = round(extra["aes256_ctr_gbps_whole_node"] / BASELINE_GBPS, 1)
+
+    bad = [k for k in ("ttable_ctr_verified", "bitsliced_ctr_verified", "aes256_ctr_verified")
+           if extra.get(k) is False]
+    if bad:
+        if rank == 0:
+            emit({"error": "extra verification failed", "failed": bad, **extra})
+        sys.exit(1)
 
     if not args.no_stream:
         extra.update(stream_pass(args, key, counter, rank, world, local, my_block0))
@@ -271,9 +412,11 @@ def main():
         from our_tree_amd.parallel import jobs
 
         del buf  # the scatter pass needs its own buffers (4 x world x chunk on the root)
-        torch.cuda.empty_cache()
-        sc = jobs.cbc_scatter_job(args.scatter_rounds, args.scatter_mib << 20, key256,
-                                  bytes(range(0xA0, 0xB0)), sector=4096, device=dev)
+        if not cpu:
+            torch.cuda.empty_cache()
+        chunk = (args.scatter_mib << 20) if not cpu else 4096 * 8
+        sc = jobs.cbc_scatter_job(args.scatter_rounds, chunk, key256, bytes(range(0xA0, 0xB0)), sector=4096,
+                                  device=dev)
         extra["rccl_cbc256_scatter_gbps"] = round(sc["gbps"], 3)
         extra["rccl_ranks"] = sc["ranks"]
         extra["rccl_ranks_verified"] = sc["ranks_verified"]
@@ -285,6 +428,17 @@ def main():
         if not sc["verified"]:
             if rank == 0:
                 emit({"error": "RCCL scatter/gather verification failed", "per_rank_ok": sc["per_rank_ok"], **extra})
+            sys.exit(1)
+
+    if not args.no_refmethod:
+        from our_tree_amd.utils import refmethod
+
+        if rank == 0:
+            extra.update(refmethod.ecb256_three_ways(device=local))
+        if torch.distributed.is_initialized():
+            torch.distributed.barrier()
+        if rank == 0 and not extra["refmethod_verified"]:
+            emit({"error": "reference-methodology ECB verification failed", **extra})
             sys.exit(1)
 
     if rank == 0:
@@ -310,17 +464,25 @@ def main():
                 "in_place": True,
                 "impl": args.impl,
                 "impl_resolved": resolved,
+                "device": args.device,
             },
             "cycles_per_byte_per_cu": round(cpb, 4),
             "cycles_per_byte_per_cu_at_held_clock": round(cpb_eff, 4) if cpb_eff else None,
             "held_clock_ghz": round(clk_ghz, 3) if clk_ghz else None,
             "per_gpu_gbps": round(value / world, 3),
+            "per_rank_gbps_min": round(min(d["gbps"] for d in table), 3),
+            **energy,
+            "per_rank": table,
+            "preflight": {"ok": pre["ok"], "seconds": pre["seconds"], "bytes": pre["bytes"],
+                          "backend": pre["backend"]},
             "baseline": {"value_gbps": BASELINE_GBPS, "what": "AES-NI CTR-256 1000MiB 8thr (BASELINE.md)",
                          "gpu_headline_gbps": BASELINE_GPU_GBPS},
-            "verified_sample": True,
+            "verified_sample": all(d["verified"] for d in table),
             **extra,
         }
         emit(line)
+    if meter is not None:
+        meter.close()
     if torch.distributed.is_initialized():
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

@@ -39,6 +39,17 @@
 
 using namespace otc_dev;
 
+/* compile-time A/B switches (make variant NAME=x VFLAGS=-D...; docs/PERF.md) */
+#ifndef OTC_TT_PF
+#define OTC_TT_PF 0 /* software-pipelined input loads in the ECB / decrypt kernels */
+#endif
+#ifndef OTC_TT_ENC_B
+#define OTC_TT_ENC_B 4 /* blocks per lane, bulk ECB-encrypt / CFB-decrypt kernel */
+#endif
+#ifndef OTC_TT_DEC_B
+#define OTC_TT_DEC_B 4 /* blocks per lane, bulk ECB / CBC decrypt kernel */
+#endif
+
 namespace {
 
 __device__ const AesTables g_tab = make_tables();
@@ -265,6 +276,44 @@ __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key
     tbl4_lane_consts(lane, lk);
     constexpr uint64_t PER = (uint64_t)THREADS * B;
 
+    if constexpr (MODE == E_ECB && OTC_TT_PF) {
+        /* software-pipelined input: the next iteration's B blocks are loaded
+         * before this iteration's rounds, so no wave starts its rounds behind
+         * an HBM round trip (in place is safe: the blocks loaded ahead belong
+         * to the next iteration, stored only after it loaded them) */
+        const uint64_t stride = (uint64_t)gridDim.x * PER;
+        uint4 nx[B];
+        auto load = [&](uint64_t bs) {
+            const bool full = bs + PER <= P.nfull;
+            const uint64_t i0 = bs + (uint64_t)wave * 64u * B + lane;
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const uint64_t i = i0 + 64u * b;
+                nx[b] = (full || i < P.nfull) ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
+            }
+        };
+        uint64_t base = (uint64_t)blockIdx.x * PER;
+        if (base < P.nfull) load(base);
+        for (; base < P.nfull; base += stride) {
+            const bool full = base + PER <= P.nfull;
+            const uint64_t i0 = base + (uint64_t)wave * 64u * B + lane;
+            uint32_t s[B][4];
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                s[b][0] = nx[b].x ^ K.rk[0]; s[b][1] = nx[b].y ^ K.rk[1];
+                s[b][2] = nx[b].z ^ K.rk[2]; s[b][3] = nx[b].w ^ K.rk[3];
+            }
+            if (base + stride < P.nfull) load(base + stride);
+            enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const uint64_t i = i0 + 64u * b;
+                if (full || i < P.nfull) st16(P.out, i, make_uint4(s[b][0], s[b][1], s[b][2], s[b][3]));
+            }
+        }
+        return;
+    }
+
     for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nfull; base += (uint64_t)gridDim.x * PER) {
         const bool full = base + PER <= P.nfull; /* wave-uniform */
         const uint64_t i0 = base + (uint64_t)wave * 64u * B + lane;
@@ -427,6 +476,69 @@ __global__ __launch_bounds__(THREADS) void k_aes_dec_tt(DecParams P, otc_aes_key
     tbl4_lane_consts(lane, lk);
     const uint32_t lk_is2 = 0x40000u | ((lane & 31u) << 3);
     constexpr uint64_t PER = (uint64_t)THREADS * B;
+
+    if constexpr (OTC_TT_PF) {
+        /* software-pipelined input (see k_aes_enc_tt): block i and, for CBC,
+         * its predecessor (or the IV at a chain start) of the next iteration
+         * are loaded before this iteration's rounds */
+        const uint64_t stride = (uint64_t)gridDim.x * PER;
+        uint4 nx[B], np[B];
+        auto load = [&](uint64_t bs) {
+            const bool full = bs + PER <= P.nfull;
+            const uint64_t i0 = bs + (uint64_t)wave * 64u * B + lane;
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const uint64_t i = i0 + 64u * b;
+                const bool ok = full || i < P.nfull;
+                nx[b] = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
+                if (MODE == D_CBC || MODE == D_CBC_SEG) {
+                    bool first;
+                    Ctr128 ivv = P.iv;
+                    if (MODE == D_CBC) {
+                        first = (i == 0);
+                    } else {
+                        first = (i & ((1ull << P.seg_shift) - 1)) == 0;
+                        const uint64_t seg = i >> P.seg_shift;
+                        ivv.lo = P.iv.lo + seg;
+                        ivv.hi = P.iv.hi + (ivv.lo < P.iv.lo ? 1 : 0);
+                    }
+                    if (first) {
+                        uint32_t w0, w1, w2, w3;
+                        ctr_words(ivv, 0, false, w0, w1, w2, w3);
+                        np[b] = make_uint4(w0, w1, w2, w3);
+                    } else {
+                        np[b] = ok ? ld16(P.in, i - 1) : make_uint4(0, 0, 0, 0);
+                    }
+                }
+            }
+        };
+        uint64_t base = (uint64_t)blockIdx.x * PER;
+        if (base < P.nfull) load(base);
+        for (; base < P.nfull; base += stride) {
+            const bool full = base + PER <= P.nfull;
+            const uint64_t i0 = base + (uint64_t)wave * 64u * B + lane;
+            uint32_t s[B][4];
+            uint4 prev[B];
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                s[b][0] = nx[b].x ^ K.rk[0]; s[b][1] = nx[b].y ^ K.rk[1];
+                s[b][2] = nx[b].z ^ K.rk[2]; s[b][3] = nx[b].w ^ K.rk[3];
+                if (MODE != D_ECB) prev[b] = np[b];
+            }
+            if (base + stride < P.nfull) load(base + stride);
+            dec_rounds4<NR, B>(tbl, lk, lk_is2, K, s);
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                const uint64_t i = i0 + 64u * b;
+                uint4 o = make_uint4(s[b][0], s[b][1], s[b][2], s[b][3]);
+                if (MODE != D_ECB) {
+                    o.x ^= prev[b].x; o.y ^= prev[b].y; o.z ^= prev[b].z; o.w ^= prev[b].w;
+                }
+                if (full || i < P.nfull) st16(P.out, i, o);
+            }
+        }
+        return;
+    }
 
     for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nfull; base += (uint64_t)gridDim.x * PER) {
         const bool full = base + PER <= P.nfull;
@@ -951,9 +1063,9 @@ inline SmallShape small_shape(uint64_t nblocks)
 }
 
 constexpr int ENC_THREADS = 1024; /* measured best of 256..1024 x B=1..4 (docs/PERF.md) */
-constexpr int ENC_B = 4;
+constexpr int ENC_B = OTC_TT_ENC_B;
 constexpr int DEC_THREADS = 1024;
-constexpr int DEC_B = 4;
+constexpr int DEC_B = OTC_TT_DEC_B;
 constexpr int SEG_THREADS = 1024;
 constexpr int SEG_B = 2;
 

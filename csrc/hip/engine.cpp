@@ -140,8 +140,12 @@ int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
     if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE) return impl;
     static const int env = [] {
         const char *e = getenv("OTC_IMPL");
-        if (e && !strcmp(e, "ttable")) return OTC_IMPL_TTABLE;
-        if (e && !strcmp(e, "bitslice")) return OTC_IMPL_BITSLICE;
+        if (!e || !*e || !strcmp(e, "auto")) return OTC_IMPL_AUTO;
+        if (!strcmp(e, "ttable")) return OTC_IMPL_TTABLE;
+        if (!strcmp(e, "bitslice")) return OTC_IMPL_BITSLICE;
+        /* an old or mistyped value (e.g. the removed "hybrid") must not
+         * silently select a different kernel: say so once */
+        fprintf(stderr, "otc: ignoring OTC_IMPL=%s (expected auto, ttable or bitslice)\n", e);
         return OTC_IMPL_AUTO;
     }();
     if (env != OTC_IMPL_AUTO) return env;
@@ -245,8 +249,8 @@ static int ctr_common(const void *in, void *out, size_t nbytes, const otc_aes_ke
     int r = check_key(k, OTC_DIR_ENCRYPT);
     if (r) return r;
     if ((r = check_bufs(in, out, nbytes, true, "aes_ctr"))) return r;
+    if ((r = check_impl(impl))) return r; /* before the empty-call return, as otc_aes_ecb */
     if (nbytes == 0) return OTC_OK;
-    if ((r = check_impl(impl))) return r;
     hipStream_t st = (hipStream_t)stream;
     const int im = pick_impl(impl, k->bits, nbytes);
     g_last_impl = im;
@@ -524,10 +528,14 @@ extern "C" int otc_rc4_crypt_batch(void *states, size_t nstreams, size_t len, co
     if (!states || !in || !out) return set_err(OTC_ERR_ARG, "rc4_crypt_batch: null buffer");
     if ((uintptr_t)states & 3u) return set_err(OTC_ERR_ARG, "rc4_crypt_batch: states must be 4-byte aligned");
     if (len > SIZE_MAX / nstreams) return set_err(OTC_ERR_ARG, "size overflow");
-    if (in != out) {
-        const uintptr_t a = (uintptr_t)in, b = (uintptr_t)out, n = nstreams * len;
-        if (a < b + n && b < a + n) return set_err(OTC_ERR_ARG, "rc4_crypt_batch: input and output overlap partially");
-    }
+    const uintptr_t a = (uintptr_t)in, b = (uintptr_t)out, n = nstreams * len;
+    if (in != out && a < b + n && b < a + n)
+        return set_err(OTC_ERR_ARG, "rc4_crypt_batch: input and output overlap partially");
+    /* every state is written back in place: it must not alias the data */
+    if (nstreams > SIZE_MAX / 264) return set_err(OTC_ERR_ARG, "size overflow");
+    const uintptr_t s = (uintptr_t)states, sn = (uintptr_t)nstreams * 264u;
+    if ((s < a + n && a < s + sn) || (s < b + n && b < s + sn))
+        return set_err(OTC_ERR_ARG, "rc4_crypt_batch: states overlap the input or output");
     hipError_t e = otc_impl::k_rc4_states(states, nstreams, len, in, out, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "rc4_crypt_batch launch");
     return OTC_OK;
@@ -632,6 +640,23 @@ extern "C" int otc_device_sync(void)
 {
     HIPCHK(hipDeviceSynchronize());
     return OTC_OK;
+}
+
+/* Streams for C harnesses (hipStreamCreate: ordered with the legacy default
+ * stream, so hipEvents recorded on the default stream bracket work on them) */
+extern "C" void *otc_stream_create(void)
+{
+    hipStream_t s = nullptr;
+    hipError_t e = hipStreamCreate(&s);
+    if (e != hipSuccess) {
+        hip_fail(e, "hipStreamCreate");
+        return nullptr;
+    }
+    return (void *)s;
+}
+extern "C" void otc_stream_destroy(void *s)
+{
+    if (s) (void)hipStreamDestroy((hipStream_t)s);
 }
 
 /* ---- device memory helpers --------------------------------------------- */

@@ -230,6 +230,10 @@ int otc_device_cus(int dev);           /* compute units */
 int otc_device_clock_khz(int dev);     /* peak shader clock */
 int otc_set_device(int dev);
 int otc_device_sync(void);
+/* A HIP stream for C callers (ordered with the default stream, so events on
+ * the default stream bracket work queued on it); NULL on failure. */
+void *otc_stream_create(void);
+void otc_stream_destroy(void *stream);
 
 /* ---- L3 engine: host-memory streaming pipeline -----------------------------
  * Encrypt/decrypt a HOST buffer through one GPU with a pinned staging ring:

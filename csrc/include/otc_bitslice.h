@@ -123,6 +123,7 @@ OTC_HD void pin_n(W *x, int n)
  * compiler can emit for them is lgkmcnt(0) -- placed at their first use inside
  * the S-box it would also wait for the prefetch just issued.  An empty asm
  * reading the terms puts that wait here. */
+/* lists t[0..10]: OTC_SBOX_KEY_TERMS (otc_sbox_lut3.h) is pinned to 11 below */
 OTC_HD void kt_ready(const W *t)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -315,6 +316,7 @@ OTC_HD void mix_columns_ark(const W *in, W *out, KF kf)
 
 } /* namespace otc_bs */
 #include "otc_sbox_lut3.h"
+static_assert(OTC_SBOX_KEY_TERMS == 11, "kt_ready lists t[0..10]: update its operand list with the S-box header");
 #include "otc_mixcol.h"
 namespace otc_bs {
 

@@ -82,6 +82,8 @@ def rc4_crypt_batch(states: torch.Tensor, x: torch.Tensor, out: torch.Tensor | N
     _check_dev(out, "out")
     if _nbytes(out) != _nbytes(x):
         raise ValueError("out must have the byte size of x")
+    if not (states.device == x.device == out.device):
+        raise ValueError(f"states, x and out must be on one device (got {states.device}, {x.device}, {out.device})")
     with torch.cuda.device(x.device):
         rc = _native.require_gpu_lib().otc_rc4_crypt_batch(states.data_ptr(), ns, length, x.data_ptr(),
                                                            out.data_ptr(), _stream(x))

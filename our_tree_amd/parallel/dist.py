@@ -317,6 +317,19 @@ def scatter_ctr(full: torch.Tensor | None, nbytes: int, key: bytes, counter: byt
     return scatter_apply_gather(full, nbytes, fn, root=root, chunk_per_rank=chunk_per_rank, overlap=overlap)
 
 
+def gather_floats(values: list[float]) -> list[list[float]]:
+    """Every rank's short float list, on every rank (rank order); ``nan``
+    stands for "not measured".  One all_gather of a float64 tensor."""
+    if not _pg_on():
+        return [list(map(float, values))]
+    on_gpu = torch.cuda.is_available() and dist.get_backend() == "nccl"
+    device = torch.device("cuda", torch.cuda.current_device()) if on_gpu else "cpu"
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    outs = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(outs, t)
+    return [o.cpu().tolist() for o in outs]
+
+
 def allreduce_max(value: float, device=None) -> float:
     if not _pg_on():
         return value

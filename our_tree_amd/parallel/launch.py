@@ -29,6 +29,7 @@ import signal
 import socket
 import subprocess
 import sys
+import threading
 import time
 from dataclasses import dataclass
 
@@ -116,22 +117,40 @@ def spawn(nprocs: int, argv: list[str], timeout_s: float | None = None, grace_s:
     ``timeout_s`` the children are terminated the same way (exit code 124)."""
     port = free_port()
     me = os.getpid()
-    procs = [subprocess.Popen(argv, env=child_env(r, nprocs, port), preexec_fn=lambda: _child_setup(me))
-             for r in range(nprocs)]
+    procs: list = []
     got = []
+
+    def _fg_group() -> bool:
+        """the launcher's process group owns the terminal: a terminal ^C
+        already reached every child (they share the group)"""
+        try:
+            return os.tcgetpgrp(sys.stdin.fileno()) == os.getpgrp()
+        except (OSError, ValueError, AttributeError):
+            return False
 
     def on_signal(signum, frame):
         got.append(signum)
+        if signum == signal.SIGINT and _fg_group():
+            return  # a second SIGINT would cut the ranks' own cleanup short
         for p in procs:
             if p.poll() is None:
                 p.send_signal(signum)
 
     handled = (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)
-    old = {s: signal.signal(s, on_signal) for s in handled}
+    old = {}
     t0 = time.monotonic()
     rc = 0
     stop_at = None  # monotonic deadline for SIGKILL after a terminate
     try:
+        # handlers first (inside the try: whatever fails, the finally below
+        # stops every child that was started); signal.signal works on the
+        # main thread only -- elsewhere the children rely on the finally and
+        # their parent-death signal
+        if threading.current_thread() is threading.main_thread():
+            old = {s_: signal.signal(s_, on_signal) for s_ in handled}
+        for r in range(nprocs):
+            procs.append(subprocess.Popen(argv, env=child_env(r, nprocs, port),
+                                          preexec_fn=lambda: _child_setup(me)))
         live = set(range(nprocs))
         while live:
             for r in sorted(live):
@@ -163,8 +182,8 @@ def spawn(nprocs: int, argv: list[str], timeout_s: float | None = None, grace_s:
             if p.poll() is None:
                 p.kill()
                 p.wait()
-        for s, h in old.items():
-            signal.signal(s, h)
+        for s_, h in old.items():
+            signal.signal(s_, h)
     if got and rc == 0:
         rc = 128 + int(got[0])
     return rc

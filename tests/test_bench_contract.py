@@ -39,13 +39,85 @@ def test_baseline_ratios_are_labelled():
     assert r["vs_baseline_aes128_equiv"] == pytest.approx(1519.0 / (0.519 * 1.4), rel=1e-3)
 
 
+def _cpu_bench(*extra, timeout=300):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gib", "0.0005",
+                           "--steps", "2", "--warmup", "1", "--scatter-rounds", "2", *extra],
+                          capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_bench_cpu_rehearsal_per_rank(n):
+    """The whole multi-rank flow on the host (self-spawned ranks, gloo, C
+    oracle): one JSON line with a per-rank row for every rank, the preflight
+    verdict and the node energy keys (None off the GPU)."""
+    r = _cpu_bench("--gpus", str(n))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.splitlines()
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in REQUIRED:
+        assert k in d, k
+    assert d["n_gpus"] == n and d["config"]["parallelism"] == f"dp{n}" and d["config"]["device"] == "cpu"
+    pr = d["per_rank"]
+    assert [x["rank"] for x in pr] == list(range(n))
+    for x in pr:
+        assert set(bench_keys()) <= set(x)
+        assert x["verified"] is True and x["gbps"] > 0
+    assert d["verified_sample"] is True
+    assert d["per_rank_gbps_min"] == min(x["gbps"] for x in pr)
+    assert d["preflight"]["ok"] is True and d["preflight"]["backend"] == "gloo"
+    assert "joules_per_gb" in d and "ppt_residency_max" in d and "avg_socket_w_per_gpu" in d
+    assert d["rccl_ranks"] == n and d["rccl_ranks_verified"] == n
+
+
+def bench_keys():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    return bench.RANK_KEYS
+
+
+def test_bench_cpu_preflight_fault_rank5():
+    r = _cpu_bench("--gpus", "8", "--preflight-fault-rank", "5")
+    assert r.returncode != 0
+    d = json.loads(r.stdout.splitlines()[0])
+    assert d["error"] == "preflight verification failed"
+    assert d["preflight"]["per_rank_ok"] == [g != 5 for g in range(8)]
+
+
+def test_bench_cpu_preflight_hang_is_bounded():
+    r = _cpu_bench("--gpus", "4", "--preflight-hang-rank", "2", "--preflight-timeout", "5", timeout=120)
+    assert r.returncode == 3
+    d = json.loads(r.stdout.splitlines()[0])
+    assert "did not finish within 5 s" in d["error"]
+
+
+def test_node_energy_and_table():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    nan = float("nan")
+    rows = [[100.0, 1.9, 1.0, 50.0, 1300.0, 0.5, 0.9, 1800.0, 10.0, 20.0],
+            [90.0, nan, 1.0, 60.0, 1350.0, 0.6, 0.95, 1790.0, nan, nan]]
+    t = bench.per_rank_table(rows)
+    assert t[0]["verified"] is True and t[1]["held_clock_ghz"] is None and t[1]["xgmi_read_kb"] is None
+    e = bench.node_energy(t, total_bytes=200 * 10**9)
+    assert e["joules_per_gb"] == pytest.approx(110.0 / 200.0)
+    assert e["avg_socket_w_per_gpu"] == pytest.approx(1325.0) and e["ppt_residency_max"] == 0.95
+    t[1]["joules"] = None
+    assert bench.node_energy(t, 1)["joules_per_gb"] is None  # one rank unmeasured: no whole-node J/GB
+
+
 @pytest.mark.gpu
 def test_bench_json_line(gpu):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--gib", "0.25", "--no-clock", "--no-aes256", "--no-other-impl",
+                        "--gib", "0.25", "--no-clock",
                         "--scatter-mib", "64", "--scatter-rounds", "2", "--stream-gib", "0.25",
                         "--stream-passes", "2"],
                        capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
@@ -62,6 +134,7 @@ def test_bench_json_line(gpu):
     assert d["config"]["model"] == "AES-128-CTR" and d["config"]["parallelism"] == "dp1"
     assert d["verified_sample"] is True
     assert d["config"]["impl_resolved"] == "ttable"  # 0.25 GiB: below the bitsliced threshold
+    assert d["bitsliced_ctr_verified"] is True and d["aes256_ctr_verified"] is True  # the extras, checked
     nbytes = d["config"]["per_gpu_bytes"]
     assert nbytes == int(0.25 * (1 << 30))
     # value (GB/s) and ms_per_step describe the same timed region
@@ -78,3 +151,15 @@ def test_bench_json_line(gpu):
     assert d["stream_ctr_bytes_per_rank"] == 2 * int(0.25 * (1 << 30))
     pr = d["stream_ctr_per_rank"]
     assert len(pr) == 1 and pr[0]["rank"] == 0 and pr[0]["h2d_gbps"] > 0 and pr[0]["d2h_gbps"] > 0
+    # per-rank table: this rank's own rate, clock, verification and energy
+    assert [x["rank"] for x in d["per_rank"]] == [0]
+    x = d["per_rank"][0]
+    assert x["verified"] is True and x["gbps"] > 100
+    assert x["joules"] is not None and x["joules"] > 0, d.get("energy_unavailable")
+    assert 100 < x["avg_socket_w"] < 2000 and 0.0 <= x["ppt_residency"] <= 1.0
+    assert d["joules_per_gb"] == pytest.approx(x["joules"] / (3 * nbytes / 1e9), rel=1e-3)
+    assert d["preflight"]["ok"] is True and d["preflight"]["backend"] == "nccl"
+    # the reference's own GPU methodology beside pinned and kernel-only, verified
+    assert d["refmethod_verified"] is True
+    assert d["refmethod_ecb256_1000mib_gbps"] > 2.41
+    assert d["kernel_only_ecb256_1000mib_gbps"] > d["pinned_e2e_ecb256_1000mib_gbps"] > 0

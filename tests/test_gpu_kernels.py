@@ -403,9 +403,9 @@ def test_aesni_shaped_device_api(gpu, bits):
 
 @pytest.mark.parametrize("bits", [128, 256])
 def test_bitslice_launch_structures(gpu, bits):
-    """Both launch structures of the bitsliced kernels: CTR runs one launch
-    with range checks, ECB a bulk launch compiled for full tasks plus a
-    one-workgroup launch for a partial first / last task -- on shapes with a
+    """The split launch of the bitsliced kernels: both CTR and ECB run a bulk
+    launch compiled for full tasks plus a one-workgroup edge launch for a
+    partial first / last task -- on shapes with a
     partial first task, a partial last task, both, a single partial task and
     none, out of place and in place (a task run by both launches would be
     XORed twice)."""

@@ -68,6 +68,11 @@ def main(argv=None):
     valu = vals.get("SQ_INSTS_VALU", vals.get("SQ_ACTIVE_INST_VALU"))
     if valu and cyc:
         print(f"  VALU wave-instr / clk / CU  {valu / a.cus / cyc:.3f}  (peak 2)")
+    lds = vals.get("SQ_LDS_IDX_ACTIVE")
+    if lds and cyc:
+        print(f"  LDS busy (IDX_ACTIVE/CU/clk) {lds / a.cus / cyc:.3f}")
+        if vals.get("SQ_INSTS_LDS"):
+            print(f"  LDS cycles per LDS instr    {lds / vals['SQ_INSTS_LDS']:.3f}  (2.0 = conflict-free b32)")
     waves = vals.get("SQ_WAVES")
     if waves:
         for k in sorted(vals):

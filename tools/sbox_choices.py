@@ -35,6 +35,9 @@ variables, 10552 rows) stopped at its 90-minute limit with a 79-LUT
 incumbent: the big-M rows leave HiGHS a weak relaxation.
 
     tools/sbox_choices.py --order-seed 5   # ~10 min (ILP), rewrites the header body
+    tools/sbox_schedule.py                 # statement order
+    tools/sbox_cover.py extract > tools/sbox77_cover.json   # record it: the test
+                                           # suite pins the header to this record
 """
 import itertools, os, random, sys, time
 import numpy as np
