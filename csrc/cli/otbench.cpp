@@ -3,7 +3,8 @@
  * gfx950 kernels (the profiling target for rocprofv3).  Prints one JSON line
  * per configuration.
  *
- *   otbench --mode ctr|ecb|ecb-dec|cbc-dec|cbc-enc-seg|cfb-enc-seg|cfb-dec-seg|cfb-dec|ctr-stream|xor|rc4|ecb-split
+ *   otbench --mode ctr|ecb|ecb-dec|cbc-dec|cbc-enc-seg|cfb-enc-seg|cfb-dec-seg|cfb-dec|ctr-stream|xor|rc4
+ *                  |ecb-split|ecbdec-split|cbcdec-split
  *           [--bits 128] [--bytes 1G] [--iters 20] [--warmup 3]
  *           [--impl auto|ttable|bitslice] [--inplace] [--verify] [--clock]
  *           [--mark]                        "OTB_MARK start|end" on stderr around the timed loop
@@ -12,9 +13,10 @@
  *           [--e2e --chunk 256M]            host-resident, pinned pipeline
  *           [--gpus N --strategy direct|rccl] single-process multi-GPU (e2e)
  *           [--seg 4096]                    CBC segment size
- *           [--share 0.2]                   ecb-split: the bitsliced kernel's share of the
+ *           [--share 0.2]                   *-split: the bitsliced kernel's share of the
  *                                           blocks, run CONCURRENTLY with the T-table kernel
- *                                           on the rest (two streams, co-resident per CU)
+ *                                           on the rest (two streams, co-resident per CU) --
+ *                                           the library's impl "split" with an explicit share
  *           [--streams 65536 --len 4096 --keylen 16 --drop 0]    RC4 many-stream shape
  *
  * Kernel-only numbers come from hipEvents around `iters` back-to-back launches
@@ -78,8 +80,17 @@ struct OpArg {
     otc_aes_key *k;
     uint8_t iv[16];
     uint8_t *keys;
-    void *sa, *sb; /* ecb-split: T-table / bitsliced streams */
+    void *sa, *sb; /* *-split: T-table / bitsliced streams */
+    uint8_t prev[16]; /* cbcdec-split: ciphertext block before the bitsliced part */
 };
+
+/* *-split: T-table bytes (the bitsliced part is whole 2048-block tasks, as
+ * the library's split) */
+static size_t split_nt(const Cfg &c)
+{
+    const size_t nb = (size_t)((double)(c.bytes / 16) * c.share) / 2048 * 2048;
+    return c.bytes - 16 * std::min(nb, c.bytes / 16);
+}
 
 static int run_op(void *p)
 {
@@ -87,12 +98,20 @@ static int run_op(void *p)
     const Cfg &c = *a->c;
     if (c.mode == "ctr") return otc_aes_ctr(a->in, a->out, c.bytes, a->k, a->iv, 0, c.impl, nullptr);
     if (c.mode == "ecb" || c.mode == "ecb-dec") return otc_aes_ecb(a->in, a->out, c.bytes, a->k, c.impl, nullptr);
-    if (c.mode == "ecb-split") { /* both streams are ordered with the default stream (otc_stream_create) */
-        const size_t nb = (size_t)(c.bytes / 16 * c.share) * 16, nt = c.bytes - nb;
+    if (c.mode == "ecb-split" || c.mode == "ecbdec-split" || c.mode == "cbcdec-split") {
+        /* both streams are ordered with the default stream (otc_stream_create) */
+        const size_t nt = split_nt(c);
+        const uint8_t *bi = (const uint8_t *)a->in + nt;
+        uint8_t *bo = (uint8_t *)a->out + nt;
+        if (c.mode == "cbcdec-split") {
+            if (int r = otc_aes_cbc_decrypt_impl(a->in, a->out, nt, a->k, a->iv, OTC_IMPL_TTABLE, a->sa)) return r;
+            return otc_aes_cbc_decrypt_impl(bi, bo, c.bytes - nt, a->k, a->prev, OTC_IMPL_BITSLICE, a->sb);
+        }
         if (int r = otc_aes_ecb(a->in, a->out, nt, a->k, OTC_IMPL_TTABLE, a->sa)) return r;
-        return otc_aes_ecb((const uint8_t *)a->in + nt, (uint8_t *)a->out + nt, nb, a->k, OTC_IMPL_BITSLICE, a->sb);
+        return otc_aes_ecb(bi, bo, c.bytes - nt, a->k, OTC_IMPL_BITSLICE, a->sb);
     }
-    if (c.mode == "cbc-dec") return otc_aes_cbc_decrypt(a->in, a->out, c.bytes, a->k, a->iv, nullptr);
+    if (c.mode == "cbc-dec")
+        return otc_aes_cbc_decrypt_impl(a->in, a->out, c.bytes, a->k, a->iv, c.impl, nullptr);
     if (c.mode == "cbc-enc-seg")
         return otc_aes_cbc_encrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
     if (c.mode == "ctr-stream") { /* resumed mid-block: 1-byte head, then a body misaligned by 1 */
@@ -124,7 +143,7 @@ struct Sample {
 };
 
 static bool is_seg_mode(const std::string &m) { return m == "cbc-enc-seg" || m == "cfb-enc-seg" || m == "cfb-dec-seg"; }
-static bool chained_dec(const std::string &m) { return m == "cbc-dec" || m == "cfb-dec"; }
+static bool chained_dec(const std::string &m) { return m == "cbc-dec" || m == "cfb-dec" || m == "cbcdec-split"; }
 
 /* sample output ranges: head, middle, tail, and the 2^32-byte boundary (32-bit
  * byte-offset overflow) when the buffer is larger than 4 GiB */
@@ -211,13 +230,13 @@ static bool oracle(const Cfg &c, const uint8_t key[32], const uint8_t iv0[16], c
     } else if (m == "ecb" || m == "ecb-split") {
         aes_setkey_enc(&ctx, key, c.bits);
         aes_ecb_bulk(&ctx, AES_ENCRYPT, in, ref.data(), s.len, 8);
-    } else if (m == "ecb-dec") {
+    } else if (m == "ecb-dec" || m == "ecbdec-split") {
         aes_setkey_dec(&ctx, key, c.bits);
         aes_ecb_bulk(&ctx, AES_DECRYPT, in, ref.data(), s.len, 8);
-    } else if (m == "cbc-dec" || m == "cfb-dec") {
+    } else if (m == "cbc-dec" || m == "cfb-dec" || m == "cbcdec-split") {
         uint8_t iv[16];
         memcpy(iv, s.off ? s.in.data() : iv0, 16);
-        if (m == "cbc-dec") {
+        if (m != "cfb-dec") {
             aes_setkey_dec(&ctx, key, c.bits);
             aes_crypt_cbc(&ctx, AES_DECRYPT, s.len, iv, in, ref.data());
         } else {
@@ -289,6 +308,14 @@ static int corrupt(void *out, size_t off, bool device)
     return 0;
 }
 
+/* --mark lines, flushed at once: on the GPU box the runtime leaves stderr
+ * buffered, and a mark that arrives late shrinks the power window */
+static void mark(const char *what)
+{
+    fprintf(stderr, "OTB_MARK %s\n", what);
+    fflush(stderr);
+}
+
 static const char *verdict(bool asked, int v) { return !asked ? "null" : v == 1 ? "true" : "false"; }
 
 int main(int argc, char **argv)
@@ -326,7 +353,7 @@ int main(int argc, char **argv)
         }
     }
     static const char *modes[] = {"ctr", "ecb", "ecb-dec", "cbc-dec", "cbc-enc-seg", "cfb-enc-seg", "cfb-dec-seg",
-                                  "cfb-dec", "ctr-stream", "xor", "rc4", "ecb-split"};
+                                  "cfb-dec", "ctr-stream", "xor", "rc4", "ecb-split", "ecbdec-split", "cbcdec-split"};
     bool known = false;
     for (const char *m : modes) known |= c.mode == m;
     if (!known) {
@@ -359,7 +386,8 @@ int main(int argc, char **argv)
     uint8_t key[32];
     srand(1337);
     for (int i = 0; i < 32; ++i) key[i] = (uint8_t)rand();
-    const bool dec = (c.mode == "ecb-dec" || c.mode == "cbc-dec");
+    const bool dec = (c.mode == "ecb-dec" || c.mode == "cbc-dec" || c.mode == "ecbdec-split" ||
+                      c.mode == "cbcdec-split");
     otc_aes_key k;
     if (otc_aes_key_init(&k, key, c.bits, dec ? OTC_DIR_DECRYPT : OTC_DIR_ENCRYPT)) {
         fprintf(stderr, "key: %s\n", otc_last_error());
@@ -391,7 +419,7 @@ int main(int argc, char **argv)
         otc_engine *eng = (c.gpus > 1 || c.strategy == 1) ? nullptr : otc_engine_create(0, c.chunk, 3);
         int v = -1;
         for (int w = 0; w <= c.warmup; ++w) {
-            if (c.mark && w == c.warmup) fprintf(stderr, "OTB_MARK start\n");
+            if (c.mark && w == c.warmup) mark("start");
             auto t0 = std::chrono::steady_clock::now();
             int r;
             if (c.gpus > 1 || c.strategy == 1) {
@@ -401,7 +429,7 @@ int main(int argc, char **argv)
                 r = eng ? otc_engine_run(eng, mode, hin, hout, c.bytes, &k, a.iv, 0, c.impl, nullptr) : OTC_ERR_NOMEM;
             }
             auto t1 = std::chrono::steady_clock::now();
-            if (c.mark && w == c.warmup) fprintf(stderr, "OTB_MARK end\n");
+            if (c.mark && w == c.warmup) mark("end");
             if (r) {
                 fprintf(stderr, "run: %s\n", otc_last_error());
                 return 1;
@@ -422,7 +450,7 @@ int main(int argc, char **argv)
         return (c.verify && v != 1) ? 3 : 0;
     }
 
-    if (c.mode == "ecb-split") {
+    if (c.mode == "ecb-split" || c.mode == "ecbdec-split" || c.mode == "cbcdec-split") {
         if (!(c.share >= 0.0 && c.share <= 1.0)) {
             fprintf(stderr, "--share must be in [0, 1]\n");
             return 2;
@@ -447,6 +475,14 @@ int main(int argc, char **argv)
         otc_fill_random(a.keys, c.streams * c.keylen, 44, nullptr);
     }
     otc_device_sync();
+    if (c.mode == "cbcdec-split") { /* the bitsliced part's IV: ciphertext block nt/16 - 1 (constant: out of place) */
+        const size_t nt = split_nt(c);
+        if (nt >= 16) {
+            if (otc_memcpy(a.prev, (const uint8_t *)a.in + nt - 16, 16, OTC_D2H)) return 1;
+        } else {
+            memcpy(a.prev, a.iv, 16);
+        }
+    }
     int v = -1;
     if (c.verify) {
         /* the inputs of the samples are copied BEFORE the op: valid in place */
@@ -469,13 +505,13 @@ int main(int argc, char **argv)
         }
     if (c.mark) {
         otc_device_sync();
-        fprintf(stderr, "OTB_MARK start\n");
+        mark("start");
     }
     if (otc_time_op(run_op, &a, c.iters, &ms)) {
         fprintf(stderr, "timing: %s\n", otc_last_error());
         return 1;
     }
-    if (c.mark) fprintf(stderr, "OTB_MARK end\n");
+    if (c.mark) mark("end");
     const double gbps = c.bytes / (ms * 1e6);
     const double cpb = (ms * 1e-3) * clk_hz * cus / (double)c.bytes;
     double held = 0.0;
@@ -487,7 +523,7 @@ int main(int argc, char **argv)
     if (c.clock)
         snprintf(clk, sizeof clk, "\"held_clock_ghz\": %.3f, \"cycles_per_byte_per_cu_held\": %.3f, ", held,
                  (ms * 1e-3) * held * 1e9 * cus / (double)c.bytes);
-    if (c.mode == "ecb-split")
+    if (c.mode.size() > 6 && c.mode.compare(c.mode.size() - 6, 6, "-split") == 0)
         snprintf(clk + strlen(clk), sizeof clk - strlen(clk), "\"share\": %.3f, ", c.share);
     printf("{\"mode\": \"%s\", \"bits\": %d, \"bytes\": %zu, \"impl\": \"%s\", \"inplace\": %s, \"iters\": %d, "
            "\"ms\": %.4f, \"gbps\": %.2f, \"cycles_per_byte_per_cu\": %.3f, \"cus\": %d, \"clock_mhz\": %.0f, %s"

@@ -103,6 +103,12 @@ int otc_aes_ctr_stream(otc_aes_ctr_ctx *ctx, const otc_aes_key *k, size_t n, con
     return OTC_OK;
 }
 
+int otc_aes_cbc_decrypt(const void *in, void *out, size_t n, const otc_aes_key *k, const uint8_t iv[16], void *);
+int otc_aes_cbc_decrypt_impl(const void *in, void *out, size_t n, const otc_aes_key *k, const uint8_t iv[16], int,
+                             void *st)
+{
+    return otc_aes_cbc_decrypt(in, out, n, k, iv, st);
+}
 int otc_aes_cbc_decrypt(const void *in, void *out, size_t n, const otc_aes_key *k, const uint8_t iv[16], void *)
 {
     if (in == out) return fail(OTC_ERR_ARG, "cbc decrypt in place");

@@ -73,6 +73,9 @@ struct BsParams {
     const uint32_t *e1tab; /* CTR counter caching: E1 plane words per task */
     uint64_t tasks;       /* 2048-block tasks of the call */
     uint32_t part;        /* BS_FULL_ONLY or BS_EDGE_ONLY */
+    uint32_t has_prev;    /* CBC decrypt: the 16 bytes before `in` are block 0's predecessor (a split's
+                             second part); otherwise block 0 XORs with iv */
+    uint32_t iv[4];       /* CBC decrypt: IV as LE words */
 };
 
 /* Which tasks a launch runs.  The bulk launch (BS_FULL_ONLY) takes only tasks
@@ -83,7 +86,9 @@ struct BsParams {
  * runs the first and the last task (wave 0 / wave 1) if they are partial. */
 enum : uint32_t { BS_FULL_ONLY = 1, BS_EDGE_ONLY = 2 };
 
-enum : int { BS_CTR = 0, BS_ECB = 1 };
+/* BS_ECB: ECB encryption; BS_ECB_DEC / BS_CBC_DEC: the inverse cipher through
+ * the forward S-box (S^-1 = L S L, otc_invmix.h) with a decryption key */
+enum : int { BS_CTR = 0, BS_ECB = 1, BS_ECB_DEC = 2, BS_CBC_DEC = 3 };
 
 __device__ __forceinline__ W lane_mask(uint32_t lane, int n) { return (W)(0u - ((lane >> n) & 1u)); }
 
@@ -146,12 +151,14 @@ __device__ __forceinline__ void ecb_load_planes(const BsParams &P, const Task &t
 /* Key-term table of the schedule (otc_bs::key_term_table on the device):
  * one thread per (round, byte); written once per call into a stream-ordered
  * buffer, then read by every wave with scalar loads. */
+template <bool DEC>
 __global__ __launch_bounds__(256) void k_bs_key_table(otc_aes_key K, uint32_t *tab)
 {
     const int e = (int)threadIdx.x; /* r * 16 + b */
     if (e >= K.nr * 16) return;
     const int r = e >> 4, b = e & 15;
-    const uint32_t byte = (K.rk[4 * r + (b >> 2)] >> (8 * (b & 3))) & 0xFFu;
+    uint32_t byte = (K.rk[4 * r + (b >> 2)] >> (8 * (b & 3))) & 0xFFu;
+    if (DEC) byte = dec_round_key_byte(byte, r); /* S-box input key of S^-1 = L S L */
     W k[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) k[i] = ((byte >> i) & 1u) ? ~0u : 0u;
@@ -245,15 +252,15 @@ __global__ __launch_bounds__(256) void k_bs_ctr_table(otc_aes_key K, Ctr128 cbas
     }
 }
 
-template <int R, int NR, int MIX>
+template <int R, int NR, int MIX, bool DEC = false>
 __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
 {
     if constexpr (R < NR - 1) {
-        round_step_kt<MIX, TableTerms<R>, 2>(s, TableTerms<R>{tp});
+        round_step_kt<MIX, TableTerms<R>, 2, DEC>(s, TableTerms<R>{tp});
         pin_n(s, 128);
-        rounds_table<R + 1, NR, MIX>(s, tp);
+        rounds_table<R + 1, NR, MIX, DEC>(s, tp);
     } else {
-        round_final_kt(s, TableTerms<NR - 1>{tp});
+        round_final_kt<TableTerms<NR - 1>, DEC>(s, TableTerms<NR - 1>{tp});
     }
 }
 
@@ -358,9 +365,14 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
     } else {
         ecb_load_planes(P, t, s, full);
     }
+    constexpr bool DEC = MODE == BS_ECB_DEC || MODE == BS_CBC_DEC;
+    if (DEC) {
+        dec_premap(s); /* L on every ciphertext byte */
+        pin_n(s, 128);
+    }
     if (!(MODE == BS_CTR && CACHE)) {
         sched_fence();
-        rounds_table<0, NR, MIX>(s, (ktab_ptr)P.ktab);
+        rounds_table<0, NR, MIX, DEC>(s, (ktab_ptr)P.ktab);
     }
     pin_n(s, 128);
     sched_fence();
@@ -379,13 +391,24 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
     /* register-loaded plaintext (slots LS..31); none is issued behind a
      * store -- vmcnt is in order on gfx9, so such a load would also wait for
      * the stores */
+    /* the block XORed into the output: CTR the plaintext, CBC decrypt the
+     * previous ciphertext block (the IV for block 0 of a whole-stream call) */
+    constexpr bool XIN = MODE == BS_CTR || MODE == BS_CBC_DEC;
+    constexpr int XOFF = MODE == BS_CBC_DEC ? -16 : 0;
     uint4 pt[32];
     auto issue = [&](int j) {
-        if (MODE == BS_CTR && j >= LS && j < 32)
-            pt[j] = slot_ok(j) ? *(const uint4 *)(ib + lo + 1024u * j) : make_uint4(0, 0, 0, 0);
+        if (XIN && j >= LS && j < 32) {
+            if (MODE == BS_CBC_DEC && !P.has_prev && tstart + lane + 64 * j == 0)
+                pt[j] = make_uint4(P.iv[0], P.iv[1], P.iv[2], P.iv[3]);
+            else
+                pt[j] = slot_ok(j) ? *(const uint4 *)(ib + lo + 1024u * j + XOFF) : make_uint4(0, 0, 0, 0);
+        }
     };
+    /* CBC decrypt: its 125-node linear layer leaves fewer registers for the
+     * output phase -- previous-block loads 4 slots ahead, none early */
+    constexpr int PRE_ = MODE == BS_CBC_DEC ? 0 : PRE, D_ = MODE == BS_CBC_DEC ? 4 : D;
 #pragma unroll
-    for (int j = 0; j < LS + PRE; ++j) issue(j);
+    for (int j = 0; j < LS + PRE_; ++j) issue(j);
     sched_fence();
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -393,7 +416,10 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
         pin_n(s + 32 * w, 32);
         sched_fence();
     }
-    const uint32_t k0 = K.rk[4 * NR + 0], k1 = K.rk[4 * NR + 1], k2 = K.rk[4 * NR + 2], k3 = K.rk[4 * NR + 3];
+    /* last round key; decryption adds the 0x05 the post-map L leaves */
+    constexpr uint32_t KD = DEC ? 0x05050505u : 0u;
+    const uint32_t k0 = K.rk[4 * NR + 0] ^ KD, k1 = K.rk[4 * NR + 1] ^ KD, k2 = K.rk[4 * NR + 2] ^ KD,
+                   k3 = K.rk[4 * NR + 3] ^ KD;
     auto ks_xor = [&](int k, uint4 x) {
         uint4 o;
         o.x = x3(x.x, s[k], k0);
@@ -407,12 +433,12 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
         if ((k & 3) == 0) {
             sched_fence();
 #pragma unroll
-            for (int j = LS + PRE; j < 32; ++j)
-                if ((j - D < 0 ? 0 : ((j - D) & ~3)) == k) issue(j);
+            for (int j = LS + PRE_; j < 32; ++j)
+                if ((j - D_ < 0 ? 0 : ((j - D_) & ~3)) == k) issue(j);
         }
         if (slot_ok(k)) {
-            const uint4 o = MODE == BS_CTR ? ks_xor(k, k < LS ? stage[(wave * LS + k) * 64 + (lo >> 4)] : pt[k])
-                                           : make_uint4(s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3);
+            const uint4 o = XIN ? ks_xor(k, k < LS ? stage[(wave * LS + k) * 64 + (lo >> 4)] : pt[k])
+                                : make_uint4(s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3);
             *(uint4 *)(ob + lo + 1024u * k) = o;
         }
     }
@@ -466,7 +492,7 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     }
     if (!cache) e = alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&tab, kt_words * 4, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_bs_key_table, dim3(1), dim3(256), 0, st, K, tab);
+    hipLaunchKernelGGL(k_bs_key_table<MODE == BS_ECB_DEC || MODE == BS_CBC_DEC>, dim3(1), dim3(256), 0, st, K, tab);
     BsParams Q = P;
     Q.ktab = tab;
     Q.tasks = tasks;
@@ -563,6 +589,32 @@ hipError_t bs_ecb_encrypt(const void *in, void *out, uint64_t nblocks, const otc
     P.out = (uint8_t *)out;
     P.nblocks = nblocks;
     return launch<BS_ECB>(P, K, st);
+}
+
+/* K: the decryption (equivalent inverse cipher) schedule, as the T-table
+ * decrypt kernel takes it */
+hipError_t bs_ecb_decrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, hipStream_t st)
+{
+    BsParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nblocks = nblocks;
+    return launch<BS_ECB_DEC>(P, K, st);
+}
+
+/* CBC decryption: block i XORs with block i-1 of `in`; block 0 with iv_le
+ * (LE words), or -- has_prev -- with the 16 bytes before `in` (the second
+ * part of a split call).  in != out. */
+hipError_t bs_cbc_decrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, const uint32_t iv_le[4],
+                          bool has_prev, hipStream_t st)
+{
+    BsParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nblocks = nblocks;
+    P.has_prev = has_prev ? 1u : 0u;
+    for (int i = 0; i < 4; ++i) P.iv[i] = iv_le ? iv_le[i] : 0u;
+    return launch<BS_CBC_DEC>(P, K, st);
 }
 
 } // namespace otc_impl

@@ -52,6 +52,8 @@ hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, boo
 hipError_t tt_ctr_shift(const void *, void *, size_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t xor_small(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
 hipError_t bs_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
+hipError_t bs_ecb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
+hipError_t bs_cbc_decrypt(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, bool, hipStream_t);
 hipError_t tt_ctr_batch(const otc_ctr_msg *, const otc_aes_key *, const uint32_t *, const uint64_t *, uint64_t, int, int,
                         hipStream_t);
 hipError_t k_xor(const void *, const void *, void *, size_t, hipStream_t);
@@ -129,26 +131,35 @@ using namespace otc_rt;
 namespace {
 
 /* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  CTR calls of >= 2 GiB
- * (AES-256: >= 1 GiB) run bitsliced, the thresholds below.  Every other mode
- * (ECB encryption included: profiles/r3/ecb256/xover_ecb_s79.jsonl, T-table
- * ahead at 1-64 GiB) and smaller calls (the bitsliced grid needs ~768
- * workgroups to fill the chip, plus two table kernels per call) take the
- * T-table.  ctr_bytes = 0 for non-CTR calls.  OTC_IMPL=ttable|bitslice
- * overrides "auto" for the whole process. */
-int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
+ * (AES-256: >= 1 GiB) run bitsliced, the thresholds below; smaller CTR calls
+ * (the bitsliced grid needs ~768 workgroups to fill the chip, plus two table
+ * kernels per call) take the T-table.  ECB encryption: the co-resident split
+ * (ecb_split below) from ecb_split_min() bytes, the T-table below that.
+ * ctr_bytes = 0 for non-CTR calls.  OTC_IMPL=ttable|bitslice|split overrides
+ * "auto" for the whole process. */
+int env_impl()
 {
-    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE) return impl;
     static const int env = [] {
         const char *e = getenv("OTC_IMPL");
         if (!e || !*e || !strcmp(e, "auto")) return OTC_IMPL_AUTO;
         if (!strcmp(e, "ttable")) return OTC_IMPL_TTABLE;
         if (!strcmp(e, "bitslice")) return OTC_IMPL_BITSLICE;
+        if (!strcmp(e, "split")) return OTC_IMPL_SPLIT;
         /* an old or mistyped value (e.g. the removed "hybrid") must not
          * silently select a different kernel: say so once */
-        fprintf(stderr, "otc: ignoring OTC_IMPL=%s (expected auto, ttable or bitslice)\n", e);
+        fprintf(stderr, "otc: ignoring OTC_IMPL=%s (expected auto, ttable, bitslice or split)\n", e);
         return OTC_IMPL_AUTO;
     }();
-    if (env != OTC_IMPL_AUTO) return env;
+    return env;
+}
+
+int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
+{
+    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE) return impl;
+    /* impl == OTC_IMPL_SPLIT: CTR has no split form (the bitsliced CTR kernel
+     * alone holds the power cap), so it routes as auto */
+    const int env = env_impl();
+    if (env == OTC_IMPL_TTABLE || env == OTC_IMPL_BITSLICE) return env;
     /* measured crossover (profiles/r3/auto_impl/xover_after_round2_tables):
      * AES-128 2 GiB 1520 vs 1506 GB/s, 1 GiB 1353 vs 1360; AES-256 1 GiB
      * 1056 vs 1049.  AES-192 takes the AES-128 threshold (not measured at
@@ -159,8 +170,150 @@ int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
 
 int check_impl(int impl)
 {
-    if (impl == OTC_IMPL_AUTO || impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE) return OTC_OK;
-    return set_err(OTC_ERR_ARG, "impl must be OTC_IMPL_AUTO, OTC_IMPL_TTABLE or OTC_IMPL_BITSLICE");
+    if (impl == OTC_IMPL_AUTO || impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_SPLIT)
+        return OTC_OK;
+    return set_err(OTC_ERR_ARG, "impl must be OTC_IMPL_AUTO, OTC_IMPL_TTABLE, OTC_IMPL_BITSLICE or OTC_IMPL_SPLIT");
+}
+
+/* ---- ECB encryption: co-resident T-table + bitsliced split -----------------
+ * The T-table kernel is LDS-bound (80% of the LDS array's cycles, 224 lookups
+ * per AES-256 block, VALU 32% busy) and leaves power on the table: 1.27 kW
+ * with the package power limit active half the time, where the VALU-bound
+ * bitsliced kernels hold the ~1.38 kW cap (profiles/r4/power).  Its one
+ * 1024-thread workgroup per CU (4 waves x 56 VGPRs per SIMD, 128 KiB LDS)
+ * also leaves room in the register file: the bitsliced ECB kernel (0 LDS,
+ * 80 VGPRs, 3 waves per SIMD) fits beside it (7 waves, 464 of 512 VGPRs).
+ * So the last `share` of the blocks goes to the bitsliced kernel on an
+ * auxiliary stream, launched right after the T-table kernel on the caller's
+ * stream, and the two run concurrently on every CU -- LDS and VALU busy at
+ * once.  The caller's stream waits for both (fork / join events).  Measured
+ * AES-256 64 GiB: T-table 1040, bitsliced 1020, split 0.35 1154-1161 GB/s
+ * (profiles/r4/ecb_split). */
+struct AuxStream {
+    int dev = -1;
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+
+/* pooled per device: a call takes one (creating it on first use), enqueues,
+ * and returns it, so concurrent callers (one host thread per GPU in
+ * otc_multi_run) never share the events they order on */
+std::mutex g_aux_mu;
+std::vector<AuxStream> g_aux_free;
+
+hipError_t aux_take(int dev, AuxStream &out)
+{
+    {
+        std::lock_guard<std::mutex> lk(g_aux_mu);
+        for (size_t i = 0; i < g_aux_free.size(); ++i)
+            if (g_aux_free[i].dev == dev) {
+                out = g_aux_free[i];
+                g_aux_free.erase(g_aux_free.begin() + (long)i);
+                return hipSuccess;
+            }
+    }
+    AuxStream a;
+    a.dev = dev;
+    hipError_t e = hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&a.fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&a.join, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        if (a.join) (void)hipEventDestroy(a.join);
+        if (a.fork) (void)hipEventDestroy(a.fork);
+        if (a.s) (void)hipStreamDestroy(a.s);
+        return e;
+    }
+    out = a;
+    return hipSuccess;
+}
+
+void aux_give(const AuxStream &a)
+{
+    std::lock_guard<std::mutex> lk(g_aux_mu);
+    g_aux_free.push_back(a);
+}
+
+/* bitsliced share of the blocks and the smallest call that splits, per key
+ * size (profiles/r4/ecb_split: share sweeps at 1, 4 and 64 GiB) */
+double ecb_split_share(int bits) { return bits == 256 ? 0.25 : bits == 192 ? 0.25 : 0.2; }
+size_t ecb_split_min(int bits) { return bits == 256 ? ((size_t)1 << 30) : ((size_t)1 << 30); }
+/* decryption (ECB, CBC): the bitsliced inverse cipher costs ~1.17x the
+ * encryption's VALU work (L o InvMixColumns o L: 121 nodes per column vs
+ * MixColumns' 55), so it takes a smaller share */
+double dec_split_share(int bits) { return bits == 256 ? 0.2 : bits == 192 ? 0.2 : 0.2; }
+size_t dec_split_min(int) { return (size_t)1 << 30; }
+
+int pick_ecb_impl(int impl, int bits, size_t nbytes)
+{
+    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_SPLIT) return impl;
+    const int env = env_impl();
+    if (env != OTC_IMPL_AUTO) return env;
+    return nbytes >= ecb_split_min(bits) ? OTC_IMPL_SPLIT : OTC_IMPL_TTABLE;
+}
+
+int pick_dec_impl(int impl, int bits, size_t nbytes)
+{
+    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_SPLIT) return impl;
+    const int env = env_impl();
+    if (env != OTC_IMPL_AUTO) return env;
+    return nbytes >= dec_split_min(bits) ? OTC_IMPL_SPLIT : OTC_IMPL_TTABLE;
+}
+
+/* The split itself: tt(nt) launches the T-table kernel over the first nt
+ * blocks on st, bs(nt, nb, aux) the bitsliced kernel over the last nb on the
+ * auxiliary stream.  nb is whole 2048-block bitsliced tasks (no edge
+ * launch); a share that rounds to none runs the T-table alone.  *ran: the
+ * kernels actually used. */
+template <class TT, class BS>
+hipError_t split_run(uint64_t nblocks, double share, hipStream_t st, int *ran, TT tt, BS bs)
+{
+    const uint64_t nb = (uint64_t)((double)nblocks * share) / 2048u * 2048u;
+    if (nb == 0 || nb >= nblocks) {
+        *ran = OTC_IMPL_TTABLE;
+        return tt(nblocks);
+    }
+    const uint64_t nt = nblocks - nb;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    AuxStream a;
+    if ((e = aux_take(dev, a)) != hipSuccess) return e;
+    /* fork: the aux stream starts after everything already queued on st */
+    if ((e = hipEventRecord(a.fork, st)) == hipSuccess && (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess &&
+        (e = tt(nt)) == hipSuccess && (e = bs(nt, nb, a.s)) == hipSuccess && (e = hipEventRecord(a.join, a.s)) == hipSuccess)
+        e = hipStreamWaitEvent(st, a.join, 0); /* join: st continues after both */
+    aux_give(a); /* reusable as soon as the work is enqueued: stream order */
+    *ran = OTC_IMPL_SPLIT;
+    return e;
+}
+
+hipError_t ecb_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, hipStream_t st, int *ran)
+{
+    const uint8_t *pi = (const uint8_t *)in;
+    uint8_t *po = (uint8_t *)out;
+    if (K.dir == OTC_DIR_ENCRYPT)
+        return split_run(
+            nblocks, ecb_split_share(K.bits), st, ran,
+            [&](uint64_t nt) { return otc_impl::tt_ecb_encrypt(pi, po, nt, K, st); },
+            [&](uint64_t nt, uint64_t nb, hipStream_t s) { return otc_impl::bs_ecb_encrypt(pi + 16 * nt, po + 16 * nt, nb, K, s); });
+    return split_run(
+        nblocks, dec_split_share(K.bits), st, ran,
+        [&](uint64_t nt) { return otc_impl::tt_ecb_decrypt(pi, po, nt, K, st); },
+        [&](uint64_t nt, uint64_t nb, hipStream_t s) { return otc_impl::bs_ecb_decrypt(pi + 16 * nt, po + 16 * nt, nb, K, s); });
+}
+
+hipError_t cbc_dec_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, const uint8_t iv[16],
+                         hipStream_t st, int *ran)
+{
+    const uint8_t *pi = (const uint8_t *)in;
+    uint8_t *po = (uint8_t *)out;
+    return split_run(
+        nblocks, dec_split_share(K.bits), st, ran,
+        [&](uint64_t nt) { return otc_impl::tt_cbc_decrypt(pi, po, nt, K, ctr_from_bytes(iv), st); },
+        /* the bitsliced part's block 0 XORs with block nt-1 of the input */
+        [&](uint64_t nt, uint64_t nb, hipStream_t s) {
+            return otc_impl::bs_cbc_decrypt(pi + 16 * nt, po + 16 * nt, nb, K, nullptr, true, s);
+        });
 }
 
 /* the kernel family the calling thread's last AES call ran (otc_last_impl) */
@@ -211,10 +364,30 @@ extern "C" int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, in
     return OTC_OK;
 }
 
-extern "C" int otc_pick_impl(int impl, int bits, int mode_ctr, uint64_t nbytes)
+/* mode: 1 CTR, 0 ECB encryption, 2 decryption (ECB / CBC) */
+extern "C" int otc_pick_impl(int impl, int bits, int mode, uint64_t nbytes)
 {
     if (check_impl(impl)) return -1;
-    return pick_impl(impl, bits, mode_ctr ? (size_t)nbytes : 0);
+    if (mode == 0) return pick_ecb_impl(impl, bits, (size_t)nbytes);
+    if (mode == 2) return pick_dec_impl(impl, bits, (size_t)nbytes);
+    return pick_impl(impl, bits, (size_t)nbytes);
+}
+
+/* the auxiliary streams of the split (otc_release_resources) */
+void otc_rt::aux_release_all()
+{
+    std::lock_guard<std::mutex> lk(g_aux_mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (AuxStream &a : g_aux_free) {
+        (void)hipSetDevice(a.dev);
+        (void)hipStreamSynchronize(a.s);
+        (void)hipEventDestroy(a.fork);
+        (void)hipEventDestroy(a.join);
+        (void)hipStreamDestroy(a.s);
+    }
+    g_aux_free.clear();
+    (void)hipSetDevice(cur);
 }
 
 extern "C" int otc_last_impl(void) { return g_last_impl; }
@@ -232,12 +405,15 @@ extern "C" int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_a
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     if (k->dir == OTC_DIR_ENCRYPT) {
-        g_last_impl = pick_impl(impl, k->bits);
-        e = g_last_impl == OTC_IMPL_BITSLICE ? otc_impl::bs_ecb_encrypt(in, out, nbytes / 16, *k, st)
-                                             : otc_impl::tt_ecb_encrypt(in, out, nbytes / 16, *k, st);
+        g_last_impl = pick_ecb_impl(impl, k->bits, nbytes);
+        if (g_last_impl == OTC_IMPL_SPLIT) e = ecb_split(in, out, nbytes / 16, *k, st, &g_last_impl);
+        else if (g_last_impl == OTC_IMPL_BITSLICE) e = otc_impl::bs_ecb_encrypt(in, out, nbytes / 16, *k, st);
+        else e = otc_impl::tt_ecb_encrypt(in, out, nbytes / 16, *k, st);
     } else {
-        g_last_impl = OTC_IMPL_TTABLE;
-        e = otc_impl::tt_ecb_decrypt(in, out, nbytes / 16, *k, st);
+        g_last_impl = pick_dec_impl(impl, k->bits, nbytes);
+        if (g_last_impl == OTC_IMPL_SPLIT) e = ecb_split(in, out, nbytes / 16, *k, st, &g_last_impl);
+        else if (g_last_impl == OTC_IMPL_BITSLICE) e = otc_impl::bs_ecb_decrypt(in, out, nbytes / 16, *k, st);
+        else e = otc_impl::tt_ecb_decrypt(in, out, nbytes / 16, *k, st);
     }
     if (e != hipSuccess) return hip_fail(e, "aes_ecb launch");
     return OTC_OK;
@@ -387,8 +563,8 @@ extern "C" int otc_aes_ctr_batch(const otc_ctr_msg *msgs, const otc_aes_key *key
     return OTC_OK;
 }
 
-extern "C" int otc_aes_cbc_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
-                                   const uint8_t iv[16], void *stream)
+extern "C" int otc_aes_cbc_decrypt_impl(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                                        const uint8_t iv[16], int impl, void *stream)
 {
     Range rg("otc_aes_cbc_decrypt");
     int r = check_key(k, OTC_DIR_DECRYPT);
@@ -396,10 +572,30 @@ extern "C" int otc_aes_cbc_decrypt(const void *in, void *out, size_t nbytes, con
     if (nbytes % 16) return set_err(OTC_ERR_ARG, "CBC length must be a multiple of 16");
     if (!iv) return set_err(OTC_ERR_ARG, "null iv");
     if ((r = check_bufs(in, out, nbytes, nbytes <= 16, "aes_cbc_decrypt"))) return r;
+    if ((r = check_impl(impl))) return r;
     if (nbytes == 0) return OTC_OK;
-    hipError_t e = otc_impl::tt_cbc_decrypt(in, out, nbytes / 16, *k, ctr_from_bytes(iv), (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    g_last_impl = pick_dec_impl(impl, k->bits, nbytes);
+    if (g_last_impl == OTC_IMPL_SPLIT) {
+        e = cbc_dec_split(in, out, nbytes / 16, *k, iv, st, &g_last_impl);
+    } else if (g_last_impl == OTC_IMPL_BITSLICE) {
+        uint32_t w[4];
+        for (int j = 0; j < 4; ++j)
+            w[j] = (uint32_t)iv[4 * j] | (uint32_t)iv[4 * j + 1] << 8 | (uint32_t)iv[4 * j + 2] << 16 |
+                   (uint32_t)iv[4 * j + 3] << 24;
+        e = otc_impl::bs_cbc_decrypt(in, out, nbytes / 16, *k, w, false, st);
+    } else {
+        e = otc_impl::tt_cbc_decrypt(in, out, nbytes / 16, *k, ctr_from_bytes(iv), st);
+    }
     if (e != hipSuccess) return hip_fail(e, "cbc_decrypt launch");
     return OTC_OK;
+}
+
+extern "C" int otc_aes_cbc_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                                   const uint8_t iv[16], void *stream)
+{
+    return otc_aes_cbc_decrypt_impl(in, out, nbytes, k, iv, OTC_IMPL_AUTO, stream);
 }
 
 extern "C" int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,

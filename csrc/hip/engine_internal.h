@@ -26,6 +26,8 @@ int hip_fail(hipError_t e, const char *what);
 Ctr128 ctr_from_bytes(const uint8_t c[16]);
 Ctr128 ctr_add(Ctr128 c, uint64_t n, bool wrap64);
 int check_key(const otc_aes_key *k, int dir);
+/* destroy the pooled auxiliary streams of the ECB split (engine.cpp) */
+void aux_release_all();
 
 /* roctx range for rocprofv3 --marker-trace (a no-op unless a tool is
  * attached): every public entry point is one named range. */

@@ -355,16 +355,22 @@ extern "C" int otc_engine_run(otc_engine *e, int mode, const void *host_in, void
 /* ---- L4 multi-GPU (single process) -------------------------------------- */
 /* ---- RCCL root scatter / gather (otc_multi_run strategy 1) -----------------
  * Round r (buffer set b = r & 1):
- *   root:   H2D(r) -> root_in[b]                      stream h2d
+ *   root:   H2D(r) -> root_in[b]                      stream sc[0]
  *   all g:  ncclScatter(root_in[b] -> piece_in[b][g])  comm set SC, stream sc[g]
  *   all g:  cipher(piece_in[b][g] -> piece_out[b][g]) stream k[g]
  *   all g:  ncclGather(piece_out[b][g] -> root_out[b]) comm set GA, stream ga[g]
- *   root:   D2H(r) <- root_out[b]                     stream d2h
- * Buffer reuse two rounds later is ordered by events, so scatter(r+1),
- * cipher(r) and gather(r-1) run at the same time; scatter and gather are on
- * separate communicators because xGMI links are full duplex and one
- * communicator would serialise the two directions.  ncclScatter needs equal
- * counts, so the last round is zero padded.
+ *   root:   D2H(r) <- root_out[b]                     stream ga[0]
+ * Three streams per GPU, the root included: a process gets GPU_MAX_HW_QUEUES
+ * (4 here) hardware queues per device, and the root's copies on streams of
+ * their own (5 streams with the caller's) made two streams share a queue,
+ * which can serialise the phases below without a trace.  The root's H2D
+ * precedes its scatter and its D2H follows its gather in stream order anyway;
+ * only H2D(r+1) no longer overlaps scatter(r) (xGMI is ~20x PCIe: a few
+ * percent).  Buffer reuse two rounds later is ordered by events, so
+ * scatter(r+1), cipher(r) and gather(r-1) run at the same time; scatter and
+ * gather are on separate communicators because xGMI links are full duplex
+ * and one communicator would serialise the two directions.  ncclScatter needs
+ * equal counts, so the last round is zero padded.
  *
  * Failure detection: waits poll hipStreamQuery and ncclCommGetAsyncError with a
  * watchdog (OTC_RCCL_TIMEOUT_S, default 600 s); on an async error or timeout
@@ -378,9 +384,7 @@ struct RcclJob {
     std::vector<hipStream_t> sc, kst, ga;         /* per GPU */
     std::vector<void *> pin[2], pout[2];           /* per GPU, double-buffered */
     std::vector<hipEvent_t> ev_sc[2], ev_k[2], ev_ga[2]; /* per GPU */
-    hipStream_t h2d = nullptr, d2h = nullptr;      /* root copy streams */
     void *root_in[2] = {nullptr, nullptr}, *root_out[2] = {nullptr, nullptr};
-    hipEvent_t ev_in[2] = {}, ev_drained[2] = {};
     bool failed = false;
 
     ~RcclJob()
@@ -392,9 +396,6 @@ struct RcclJob {
                     if (s) (void)hipStreamSynchronize(s);
             }
         (void)hipSetDevice(0);
-        if (!failed)
-            for (hipStream_t s : {h2d, d2h})
-                if (s) (void)hipStreamSynchronize(s);
         for (auto *cv : {&comm_sc, &comm_ga})
             for (ncclComm_t c : *cv)
                 if (c) {
@@ -416,11 +417,7 @@ struct RcclJob {
         for (int i = 0; i < 2; ++i) {
             if (root_in[i]) (void)hipFree(root_in[i]);
             if (root_out[i]) (void)hipFree(root_out[i]);
-            for (hipEvent_t ev : {ev_in[i], ev_drained[i]})
-                if (ev) (void)hipEventDestroy(ev);
         }
-        if (h2d) (void)hipStreamDestroy(h2d);
-        if (d2h) (void)hipStreamDestroy(d2h);
     }
 
     /* wait for `s` while watching every communicator */
@@ -481,12 +478,9 @@ static int rccl_job_init(RcclJob &J, int ngpus, size_t S)
         }
     }
     HIPCHK(hipSetDevice(0));
-    HIPCHK(hipStreamCreateWithFlags(&J.h2d, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&J.d2h, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
         HIPCHK(dev_alloc(&J.root_in[i], round));
         HIPCHK(dev_alloc(&J.root_out[i], round));
-        for (hipEvent_t *ev : {&J.ev_in[i], &J.ev_drained[i]}) HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
     }
     return OTC_OK;
 }
@@ -507,12 +501,10 @@ static int rccl_job_run(RcclJob &J, int mode, const uint8_t *hin, uint8_t *hout,
         const int b = (int)(r & 1);
         const size_t off = r * round, n = std::min(round, nbytes - off);
         HIPCHK(hipSetDevice(0));
-        /* root_in[b] is free once round r-2's scatter has read it */
-        if (r >= 2) HIPCHK(hipStreamWaitEvent(J.h2d, J.ev_sc[b][0], 0));
-        if (n < round) HIPCHK(hipMemsetAsync(J.root_in[b], 0, round, J.h2d));
-        HIPCHK(hipMemcpyAsync(J.root_in[b], hin + off, n, hipMemcpyHostToDevice, J.h2d));
-        HIPCHK(hipEventRecord(J.ev_in[b], J.h2d));
-        HIPCHK(hipStreamWaitEvent(J.sc[0], J.ev_in[b], 0));
+        /* on sc[0]: after round r-2's scatter (which read root_in[b]), before
+         * this round's */
+        if (n < round) HIPCHK(hipMemsetAsync(J.root_in[b], 0, round, J.sc[0]));
+        HIPCHK(hipMemcpyAsync(J.root_in[b], hin + off, n, hipMemcpyHostToDevice, J.sc[0]));
         /* piece_in[b][g] is free once round r-2's cipher has read it */
         if (r >= 2)
             for (int g = 0; g < ngpus; ++g) {
@@ -541,9 +533,9 @@ static int rccl_job_run(RcclJob &J, int mode, const uint8_t *hin, uint8_t *hout,
             HIPCHK(hipEventRecord(J.ev_k[b][g], J.kst[g]));
             HIPCHK(hipStreamWaitEvent(J.ga[g], J.ev_k[b][g], 0));
         }
-        /* root_out[b] is free once round r-2's D2H has drained it */
+        /* root_out[b] is free once round r-2's D2H has drained it: that D2H
+         * precedes this gather on ga[0] */
         HIPCHK(hipSetDevice(0));
-        if (r >= 2) HIPCHK(hipStreamWaitEvent(J.ga[0], J.ev_drained[b], 0));
         RCCLCHK(ncclGroupStart());
         for (int g = 0; g < ngpus; ++g)
             RCCLCHK(ncclGather(J.pout[b][g], J.root_out[b], S, ncclUint8, 0, J.comm_ga[g], J.ga[g]));
@@ -553,9 +545,7 @@ static int rccl_job_run(RcclJob &J, int mode, const uint8_t *hin, uint8_t *hout,
             HIPCHK(hipEventRecord(J.ev_ga[b][g], J.ga[g]));
         }
         HIPCHK(hipSetDevice(0));
-        HIPCHK(hipStreamWaitEvent(J.d2h, J.ev_ga[b][0], 0));
-        HIPCHK(hipMemcpyAsync(hout + off, J.root_out[b], n, hipMemcpyDeviceToHost, J.d2h));
-        HIPCHK(hipEventRecord(J.ev_drained[b], J.d2h));
+        HIPCHK(hipMemcpyAsync(hout + off, J.root_out[b], n, hipMemcpyDeviceToHost, J.ga[0]));
         /* the host only enqueues; it blocks in the copies when the host
          * buffers are pageable (pin them -- otc_host_register -- to overlap) */
     }
@@ -565,7 +555,6 @@ static int rccl_job_run(RcclJob &J, int mode, const uint8_t *hin, uint8_t *hout,
             if (int w = J.wait(s, timeout_s)) return w;
     }
     HIPCHK(hipSetDevice(0));
-    if (int w = J.wait(J.d2h, timeout_s)) return w;
     return OTC_OK;
 }
 
@@ -636,6 +625,7 @@ extern "C" void otc_multi_release(void)
 extern "C" void otc_release_resources(void)
 {
     otc_multi_release();
+    otc_rt::aux_release_all();
 }
 
 /* Logical shards -> devices: shard g runs on device g, or g % ndev when

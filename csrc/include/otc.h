@@ -59,14 +59,18 @@ int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 
 /* ---- implementation selection ------------------------------------------- */
 #define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for CTR calls >= 2 GiB (AES-256:
-                               >= 1 GiB), T-table otherwise (OTC_IMPL=ttable|bitslice env overrides for the whole
-                               process) */
+                               >= 1 GiB), the split below for ECB / CBC-decrypt >= 1 GiB, T-table otherwise
+                               (OTC_IMPL=ttable|bitslice|split env overrides for the whole process) */
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
 #define OTC_IMPL_BITSLICE 2 /* 32-block-per-lane bitsliced VALU kernel */
+#define OTC_IMPL_SPLIT 3    /* ECB and CBC-decrypt: both kernels CONCURRENTLY on disjoint ranges (the bitsliced
+                               one on an auxiliary stream), co-resident on every CU -- LDS and VALU busy at
+                               once; "auto" for these calls >= 1 GiB.  CTR: as auto */
 
-/* The kernel family `impl` resolves to for a call (mode_ctr: CTR, else ECB
- * encrypt) of nbytes with a bits-bit key; -1 for an invalid impl. */
-int otc_pick_impl(int impl, int bits, int mode_ctr, uint64_t nbytes);
+/* The kernel family `impl` resolves to for a call of nbytes with a bits-bit
+ * key (mode 1: CTR, 0: ECB encryption, 2: ECB / CBC decryption); -1 for an
+ * invalid impl. */
+int otc_pick_impl(int impl, int bits, int mode, uint64_t nbytes);
 /* OTC_IMPL_TTABLE / OTC_IMPL_BITSLICE: what the calling thread's last
  * otc_aes_ctr / otc_aes_ecb call ran (OTC_IMPL_AUTO before any call). */
 int otc_last_impl(void);
@@ -109,9 +113,12 @@ int otc_aes_ctr_rfc3686(const void *in, void *out, size_t nbytes, const otc_aes_
                         const uint8_t nonce[4], const uint8_t ivec[8], uint64_t block_offset,
                         int impl, void *stream);
 
-/* CBC decryption (parallel): P_i = D(C_i) ^ C_{i-1}, C_{-1} = iv. */
+/* CBC decryption (parallel): P_i = D(C_i) ^ C_{i-1}, C_{-1} = iv.  _impl:
+ * with a kernel choice (OTC_IMPL_*; the plain form is OTC_IMPL_AUTO). */
 int otc_aes_cbc_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
                         const uint8_t iv[16], void *stream);
+int otc_aes_cbc_decrypt_impl(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                             const uint8_t iv[16], int impl, void *stream);
 
 /* CBC encryption over `nseg` independent segments of `seg_bytes` each
  * (contiguous, segment s at offset s*seg_bytes).  Segment s uses

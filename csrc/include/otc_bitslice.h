@@ -318,6 +318,7 @@ OTC_HD void mix_columns_ark(const W *in, W *out, KF kf)
 #include "otc_sbox_lut3.h"
 static_assert(OTC_SBOX_KEY_TERMS == 11, "kt_ready lists t[0..10]: update its operand list with the S-box header");
 #include "otc_mixcol.h"
+#include "otc_invmix.h"
 namespace otc_bs {
 
 template <bool CTR_CACHE, int R, class KF>
@@ -390,12 +391,14 @@ OTC_HD void encrypt_round(W *s, KF &kf)
  * The key comes as S-box key TERMS: kt(b, t) fills the OTC_SBOX_KEY_TERMS
  * values of byte b (sbox_key_terms of its 8 plane masks) -- computed from the
  * round key on the fly (KeyMasks) or read from a precomputed table. */
-template <int MIX, class KT, int FENCE = 2>
+template <int MIX, class KT, int FENCE = 2, bool DEC = false>
 OTC_HD void round_step_kt(W *s, KT kt)
 {
     W ns[128];
     /* S-box i of the round (streaming order) is byte r + 4((c + r) & 3) with
-     * c = i / 4, r = i % 4 */
+     * c = i / 4, r = i % 4 (ShiftRows brings it into column c); decryption:
+     * r + 4((c - r) & 3) (InvShiftRows) */
+    constexpr int SG = DEC ? -1 : 1;
     W tn[OTC_SBOX_KEY_TERMS];
     if (OTC_BS_KT_PREFETCH) kt(0, tn);
 #pragma unroll
@@ -403,7 +406,7 @@ OTC_HD void round_step_kt(W *s, KT kt)
         W col[32];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int b = r + 4 * ((c + r) & 3);
+            const int b = r + 4 * ((c + SG * r) & 3);
             W *x = s + 8 * b;
             W t[OTC_SBOX_KEY_TERMS];
             if (OTC_BS_KT_PREFETCH) {
@@ -411,7 +414,7 @@ OTC_HD void round_step_kt(W *s, KT kt)
                 for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = tn[j];
                 kt_ready(t);
                 const int i = 4 * c + r + 1;
-                if (i < 16) kt((i & 3) + 4 * (((i >> 2) + (i & 3)) & 3), tn);
+                if (i < 16) kt((i & 3) + 4 * (((i >> 2) + SG * (i & 3)) & 3), tn);
                 sched_fence(); /* the loads issue here, not next to their use */
             } else {
                 kt(b, t);
@@ -427,7 +430,9 @@ OTC_HD void round_step_kt(W *s, KT kt)
 #pragma unroll
             for (int i = 0; i < 8; ++i) col[8 * r + i] = x[i];
         }
-        if (MIX == 2)
+        if (DEC)
+            inv_mix_column_g(col, ns + 32 * c); /* L o InvMixColumns o L (otc_invmix.h) */
+        else if (MIX == 2)
             mix_column_g(col, ns + 32 * c);
         else if (MIX == 1)
             mix_column_t<true>(col, ns + 32 * c);
@@ -443,8 +448,9 @@ OTC_HD void round_step_kt(W *s, KT kt)
 }
 
 /* Final round: S-box with the key folded in + ShiftRows (the last round key
- * is left to the caller's output XOR, as in encrypt_planes). */
-template <class KT>
+ * is left to the caller's output XOR, as in encrypt_planes).  Decryption:
+ * InvShiftRows, then L on every byte (the post-map of S^-1 = L S L). */
+template <class KT, bool DEC = false>
 OTC_HD void round_final_kt(W *s, KT kt)
 {
     W tn[OTC_SBOX_KEY_TERMS];
@@ -467,10 +473,44 @@ OTC_HD void round_final_kt(W *s, KT kt)
         pin8(x);
     }
     W t[128];
-    shift_rows(s, t);
+    if (DEC) {
+        /* new byte (r, c) = L(old byte (r, c - r)) */
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) lmap_byte(s + 8 * (r + 4 * ((c - r) & 3)), t + 8 * (r + 4 * c));
+    } else {
+        shift_rows(s, t);
+    }
 #pragma unroll
     for (int q = 0; q < 128; ++q) s[q] = t[q];
 }
+
+/* Decryption pre-map: L on every byte of the loaded ciphertext planes */
+OTC_HD void dec_premap(W *s)
+{
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        W t[8];
+        lmap_byte(s + 8 * b, t);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s[8 * b + i] = t[i];
+    }
+}
+
+/* Byte value of L = M^-1 (bit i <- bits i+2, i+5, i+7 mod 8) and the
+ * S-box input key of decryption round r from the equivalent-inverse-cipher
+ * round-key byte k (otc_invmix.h): L(k) ^ 0x05, and ^ L(0x05) = 0x63 after
+ * the first round (the constant the previous round's L o InvMixColumns o L
+ * leaves behind). */
+OTC_HD uint32_t lmap_value(uint32_t v)
+{
+    uint32_t o = 0;
+    for (int i = 0; i < 8; ++i)
+        o |= (((v >> ((i + 2) & 7)) ^ (v >> ((i + 5) & 7)) ^ (v >> ((i + 7) & 7))) & 1u) << i;
+    return o;
+}
+OTC_HD uint32_t dec_round_key_byte(uint32_t k, int r) { return lmap_value(k) ^ 0x05u ^ (r > 0 ? 0x63u : 0u); }
 
 /* key terms from a plane-mask functor kf(p) */
 template <class KF>

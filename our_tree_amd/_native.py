@@ -167,6 +167,9 @@ def _declare_gpu(lib):
         "otc_aes_ctr_ctx_init": (c_int, [P(OtcCtrCtx), c_u8p]),
         "otc_aes_ctr_stream": (c_int, [P(OtcCtrCtx), K, c_sz, c_vp, c_vp, c_int, c_vp]),
         "otc_aes_cbc_decrypt": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_vp]),
+        "otc_aes_cbc_decrypt_impl": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_int, c_vp]),
+        "otc_stream_create": (c_vp, []),
+        "otc_stream_destroy": (None, [c_vp]),
         "otc_aes_cbc_encrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cbc_decrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cfb128_decrypt": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_vp]),

@@ -16,7 +16,7 @@ import torch
 from .. import _native
 from .keys import expand_key
 
-IMPLS = {"auto": 0, "ttable": 1, "bitslice": 2}
+IMPLS = {"auto": 0, "ttable": 1, "bitslice": 2, "split": 3}  # otc.h OTC_IMPL_*
 
 
 def _impl(impl) -> int:
@@ -31,10 +31,16 @@ def _impl(impl) -> int:
 _IMPL_NAMES = {v: k for k, v in IMPLS.items()}
 
 
+_PICK_MODES = {"ctr": 1, "ecb": 0, "dec": 2, "ecb-dec": 2, "cbc-dec": 2}
+
+
 def pick_impl(impl="auto", bits: int = 128, mode: str = "ctr", nbytes: int = 0) -> str:
-    """The kernel family ``impl`` resolves to for a ``mode`` ("ctr" or "ecb")
-    call of ``nbytes`` with a ``bits``-bit key (the native routing rule)."""
-    r = _lib().otc_pick_impl(_impl(impl), int(bits), 1 if mode == "ctr" else 0, int(nbytes))
+    """The kernel family ``impl`` resolves to for a ``mode`` call ("ctr",
+    "ecb" = ECB encryption, "dec" = ECB / CBC decryption) of ``nbytes`` with
+    a ``bits``-bit key (the native routing rule)."""
+    if mode not in _PICK_MODES:
+        raise ValueError(f"mode must be one of {list(_PICK_MODES)}")
+    r = _lib().otc_pick_impl(_impl(impl), int(bits), _PICK_MODES[mode], int(nbytes))
     if r < 0:
         raise ValueError(f"bad impl {impl!r}")
     return _IMPL_NAMES[r]
@@ -461,25 +467,30 @@ def ecb_encrypt(x: torch.Tensor, key: bytes, out=None, impl="auto") -> torch.Ten
     return out
 
 
-def ecb_decrypt(x: torch.Tensor, key: bytes, out=None) -> torch.Tensor:
+def ecb_decrypt(x: torch.Tensor, key: bytes, out=None, impl="auto") -> torch.Tensor:
+    """ECB decryption: the T-table inverse cipher, the bitsliced one (the
+    forward S-box as S^-1 = L S L), or both concurrently ("split", auto from
+    1 GiB)."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     k = expand_key(key, decrypt=True)
     with torch.cuda.device(x.device):
-        rc = _run(x, out, lambda ip, op: _lib().otc_aes_ecb(ip, op, _nbytes(x), ctypes.byref(k), 0, _stream(x)))
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_ecb(ip, op, _nbytes(x), ctypes.byref(k), _impl(impl),
+                                                           _stream(x)))
     _native.check(rc, "otc_aes_ecb(decrypt)")
     return out
 
 
-def cbc_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None) -> torch.Tensor:
-    """Parallel CBC decryption.  In place (out=x) runs through a copy of the
-    input: block i needs ciphertext block i-1, which its own output overwrites."""
+def cbc_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None, impl="auto") -> torch.Tensor:
+    """Parallel CBC decryption (kernel choice as ecb_decrypt).  In place
+    (out=x) runs through a copy of the input: block i needs ciphertext block
+    i-1, which its own output overwrites."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     k = expand_key(key, decrypt=True)
     with torch.cuda.device(x.device):
-        rc = _run(x, out, lambda ip, op: _lib().otc_aes_cbc_decrypt(ip, op, _nbytes(x), ctypes.byref(k), _b16(iv, "iv"),
-            _stream(x)), inplace_ok=False)
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_cbc_decrypt_impl(ip, op, _nbytes(x), ctypes.byref(k),
+            _b16(iv, "iv"), _impl(impl), _stream(x)), inplace_ok=False)
     _native.check(rc, "otc_aes_cbc_decrypt")
     return out
 

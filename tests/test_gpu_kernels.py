@@ -433,20 +433,65 @@ def test_bitslice_launch_structures(gpu, bits):
 
 
 def test_auto_routing_rule(gpu):
-    """impl="auto" by size (docs/PERF.md, profiles/r3/auto_impl): bitsliced
-    CTR from 2 GiB (AES-128/192) or 1 GiB (AES-256), T-table for everything
-    else; the boundaries are exact."""
+    """impl="auto" by size (docs/PERF.md, profiles/r3/auto_impl,
+    profiles/r4/ecb_split): bitsliced CTR from 2 GiB (AES-128/192) or 1 GiB
+    (AES-256), the co-resident split for ECB encryption from 1 GiB, T-table
+    for everything else; the boundaries are exact.  "split" is an
+    ECB-encryption form: for CTR it routes as auto."""
     G = 1 << 30
     cases = [(128, "ctr", 64 * G, "bitslice"), (128, "ctr", 2 * G - 16, "ttable"), (128, "ctr", 2 * G, "bitslice"),
              (256, "ctr", 1 * G, "bitslice"), (256, "ctr", 1 * G - 16, "ttable"), (256, "ctr", 4 * G, "bitslice"),
              (192, "ctr", 2 * G, "bitslice"), (192, "ctr", 2 * G - 16, "ttable"), (192, "ctr", 1 * G, "ttable"),
-             (256, "ecb", 64 * G, "ttable"), (128, "ctr", 16, "ttable")]
+             (256, "ecb", 64 * G, "split"), (128, "ecb", 1 * G, "split"), (192, "ecb", 1 * G - 16, "ttable"),
+             (128, "ctr", 16, "ttable")]
     for bits, mode, n, want in cases:
         assert ops.pick_impl("auto", bits, mode, n) == want, (bits, mode, n)
         assert ops.pick_impl("ttable", bits, mode, n) == "ttable"
         assert ops.pick_impl("bitslice", bits, mode, n) == "bitslice"
+        assert ops.pick_impl("split", bits, mode, n) == ("split" if mode == "ecb" else want)
     with pytest.raises(ValueError):
         ops.pick_impl("hybrid")
+
+
+@pytest.mark.parametrize("bits", [128, 192, 256])
+def test_ecb_split_matches_ttable(gpu, bits):
+    """The co-resident split (T-table kernel on the caller's stream, bitsliced
+    kernel on the auxiliary stream over the last share of the blocks) is
+    byte-identical to the T-table alone, out of place and in place, on sizes
+    whose split point is not task aligned on the T-table side; a size whose
+    share rounds to no full bitsliced task runs the T-table alone."""
+    for n, want in ((64 * 2048 * 16 * 3 + 48, "split"), (2048 * 16 + 16, "ttable"), (160 << 20, "split")):
+        key = os.urandom(bits // 8)
+        x = torch.empty(n, dtype=torch.uint8, device=gpu)
+        ops.fill_random_(x, seed=n + bits)
+        t = ops.ecb_encrypt(x, key, impl="ttable")
+        y = ops.ecb_encrypt(x, key, impl="split")
+        assert ops.last_impl() == want, (n, ops.last_impl())
+        w = x.clone()
+        ops.ecb_encrypt(w, key, out=w, impl="split")
+        torch.cuda.synchronize()
+        assert torch.equal(y, t), (bits, n)
+        assert torch.equal(w, t), (bits, n, "in place")
+        S = 1 << 14
+        for off in (0, (n // 2) & ~15, n - S):
+            assert host(y[off:off + S]) == cpu_ref.ecb(key, host(x[off:off + S])), (bits, n, off)
+
+
+def test_ecb_split_stream_order(gpu):
+    """The caller's stream waits for BOTH kernels: work queued behind the
+    split on the same stream sees the whole output, and the split starts only
+    after work queued before it (fork / join events)."""
+    key = os.urandom(32)
+    n = 256 << 20
+    x = torch.empty(n, dtype=torch.uint8, device=gpu)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        ops.fill_random_(x, seed=77)  # queued before the split on the same stream
+        y = ops.ecb_encrypt(x, key, impl="split")
+        z = ops.ecb_encrypt(y, key, impl="ttable")  # consumes the split's output, tail included
+    s.synchronize()
+    exp = cpu_ref.ecb(key, cpu_ref.ecb(key, host(x[n - 4096:])))
+    assert host(z[n - 4096:]) == exp
 
 
 @pytest.mark.parametrize("bits,n", [(128, (2 << 30) + 3), (192, (2 << 30) + 3), (256, (1 << 30) + 3)])
@@ -472,3 +517,35 @@ def test_ctr_auto_large_bitsliced(gpu, bits, n):
     del x, y, t
     torch.cuda.empty_cache()
 
+
+
+@pytest.mark.parametrize("bits", [128, 192, 256])
+def test_bitsliced_decrypt_matches_ttable(gpu, bits):
+    """The bitsliced inverse cipher (the forward 77-LUT S-box as S^-1 = L S L,
+    L o InvMixColumns o L between rounds, otc_invmix.h) and the decrypt split
+    equal the T-table decryption, ECB (in and out of place) and CBC (IV on
+    block 0; the split's bitsliced part takes block nt-1 as its predecessor),
+    on sizes with partial first / last bitsliced tasks."""
+    for n in (16 * 2048 * 9 + 16 * 77, 16 * 100, 16 * 2048 * 40 + 16, 96 << 20):
+        key = os.urandom(bits // 8)
+        iv = os.urandom(16)
+        x = torch.empty(n, dtype=torch.uint8, device=gpu)
+        ops.fill_random_(x, seed=n ^ bits)
+        t = ops.ecb_decrypt(x, key, impl="ttable")
+        for impl in ("bitslice", "split"):
+            y = ops.ecb_decrypt(x, key, impl=impl)
+            w = x.clone()
+            ops.ecb_decrypt(w, key, out=w, impl=impl)
+            torch.cuda.synchronize()
+            assert torch.equal(y, t), ("ecb", impl, bits, n)
+            assert torch.equal(w, t), ("ecb in place", impl, bits, n)
+        tc = ops.cbc_decrypt(x, key, iv, impl="ttable")
+        for impl in ("bitslice", "split"):
+            c = ops.cbc_decrypt(x, key, iv, impl=impl)
+            torch.cuda.synchronize()
+            assert torch.equal(c, tc), ("cbc", impl, bits, n)
+        S = min(n, 1 << 14)
+        assert host(t[:S]) == cpu_ref.ecb(key, host(x[:S]), decrypt=True)
+        assert host(tc[:S]) == cpu_ref.cbc(key, iv, host(x[:S]), decrypt=True)
+    assert ops.pick_impl("auto", bits, "dec", 1 << 30) == "split"
+    assert ops.pick_impl("auto", bits, "dec", (1 << 30) - 16) == "ttable"

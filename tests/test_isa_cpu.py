@@ -26,21 +26,29 @@ def counts():
                          capture_output=True, text=True).stdout
     rows = {}
     for line in out.splitlines():
-        m = re.search(r": (\w+) (AES-\d+) VALU (\d+) .* VGPRs (-?\d+) scratch (-?\d+)", line)
+        m = re.search(r": ([\w-]+) (AES-\d+) VALU (\d+) .* VGPRs (-?\d+) scratch (-?\d+) scratch_ops (\d+)", line)
         if m:
-            rows[(m.group(1), m.group(2))] = (int(m.group(3)), int(m.group(4)), int(m.group(5)))
+            rows[(m.group(1), m.group(2))] = (int(m.group(3)), int(m.group(4)), int(m.group(5)), int(m.group(6)))
     return rows
 
 
 def test_every_bulk_kernel_found(counts):
-    for mode in ("CTR", "ECB"):
+    for mode in ("CTR", "ECB", "ECB-dec", "CBC-dec"):
         for bits in ("AES-128", "AES-192", "AES-256"):
             assert (mode, bits) in counts, (mode, bits, sorted(counts))
 
 
 def test_bulk_kernels_spill_free(counts):
-    for key, (valu, vgprs, scratch) in counts.items():
-        assert scratch == 0, (key, scratch)
+    """Encryption kernels: no scratch at all.  The decryption kernels (L o
+    InvMixColumns o L is 125 nodes per column against MixColumns' 55) keep a
+    few 64-bit addresses in scratch across the rounds: at most 24 scratch
+    instructions per 2048-block task (beside ~26k VALU), none in the rounds
+    themselves."""
+    for key, (valu, vgprs, scratch, sops) in counts.items():
+        if key[0] in ("ECB-dec", "CBC-dec"):
+            assert sops <= 24, (key, sops)
+        else:
+            assert scratch == 0, (key, scratch)
         assert 0 < vgprs <= 168, (key, vgprs)  # 3 waves per SIMD
 
 

@@ -62,14 +62,14 @@ def main():
             ins = re.findall(r"^\s+([a-z_0-9]+)", f, re.M)
             cnt = lambda p: sum(1 for i in ins if i.startswith(p))
             tm = re.search(r"t3ILi(\d+)ELi(\d)E", name)
-            mode = {"0": "CTR", "1": "ECB"}.get(tm.group(2), "?") if tm else "?"
+            mode = {"0": "CTR", "1": "ECB", "2": "ECB-dec", "3": "CBC-dec"}.get(tm.group(2), "?") if tm else "?"
             if mode == "CTR" and re.search(r"Lb0ELb1EEE", name):
                 mode = "CTR-nocache"  # fallback when the counter-caching tables do not fit
             bits = NAMES.get(f"Li{tm.group(1)}E", "?") if tm else "?"
             vg, scr = meta.get(name + ".kd", meta.get(name, (-1, -1)))
             print(f"{obj}: {mode} {bits} VALU {cnt('v_')} SALU {cnt('s_') - cnt('s_load') - cnt('s_buffer')} "
                   f"SMEM {cnt('s_load') + cnt('s_buffer')} VMEM {cnt('global_') + cnt('buffer_')} "
-                  f"LDS {cnt('ds_')} VGPRs {vg} scratch {scr}")
+                  f"LDS {cnt('ds_')} VGPRs {vg} scratch {scr} scratch_ops {cnt('scratch_')}")
 
 
 if __name__ == "__main__":
