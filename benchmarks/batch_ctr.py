@@ -16,6 +16,8 @@ Synthetic random messages and keys.  Prints one JSON line.
 import argparse
 import json
 import os
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # before torch / HIP: dmabuf IPC only on this host driver (as bench.py)
 import sys
 import time
 

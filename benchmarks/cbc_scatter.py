@@ -34,6 +34,8 @@ duplex communicators, so the collective code path is what is measured.
 import argparse
 import json
 import os
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # before torch / HIP: dmabuf IPC only on this host driver (as bench.py)
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

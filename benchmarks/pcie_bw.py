@@ -2,6 +2,10 @@
 """PCIe ceiling of the box: pinned 4 GiB H2D, D2H and both directions at once
 (two streams); the reference point for host-streamed cipher throughput
 (config 5, docs/PERF.md)."""
+import os
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # before torch / HIP: dmabuf IPC only on this host driver (as bench.py)
+
 import torch, time, json
 n = 4 << 30
 h = torch.empty(n, dtype=torch.uint8, pin_memory=True)

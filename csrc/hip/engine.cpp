@@ -240,7 +240,7 @@ size_t ecb_split_min(int bits) { return bits == 256 ? ((size_t)1 << 30) : ((size
 /* decryption (ECB, CBC): the bitsliced inverse cipher costs ~1.17x the
  * encryption's VALU work (L o InvMixColumns o L: 121 nodes per column vs
  * MixColumns' 55), so it takes a smaller share */
-double dec_split_share(int bits) { return bits == 256 ? 0.2 : bits == 192 ? 0.2 : 0.2; }
+double dec_split_share(int bits, bool cbc) { return (!cbc && bits == 256) ? 0.2 : 0.15; }
 size_t dec_split_min(int) { return (size_t)1 << 30; }
 
 int pick_ecb_impl(int impl, int bits, size_t nbytes)
@@ -297,7 +297,7 @@ hipError_t ecb_split(const void *in, void *out, uint64_t nblocks, const otc_aes_
             [&](uint64_t nt) { return otc_impl::tt_ecb_encrypt(pi, po, nt, K, st); },
             [&](uint64_t nt, uint64_t nb, hipStream_t s) { return otc_impl::bs_ecb_encrypt(pi + 16 * nt, po + 16 * nt, nb, K, s); });
     return split_run(
-        nblocks, dec_split_share(K.bits), st, ran,
+        nblocks, dec_split_share(K.bits, false), st, ran,
         [&](uint64_t nt) { return otc_impl::tt_ecb_decrypt(pi, po, nt, K, st); },
         [&](uint64_t nt, uint64_t nb, hipStream_t s) { return otc_impl::bs_ecb_decrypt(pi + 16 * nt, po + 16 * nt, nb, K, s); });
 }
@@ -308,7 +308,7 @@ hipError_t cbc_dec_split(const void *in, void *out, uint64_t nblocks, const otc_
     const uint8_t *pi = (const uint8_t *)in;
     uint8_t *po = (uint8_t *)out;
     return split_run(
-        nblocks, dec_split_share(K.bits), st, ran,
+        nblocks, dec_split_share(K.bits, true), st, ran,
         [&](uint64_t nt) { return otc_impl::tt_cbc_decrypt(pi, po, nt, K, ctr_from_bytes(iv), st); },
         /* the bitsliced part's block 0 XORs with block nt-1 of the input */
         [&](uint64_t nt, uint64_t nb, hipStream_t s) {

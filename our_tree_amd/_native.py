@@ -169,6 +169,9 @@ def _declare_gpu(lib):
         "otc_aes_cbc_decrypt": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cbc_decrypt_impl": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_int, c_vp]),
         "otc_stream_create": (c_vp, []),
+        "otc_dev_malloc": (c_vp, [c_sz]),
+        "otc_dev_free": (None, [c_vp]),
+        "otc_memcpy": (c_int, [c_vp, c_vp, c_sz, c_int]),
         "otc_stream_destroy": (None, [c_vp]),
         "otc_aes_cbc_encrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cbc_decrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),

@@ -58,7 +58,18 @@ rehearse)
     # N shards must fit ONE GPU: 2 GiB each unless the args say otherwise (argparse keeps the last --gib)
     OTC_DIST_BACKEND=gloo OTC_SHARE_GPUS=1 timeout -k 10 600 python bench.py --gpus "$n" --no-clock --gib 2 "$@" \
         > $OUT/rehearse_dp$n.txt 2>&1 || { tail -30 $OUT/rehearse_dp$n.txt; exit 1; }
-    grep '^{' $OUT/rehearse_dp$n.txt
+    grep '^{' $OUT/rehearse_dp$n.txt | tail -1 > $OUT/rehearse_dp$n.json
+    cat $OUT/rehearse_dp$n.json
+    # the per-rank table (ranks share one GPU here: their energy keys all read that GPU)
+    python3 - $OUT/rehearse_dp$n.json <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read())
+print(f"{'rank':>4} {'GB/s':>9} {'verified':>8} {'W':>7} {'J/GB':>7} {'PPT':>6}")
+for r in d.get("per_rank", []):
+    print(f"{r['rank']:>4} {r['gbps']:>9} {str(r['verified']):>8} {str(r['avg_socket_w']):>7} "
+          f"{str(r['joules_per_gb']):>7} {str(r['ppt_residency']):>6}")
+print("preflight", d.get("preflight"), "rccl_ranks_verified", d.get("rccl_ranks_verified"))
+PY
     ;;
 kt)
     name=$1; shift; [ "$1" = "--" ] && shift

@@ -2,7 +2,8 @@
 # Mode x key-size sweep of the current build (through gpurun):
 #   gpurun --timeout 900 -- bash scripts/sweep.sh OUTNAME
 # every AES mode at 128/192/256 bits on a 4 GiB buffer (impl auto; in place
-# except the chained decrypts),
+# except the chained decrypts), every line verified against the oracle
+# (otbench --verify: pre-op snapshots, so in place too; exit 3 on a mismatch),
 # CTR at 64 GiB with both kernels, then the J/GB power probe and a kernel trace
 # of a short bench.py run.  Output under gpurun_out/OUTNAME/.
 set -o pipefail
@@ -11,10 +12,10 @@ O=gpurun_out/${1:-sweep}; mkdir -p $O
 for m in ctr ecb ecb-dec cbc-dec cfb-dec cbc-enc-seg cfb-enc-seg; do for b in 128 192 256; do
     ip=--inplace  # the chained decrypts read the previous ciphertext block: out of place
     case $m in cbc-dec|cfb-dec) ip= ;; esac
-    timeout -k 10 120 ./bin/otbench --mode $m --bits $b --bytes 4G $ip --iters 10 --warmup 2 --clock >> $O/sweep.jsonl || exit 1
+    timeout -k 10 120 ./bin/otbench --mode $m --bits $b --bytes 4G $ip --iters 10 --warmup 2 --clock --verify >> $O/sweep.jsonl || exit 1
 done; done
 for i in ttable bitslice; do for b in 128 256; do
-    timeout -k 10 120 ./bin/otbench --mode ctr --bits $b --bytes 64G --inplace --iters 10 --warmup 2 --impl $i --clock >> $O/ctr64g.jsonl || exit 1
+    timeout -k 10 120 ./bin/otbench --mode ctr --bits $b --bytes 64G --inplace --iters 10 --warmup 2 --impl $i --clock --verify >> $O/ctr64g.jsonl || exit 1
 done; done
 bash scripts/power_probe.sh "bitslice" > $O/power.txt 2>&1 || { tail -5 $O/power.txt; exit 1; }
 cp -r gpurun_out/power $O/ 2>/dev/null
@@ -28,6 +29,7 @@ o = sys.argv[1]
 for f in ("sweep.jsonl", "ctr64g.jsonl"):
     for l in open(f"{o}/{f}"):
         d = json.loads(l)
-        print(f, d["mode"], d["bits"], d["bytes"] >> 30, "GiB", d["impl"], d["gbps"], d.get("held_clock_ghz"))
+        print(f, d["mode"], d["bits"], d["bytes"] >> 30, "GiB", d["impl"], d["gbps"], d.get("held_clock_ghz"),
+              "verified" if d["verified"] is True else "NOT VERIFIED")
 PY
 cat $O/power.txt | tail -3
