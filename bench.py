@@ -69,8 +69,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 BASELINE_GBPS = 0.519  # BASELINE.md headline CTR: AES-NI CTR-256, 1000 MiB, 8 threads (frankchn)
 BASELINE_GPU_GBPS = 2.41  # BASELINE.md repo headline: CUDA "AES ECB" 1000 MiB (baryon)
 AES128_EQUIV = 14 / 10  # AES-256 -> AES-128 round ratio (BASELINE.md caveat 5: derived, not published)
-RANK_KEYS = ("gbps", "held_clock_ghz", "verified", "joules", "avg_socket_w", "joules_per_gb", "ppt_residency",
-             "gfxclk_mhz_mean", "xgmi_read_kb", "xgmi_write_kb")
+RANK_KEYS = ("gbps", "held_clock_ghz", "verified", "joules", "energy_gb", "avg_socket_w", "joules_per_gb",
+             "ppt_residency", "gfxclk_mhz_mean", "xgmi_read_kb", "xgmi_write_kb")
 
 
 def baseline_ratios(value: float) -> dict:
@@ -106,15 +106,17 @@ def per_rank_table(rows: list[list[float]]) -> list[dict]:
     return out
 
 
-def node_energy(table: list[dict], total_bytes: int) -> dict:
-    """Whole-node energy keys from the per-rank table (None when no rank
-    could read its power counters)."""
+def node_energy(table: list[dict]) -> dict:
+    """Whole-node energy keys from the per-rank table: J/GB = all ranks'
+    socket energy over all the bytes their energy windows processed (None
+    unless every rank read its counters)."""
     js = [d["joules"] for d in table if d["joules"] is not None]
+    gb = [d["energy_gb"] for d in table if d["energy_gb"] is not None]
     ws = [d["avg_socket_w"] for d in table if d["avg_socket_w"] is not None]
     pp = [d["ppt_residency"] for d in table if d["ppt_residency"] is not None]
-    full = len(js) == len(table)
+    full = len(js) == len(gb) == len(table)
     return {
-        "joules_per_gb": round(sum(js) / (total_bytes / 1e9), 4) if full and js else None,
+        "joules_per_gb": round(sum(js) / sum(gb), 4) if full and js and sum(gb) > 0 else None,
         "avg_socket_w_per_gpu": round(sum(ws) / len(ws), 1) if ws else None,
         "ppt_residency_max": round(max(pp), 4) if pp else None,
         "energy_ranks": len(js),
@@ -184,6 +186,8 @@ def main():
                     help="skip timing the other AES-128 CTR kernel (T-table vs bitsliced) on the same shard")
     ap.add_argument("--no-clock", action="store_true")
     ap.add_argument("--no-power", action="store_true", help="skip the amdsmi energy / power / PPT counters")
+    ap.add_argument("--energy-min-s", type=float, default=2.0,
+                    help="shortest energy window: untimed identical steps extend it after the timed ones")
     ap.add_argument("--no-scatter", action="store_true", help="skip the RCCL scatter/gather AES-256-CBC pass")
     ap.add_argument("--scatter-mib", type=int, default=512, help="per-rank bytes per scatter round (MiB)")
     ap.add_argument("--scatter-rounds", type=int, default=4)
@@ -317,7 +321,11 @@ def main():
 
     def timed(nsteps, k, impl=args.impl, measure=False):
         """returns (MAX over ranks of the barrier-to-barrier time, this rank's
-        own time to its last synchronize, power stats of this rank or None)"""
+        own time to its last synchronize, power stats of this rank or None).
+        With ``measure`` the energy window opens with the timed steps and,
+        if they took less than --energy-min-s, stays open over identical
+        untimed steps after the clock has stopped: the socket energy counter
+        updates about every millisecond, so a short window reads ~0 J."""
         for _ in range(args.warmup):
             step(k, impl)
         sync()
@@ -331,10 +339,19 @@ def main():
             step(k, impl)
         sync()
         mine = time.perf_counter() - t0
-        pw = meter.stop(nbytes * nsteps) if measure and meter is not None else None
         if torch.distributed.is_initialized():
             torch.distributed.barrier()
         el = time.perf_counter() - t0
+        pw = None
+        if measure and meter is not None:
+            done = nsteps
+            while time.perf_counter() - t0 < args.energy_min_s:
+                step(k, impl)
+                done += 1
+            sync()
+            pw = meter.stop(nbytes * done)
+            if pw.get("available"):
+                pw["energy_steps"] = done
         return pdist.allreduce_max(el), mine, pw
 
     elapsed, mine, pw = timed(args.steps, key, measure=True)
@@ -366,11 +383,15 @@ def main():
     nan = float("nan")
     pwv = pw if pw and pw.get("available") else {}
     row = [nbytes * args.steps / mine / 1e9, clk_ghz if clk_ghz else nan, 1.0 if ok else 0.0]
+    energy_gb = nbytes * pwv["energy_steps"] / 1e9 if pwv.get("energy_steps") else None
+    row += [float(pwv["joules"]) if pwv.get("joules") is not None else nan, energy_gb if energy_gb else nan]
     row += [float(pwv[k]) if pwv.get(k) is not None else nan
-            for k in ("joules", "avg_socket_w", "joules_per_gb", "ppt_residency", "gfxclk_mhz_mean",
-                      "xgmi_read_kb", "xgmi_write_kb")]
+            for k in ("avg_socket_w", "joules_per_gb", "ppt_residency", "gfxclk_mhz_mean", "xgmi_read_kb",
+                      "xgmi_write_kb")]
     table = per_rank_table(pdist.gather_floats(row))
-    energy = node_energy(table, total_bytes)
+    energy = node_energy(table)
+    if pwv:
+        energy["energy_window_s"] = pwv.get("window_s")  # rank 0's: timed steps + untimed extension
     if meter is not None and not pwv:
         energy["energy_unavailable"] = pw.get("reason") if pw else "no window"
 

@@ -14,6 +14,12 @@ for m in ctr ecb ecb-dec cbc-dec cfb-dec cbc-enc-seg cfb-enc-seg; do for b in 12
     case $m in cbc-dec|cfb-dec) ip= ;; esac
     timeout -k 10 120 ./bin/otbench --mode $m --bits $b --bytes 4G $ip --iters 10 --warmup 2 --clock --verify >> $O/sweep.jsonl || exit 1
 done; done
+# the ECB / decrypt paths at 64 GiB (32 GiB out of place for CBC), auto = the co-resident split
+for m in ecb ecb-dec cbc-dec; do for b in 128 256; do
+    sz=64G; ip=--inplace
+    [ $m = cbc-dec ] && { sz=32G; ip=; }
+    timeout -k 10 120 ./bin/otbench --mode $m --bits $b --bytes $sz $ip --iters 10 --warmup 2 --clock --verify >> $O/big.jsonl || exit 1
+done; done
 for i in ttable bitslice; do for b in 128 256; do
     timeout -k 10 120 ./bin/otbench --mode ctr --bits $b --bytes 64G --inplace --iters 10 --warmup 2 --impl $i --clock --verify >> $O/ctr64g.jsonl || exit 1
 done; done
@@ -26,7 +32,7 @@ python3 tools/rocpd_summary.py "$db" > $O/kt/kernels.txt && head -12 $O/kt/kerne
 python3 - "$O" <<'PY'
 import json, sys
 o = sys.argv[1]
-for f in ("sweep.jsonl", "ctr64g.jsonl"):
+for f in ("sweep.jsonl", "big.jsonl", "ctr64g.jsonl"):
     for l in open(f"{o}/{f}"):
         d = json.loads(l)
         print(f, d["mode"], d["bits"], d["bytes"] >> 30, "GiB", d["impl"], d["gbps"], d.get("held_clock_ghz"),

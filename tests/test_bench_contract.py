@@ -100,15 +100,15 @@ def test_node_energy_and_table():
     import bench
 
     nan = float("nan")
-    rows = [[100.0, 1.9, 1.0, 50.0, 1300.0, 0.5, 0.9, 1800.0, 10.0, 20.0],
-            [90.0, nan, 1.0, 60.0, 1350.0, 0.6, 0.95, 1790.0, nan, nan]]
+    rows = [[100.0, 1.9, 1.0, 50.0, 100.0, 1300.0, 0.5, 0.9, 1800.0, 10.0, 20.0],
+            [90.0, nan, 1.0, 60.0, 120.0, 1350.0, 0.5, 0.95, 1790.0, nan, nan]]
     t = bench.per_rank_table(rows)
     assert t[0]["verified"] is True and t[1]["held_clock_ghz"] is None and t[1]["xgmi_read_kb"] is None
-    e = bench.node_energy(t, total_bytes=200 * 10**9)
-    assert e["joules_per_gb"] == pytest.approx(110.0 / 200.0)
+    e = bench.node_energy(t)
+    assert e["joules_per_gb"] == pytest.approx(110.0 / 220.0)  # all joules over all window bytes
     assert e["avg_socket_w_per_gpu"] == pytest.approx(1325.0) and e["ppt_residency_max"] == 0.95
     t[1]["joules"] = None
-    assert bench.node_energy(t, 1)["joules_per_gb"] is None  # one rank unmeasured: no whole-node J/GB
+    assert bench.node_energy(t)["joules_per_gb"] is None  # one rank unmeasured: no whole-node J/GB
 
 
 @pytest.mark.gpu
@@ -157,7 +157,9 @@ def test_bench_json_line(gpu):
     assert x["verified"] is True and x["gbps"] > 100
     assert x["joules"] is not None and x["joules"] > 0, d.get("energy_unavailable")
     assert 100 < x["avg_socket_w"] < 2000 and 0.0 <= x["ppt_residency"] <= 1.0
-    assert d["joules_per_gb"] == pytest.approx(x["joules"] / (3 * nbytes / 1e9), rel=1e-3)
+    assert x["energy_gb"] >= 3 * nbytes / 1e9  # the timed steps, extended to >= 2 s by untimed ones
+    assert d["joules_per_gb"] == pytest.approx(x["joules"] / x["energy_gb"], rel=1e-3)
+    assert d["energy_window_s"] >= 2.0
     assert d["preflight"]["ok"] is True and d["preflight"]["backend"] == "nccl"
     # the reference's own GPU methodology beside pinned and kernel-only, verified
     assert d["refmethod_verified"] is True

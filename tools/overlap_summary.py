@@ -11,7 +11,10 @@ on different streams).  Prints each phase's busy time and, for every pair,
 the time both were busy at once -- the overlap the pipeline was built for
 (csrc/hip/pipeline.cpp: scatter(r+1) | cipher(r) | gather(r-1)).
 
-    python3 tools/overlap_summary.py gpurun_out/trace/x_results.db
+    python3 tools/overlap_summary.py gpurun_out/trace/x_results.db [--together h2d,aes,d2h]
+
+``--together A,B,C`` also prints the time every named phase (kernel phases
+over all their queues) was busy at once: the three-stage overlap.
 """
 import argparse
 import re
@@ -75,6 +78,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--phase", action="append", help="NAME=REGEX (repeatable)")
+    ap.add_argument("--together", default="h2d,aes,d2h", help="comma list of phases; '' to skip")
     a = ap.parse_args(argv)
     phases = [p.split("=", 1) for p in (a.phase or DEFAULT)]
     rows = load(a.db)
@@ -103,7 +107,34 @@ def main(argv=None):
         ov = intersect(merged[x], merged[y])
         small = min(union([tuple(i) for i in merged[x]])[0], union([tuple(i) for i in merged[y]])[0]) or 1
         print(f"{x + ' | ' + y:<44} {ov / 1e6:>10.3f} {100 * ov / small:>12.1f}%")
+    names = [n for n in a.together.split(",") if n]
+    if names:
+        sets = []
+        for n in names:
+            iv = [tuple(i) for k, m in merged.items() if k.split("@")[0] == n for i in m]
+            sets.append(union(iv)[1] if iv else [])
+        acc = sets[0]
+        for other in sets[1:]:
+            acc = intersect_list(acc, other)
+        both = sum(e - s for s, e in acc)
+        small = min(sum(e - s for s, e in x) for x in sets) or 1
+        print(f"\n{' & '.join(names) + ' (all at once)':<44} {both / 1e6:>10.3f} {100 * both / small:>12.1f}%")
     return 0
+
+
+def intersect_list(a, b):
+    """the intervals where both merged interval lists are busy"""
+    i = j = 0
+    out = []
+    while i < len(a) and j < len(b):
+        s, e = max(a[i][0], b[j][0]), min(a[i][1], b[j][1])
+        if e > s:
+            out.append([s, e])
+        if a[i][1] < b[j][1]:
+            i += 1
+        else:
+            j += 1
+    return out
 
 
 if __name__ == "__main__":
