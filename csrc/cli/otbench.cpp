@@ -4,7 +4,7 @@
  * per configuration.
  *
  *   otbench --mode ctr|ecb|ecb-dec|cbc-dec|cbc-enc-seg|cfb-enc-seg|cfb-dec-seg|cfb-dec|ctr-stream|xor|rc4
- *                  |ecb-split|ecbdec-split|cbcdec-split
+ *                  |ecb-split|ecbdec-split|cbcdec-split|cfbdec-split
  *           [--bits 128] [--bytes 1G] [--iters 20] [--warmup 3]
  *           [--impl auto|ttable|bitslice] [--inplace] [--verify] [--clock]
  *           [--mark]                        "OTB_MARK start|end" on stderr around the timed loop
@@ -81,8 +81,13 @@ struct OpArg {
     uint8_t iv[16];
     uint8_t *keys;
     void *sa, *sb; /* *-split: T-table / bitsliced streams */
-    uint8_t prev[16]; /* cbcdec-split: ciphertext block before the bitsliced part */
+    uint8_t prev[16]; /* cbcdec-split / cfbdec-split: ciphertext block before the bitsliced part */
 };
+
+static bool is_split(const std::string &m)
+{
+    return m == "ecb-split" || m == "ecbdec-split" || m == "cbcdec-split" || m == "cfbdec-split";
+}
 
 /* *-split: T-table bytes (the bitsliced part is whole 2048-block tasks, as
  * the library's split) */
@@ -98,7 +103,7 @@ static int run_op(void *p)
     const Cfg &c = *a->c;
     if (c.mode == "ctr") return otc_aes_ctr(a->in, a->out, c.bytes, a->k, a->iv, 0, c.impl, nullptr);
     if (c.mode == "ecb" || c.mode == "ecb-dec") return otc_aes_ecb(a->in, a->out, c.bytes, a->k, c.impl, nullptr);
-    if (c.mode == "ecb-split" || c.mode == "ecbdec-split" || c.mode == "cbcdec-split") {
+    if (is_split(c.mode)) {
         /* both streams are ordered with the default stream (otc_stream_create) */
         const size_t nt = split_nt(c);
         const uint8_t *bi = (const uint8_t *)a->in + nt;
@@ -106,6 +111,10 @@ static int run_op(void *p)
         if (c.mode == "cbcdec-split") {
             if (int r = otc_aes_cbc_decrypt_impl(a->in, a->out, nt, a->k, a->iv, OTC_IMPL_TTABLE, a->sa)) return r;
             return otc_aes_cbc_decrypt_impl(bi, bo, c.bytes - nt, a->k, a->prev, OTC_IMPL_BITSLICE, a->sb);
+        }
+        if (c.mode == "cfbdec-split") {
+            if (int r = otc_aes_cfb128_decrypt_impl(a->in, a->out, nt, a->k, a->iv, OTC_IMPL_TTABLE, a->sa)) return r;
+            return otc_aes_cfb128_decrypt_impl(bi, bo, c.bytes - nt, a->k, a->prev, OTC_IMPL_BITSLICE, a->sb);
         }
         if (int r = otc_aes_ecb(a->in, a->out, nt, a->k, OTC_IMPL_TTABLE, a->sa)) return r;
         return otc_aes_ecb(bi, bo, c.bytes - nt, a->k, OTC_IMPL_BITSLICE, a->sb);
@@ -124,7 +133,7 @@ static int run_op(void *p)
         return otc_aes_cfb128_encrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
     if (c.mode == "cfb-dec-seg")
         return otc_aes_cfb128_decrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
-    if (c.mode == "cfb-dec") return otc_aes_cfb128_decrypt(a->in, a->out, c.bytes, a->k, a->iv, nullptr);
+    if (c.mode == "cfb-dec") return otc_aes_cfb128_decrypt_impl(a->in, a->out, c.bytes, a->k, a->iv, c.impl, nullptr);
     if (c.mode == "xor") return otc_xor(a->in, a->out, a->out, c.bytes, nullptr);
     if (c.mode == "rc4") return otc_rc4_multi(a->keys, (int)c.keylen, c.streams, c.len, c.drop, a->in, a->out, nullptr);
     return OTC_ERR_ARG;
@@ -143,7 +152,10 @@ struct Sample {
 };
 
 static bool is_seg_mode(const std::string &m) { return m == "cbc-enc-seg" || m == "cfb-enc-seg" || m == "cfb-dec-seg"; }
-static bool chained_dec(const std::string &m) { return m == "cbc-dec" || m == "cfb-dec" || m == "cbcdec-split"; }
+static bool chained_dec(const std::string &m)
+{
+    return m == "cbc-dec" || m == "cfb-dec" || m == "cbcdec-split" || m == "cfbdec-split";
+}
 
 /* sample output ranges: head, middle, tail, and the 2^32-byte boundary (32-bit
  * byte-offset overflow) when the buffer is larger than 4 GiB */
@@ -233,10 +245,10 @@ static bool oracle(const Cfg &c, const uint8_t key[32], const uint8_t iv0[16], c
     } else if (m == "ecb-dec" || m == "ecbdec-split") {
         aes_setkey_dec(&ctx, key, c.bits);
         aes_ecb_bulk(&ctx, AES_DECRYPT, in, ref.data(), s.len, 8);
-    } else if (m == "cbc-dec" || m == "cfb-dec" || m == "cbcdec-split") {
+    } else if (chained_dec(m)) {
         uint8_t iv[16];
         memcpy(iv, s.off ? s.in.data() : iv0, 16);
-        if (m != "cfb-dec") {
+        if (m == "cbc-dec" || m == "cbcdec-split") {
             aes_setkey_dec(&ctx, key, c.bits);
             aes_crypt_cbc(&ctx, AES_DECRYPT, s.len, iv, in, ref.data());
         } else {
@@ -353,7 +365,8 @@ int main(int argc, char **argv)
         }
     }
     static const char *modes[] = {"ctr", "ecb", "ecb-dec", "cbc-dec", "cbc-enc-seg", "cfb-enc-seg", "cfb-dec-seg",
-                                  "cfb-dec", "ctr-stream", "xor", "rc4", "ecb-split", "ecbdec-split", "cbcdec-split"};
+                                  "cfb-dec", "ctr-stream", "xor", "rc4", "ecb-split", "ecbdec-split", "cbcdec-split",
+                                  "cfbdec-split"};
     bool known = false;
     for (const char *m : modes) known |= c.mode == m;
     if (!known) {
@@ -450,7 +463,7 @@ int main(int argc, char **argv)
         return (c.verify && v != 1) ? 3 : 0;
     }
 
-    if (c.mode == "ecb-split" || c.mode == "ecbdec-split" || c.mode == "cbcdec-split") {
+    if (is_split(c.mode)) {
         if (!(c.share >= 0.0 && c.share <= 1.0)) {
             fprintf(stderr, "--share must be in [0, 1]\n");
             return 2;
@@ -475,7 +488,8 @@ int main(int argc, char **argv)
         otc_fill_random(a.keys, c.streams * c.keylen, 44, nullptr);
     }
     otc_device_sync();
-    if (c.mode == "cbcdec-split") { /* the bitsliced part's IV: ciphertext block nt/16 - 1 (constant: out of place) */
+    if (c.mode == "cbcdec-split" || c.mode == "cfbdec-split") {
+        /* the bitsliced part's IV: ciphertext block nt/16 - 1 (constant: out of place) */
         const size_t nt = split_nt(c);
         if (nt >= 16) {
             if (otc_memcpy(a.prev, (const uint8_t *)a.in + nt - 16, 16, OTC_D2H)) return 1;

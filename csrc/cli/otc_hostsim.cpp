@@ -152,6 +152,12 @@ int otc_aes_cfb128_decrypt_segments(const void *in, void *out, size_t seg, size_
     return segs(2, in, out, seg, nseg, k, iv0);
 }
 
+int otc_aes_cfb128_decrypt(const void *in, void *out, size_t n, const otc_aes_key *k, const uint8_t iv[16], void *);
+int otc_aes_cfb128_decrypt_impl(const void *in, void *out, size_t n, const otc_aes_key *k, const uint8_t iv[16], int,
+                                void *st)
+{
+    return otc_aes_cfb128_decrypt(in, out, n, k, iv, st);
+}
 int otc_aes_cfb128_decrypt(const void *in, void *out, size_t n, const otc_aes_key *k, const uint8_t iv[16], void *)
 {
     if (in == out) return fail(OTC_ERR_ARG, "cfb decrypt in place");

@@ -73,9 +73,9 @@ struct BsParams {
     const uint32_t *e1tab; /* CTR counter caching: E1 plane words per task */
     uint64_t tasks;       /* 2048-block tasks of the call */
     uint32_t part;        /* BS_FULL_ONLY or BS_EDGE_ONLY */
-    uint32_t has_prev;    /* CBC decrypt: the 16 bytes before `in` are block 0's predecessor (a split's
-                             second part); otherwise block 0 XORs with iv */
-    uint32_t iv[4];       /* CBC decrypt: IV as LE words */
+    uint32_t has_prev;    /* CBC / CFB decrypt: the 16 bytes before `in` are block 0's predecessor (a
+                             split's second part); otherwise block 0's predecessor is iv */
+    uint32_t iv[4];       /* CBC / CFB decrypt: IV as LE words */
 };
 
 /* Which tasks a launch runs.  The bulk launch (BS_FULL_ONLY) takes only tasks
@@ -87,10 +87,26 @@ struct BsParams {
 enum : uint32_t { BS_FULL_ONLY = 1, BS_EDGE_ONLY = 2 };
 
 /* BS_ECB: ECB encryption; BS_ECB_DEC / BS_CBC_DEC: the inverse cipher through
- * the forward S-box (S^-1 = L S L, otc_invmix.h) with a decryption key */
-enum : int { BS_CTR = 0, BS_ECB = 1, BS_ECB_DEC = 2, BS_CBC_DEC = 3 };
+ * the forward S-box (S^-1 = L S L, otc_invmix.h) with a decryption key;
+ * BS_CFB_DEC: CFB128 decryption, P_i = E(C_{i-1}) ^ C_i -- the forward cipher
+ * on the input shifted back one block, XORed with the input */
+enum : int { BS_CTR = 0, BS_ECB = 1, BS_ECB_DEC = 2, BS_CBC_DEC = 3, BS_CFB_DEC = 4 };
 
 __device__ __forceinline__ W lane_mask(uint32_t lane, int n) { return (W)(0u - ((lane >> n) & 1u)); }
+
+/* v, or the IV where `first`: an explicit per-word blend after an unconditional
+ * load from a valid address -- written as a select of the IV and the loaded
+ * block, hipcc made a 16-byte private copy of the IV and loaded through a
+ * pointer select (scratch traffic in every task) */
+__device__ __forceinline__ uint4 blend_iv(uint4 v, bool first, const BsParams &P)
+{
+    const uint32_t m = 0u - (uint32_t)first;
+    v.x = (v.x & ~m) | (P.iv[0] & m);
+    v.y = (v.y & ~m) | (P.iv[1] & m);
+    v.z = (v.z & ~m) | (P.iv[2] & m);
+    v.w = (v.w & ~m) | (P.iv[3] & m);
+    return v;
+}
 
 /* Task geometry shared by both kernels. */
 struct Task {
@@ -124,16 +140,28 @@ __device__ __forceinline__ bool task_of(const BsParams &P, Task &t)
 
 /* ECB input: load 32 blocks (uniform task base + 32-bit lane offsets: 64-bit
  * per-slot addresses would be CSE'd with the stores and kept live across the
- * rounds) and transpose each word column into 32 planes */
+ * rounds) and transpose each word column into 32 planes.  CFB decryption
+ * enciphers the block before each output block: the same loads one block back,
+ * with the IV in front of block 0 of a whole-stream call. */
+template <int MODE>
 __device__ __forceinline__ void ecb_load_planes(const BsParams &P, const Task &t, W *s, bool full)
 {
-    const uint8_t *tb = P.in + t.vbase * 16;
+    constexpr int64_t BACK = MODE == BS_CFB_DEC ? 16 : 0;
+    const uint8_t *tb = P.in + (int64_t)(t.vbase * 16) - BACK;
     const uint32_t lo = t.lane * 16u;
     uint4 blk[32];
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
         const uint64_t i = t.vbase + t.lane + 64u * k;
-        blk[k] = (full || i < P.nblocks) ? *(const uint4 *)(tb + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
+        if (MODE == BS_CFB_DEC && k == 0) {
+            /* only slot 0 of lane 0 of task 0 can be block 0: it loads block 0
+             * itself (a valid address) and takes the IV instead */
+            const bool first = !P.has_prev && i == 0;
+            const uint8_t *src = P.in + (int64_t)(t.vbase * 16) + lo - (first ? 0 : 16);
+            blk[k] = blend_iv((full || i < P.nblocks) ? *(const uint4 *)src : make_uint4(0, 0, 0, 0), first, P);
+        } else {
+            blk[k] = (full || i < P.nblocks) ? *(const uint4 *)(tb + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
+        }
     }
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -275,6 +303,9 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
  * 81-LUT S-box (27 live planes at its peak) 4 early slots spilled in the
  * output phase; with the 79-LUT one (24) they no longer spill but measured
  * 1-1.5% slower, profiles/r3/sbox79; the 77-LUT one peaks at 23) */
+#ifndef OTC_BS_CFB_D
+#define OTC_BS_CFB_D 2
+#endif
 #ifndef OTC_BS_PRE
 #define OTC_BS_PRE 2
 #endif
@@ -363,7 +394,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
 #pragma unroll
         for (int q = 0; q < 128; ++q) asm volatile("" : "+v"(s[q]));
     } else {
-        ecb_load_planes(P, t, s, full);
+        ecb_load_planes<MODE>(P, t, s, full);
     }
     constexpr bool DEC = MODE == BS_ECB_DEC || MODE == BS_CBC_DEC;
     if (DEC) {
@@ -392,21 +423,29 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
      * store -- vmcnt is in order on gfx9, so such a load would also wait for
      * the stores */
     /* the block XORed into the output: CTR the plaintext, CBC decrypt the
-     * previous ciphertext block (the IV for block 0 of a whole-stream call) */
-    constexpr bool XIN = MODE == BS_CTR || MODE == BS_CBC_DEC;
+     * previous ciphertext block (the IV for block 0 of a whole-stream call),
+     * CFB decrypt the ciphertext block itself */
+    constexpr bool XIN = MODE == BS_CTR || MODE == BS_CBC_DEC || MODE == BS_CFB_DEC;
     constexpr int XOFF = MODE == BS_CBC_DEC ? -16 : 0;
     uint4 pt[32];
     auto issue = [&](int j) {
         if (XIN && j >= LS && j < 32) {
-            if (MODE == BS_CBC_DEC && !P.has_prev && tstart + lane + 64 * j == 0)
-                pt[j] = make_uint4(P.iv[0], P.iv[1], P.iv[2], P.iv[3]);
-            else
+            if (MODE == BS_CBC_DEC && j == 0) {
+                /* block 0 of a whole-stream call XORs with the IV: it loads
+                 * itself (a valid address) and blends the IV in */
+                const bool first = !P.has_prev && tstart + lane == 0;
+                const uint4 v = slot_ok(j) ? *(const uint4 *)(ib + lo + (first ? 0 : XOFF)) : make_uint4(0, 0, 0, 0);
+                pt[j] = blend_iv(v, first, P);
+            } else {
                 pt[j] = slot_ok(j) ? *(const uint4 *)(ib + lo + 1024u * j + XOFF) : make_uint4(0, 0, 0, 0);
+            }
         }
     };
-    /* CBC decrypt: its 125-node linear layer leaves fewer registers for the
-     * output phase -- previous-block loads 4 slots ahead, none early */
-    constexpr int PRE_ = MODE == BS_CBC_DEC ? 0 : PRE, D_ = MODE == BS_CBC_DEC ? 4 : D;
+    /* CBC / CFB decrypt load all 32 XOR blocks into registers (CTR stages 8 in
+     * LDS): few slots ahead (CBC 4, CFB 2: 163 VGPRs, no scratch; 4 spills),
+     * none early, or the output phase spills */
+    constexpr bool REG_XIN = MODE == BS_CBC_DEC || MODE == BS_CFB_DEC;
+    constexpr int PRE_ = REG_XIN ? 0 : PRE, D_ = MODE == BS_CFB_DEC ? OTC_BS_CFB_D : REG_XIN ? 4 : D;
 #pragma unroll
     for (int j = 0; j < LS + PRE_; ++j) issue(j);
     sched_fence();
@@ -615,6 +654,21 @@ hipError_t bs_cbc_decrypt(const void *in, void *out, uint64_t nblocks, const otc
     P.has_prev = has_prev ? 1u : 0u;
     for (int i = 0; i < 4; ++i) P.iv[i] = iv_le ? iv_le[i] : 0u;
     return launch<BS_CBC_DEC>(P, K, st);
+}
+
+/* CFB128 decryption with the ENCRYPTION schedule: block i = E(block i-1 of
+ * `in`) ^ block i; block 0's predecessor is iv_le or -- has_prev -- the 16
+ * bytes before `in`.  in != out. */
+hipError_t bs_cfb_decrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, const uint32_t iv_le[4],
+                          bool has_prev, hipStream_t st)
+{
+    BsParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nblocks = nblocks;
+    P.has_prev = has_prev ? 1u : 0u;
+    for (int i = 0; i < 4; ++i) P.iv[i] = iv_le ? iv_le[i] : 0u;
+    return launch<BS_CFB_DEC>(P, K, st);
 }
 
 } // namespace otc_impl

@@ -54,6 +54,7 @@ hipError_t xor_small(const void *, void *, uint32_t, const uint8_t *, hipStream_
 hipError_t bs_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
 hipError_t bs_ecb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
 hipError_t bs_cbc_decrypt(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, bool, hipStream_t);
+hipError_t bs_cfb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, bool, hipStream_t);
 hipError_t tt_ctr_batch(const otc_ctr_msg *, const otc_aes_key *, const uint32_t *, const uint64_t *, uint64_t, int, int,
                         hipStream_t);
 hipError_t k_xor(const void *, const void *, void *, size_t, hipStream_t);
@@ -241,6 +242,9 @@ size_t ecb_split_min(int bits) { return bits == 256 ? ((size_t)1 << 30) : ((size
  * encryption's VALU work (L o InvMixColumns o L: 121 nodes per column vs
  * MixColumns' 55), so it takes a smaller share */
 double dec_split_share(int bits, bool cbc) { return (!cbc && bits == 256) ? 0.2 : 0.15; }
+/* CFB128 decryption: the bitsliced forward cipher plus a second input load per
+ * block (profiles/r4/cfb_split: 0.2 beat 0.25-0.35 at 4 and 32 GiB) */
+double cfb_split_share(int) { return 0.2; }
 size_t dec_split_min(int) { return (size_t)1 << 30; }
 
 int pick_ecb_impl(int impl, int bits, size_t nbytes)
@@ -316,6 +320,22 @@ hipError_t cbc_dec_split(const void *in, void *out, uint64_t nblocks, const otc_
         });
 }
 
+/* CFB128 decryption enciphers the previous ciphertext block: ECB encryption's
+ * work plus one more input load per block */
+hipError_t cfb_dec_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, const uint32_t ivw[4],
+                         hipStream_t st, int *ran)
+{
+    const uint8_t *pi = (const uint8_t *)in;
+    uint8_t *po = (uint8_t *)out;
+    return split_run(
+        nblocks, cfb_split_share(K.bits), st, ran,
+        [&](uint64_t nt) { return otc_impl::tt_cfb_decrypt(pi, po, nt, K, ivw, st); },
+        /* the bitsliced part's block 0 enciphers block nt-1 of the input */
+        [&](uint64_t nt, uint64_t nb, hipStream_t s) {
+            return otc_impl::bs_cfb_decrypt(pi + 16 * nt, po + 16 * nt, nb, K, nullptr, true, s);
+        });
+}
+
 /* the kernel family the calling thread's last AES call ran (otc_last_impl) */
 thread_local int g_last_impl = OTC_IMPL_AUTO;
 
@@ -364,11 +384,11 @@ extern "C" int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, in
     return OTC_OK;
 }
 
-/* mode: 1 CTR, 0 ECB encryption, 2 decryption (ECB / CBC) */
+/* mode: 1 CTR, 0 ECB encryption, 2 decryption (ECB / CBC), 3 CFB decryption */
 extern "C" int otc_pick_impl(int impl, int bits, int mode, uint64_t nbytes)
 {
     if (check_impl(impl)) return -1;
-    if (mode == 0) return pick_ecb_impl(impl, bits, (size_t)nbytes);
+    if (mode == 0 || mode == 3) return pick_ecb_impl(impl, bits, (size_t)nbytes);
     if (mode == 2) return pick_dec_impl(impl, bits, (size_t)nbytes);
     return pick_impl(impl, bits, (size_t)nbytes);
 }
@@ -671,8 +691,8 @@ extern "C" int otc_aes_cfb128_decrypt_segments(const void *in, void *out, size_t
     return cfb_seg_common(in, out, seg_bytes, nseg, k, iv0, stream, true, "cfb128_decrypt_segments");
 }
 
-extern "C" int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
-                                      const uint8_t iv[16], void *stream)
+extern "C" int otc_aes_cfb128_decrypt_impl(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                                           const uint8_t iv[16], int impl, void *stream)
 {
     Range rg("otc_aes_cfb128_decrypt");
     int r = check_key(k, OTC_DIR_ENCRYPT);
@@ -680,12 +700,27 @@ extern "C" int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, 
     if (nbytes % 16) return set_err(OTC_ERR_ARG, "CFB128 device path needs a multiple of 16 bytes");
     if (!iv) return set_err(OTC_ERR_ARG, "null iv");
     if ((r = check_bufs(in, out, nbytes, nbytes <= 16, "aes_cfb128_decrypt"))) return r;
+    if ((r = check_impl(impl))) return r;
     if (nbytes == 0) return OTC_OK;
     uint32_t ivw[4];
-    memcpy(ivw, iv, 16);
-    hipError_t e = otc_impl::tt_cfb_decrypt(in, out, nbytes / 16, *k, ivw, (hipStream_t)stream);
+    memcpy(ivw, iv, 16); /* LE words of the IV bytes, as both kernels load blocks */
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    g_last_impl = pick_ecb_impl(impl, k->bits, nbytes);
+    if (g_last_impl == OTC_IMPL_SPLIT)
+        e = cfb_dec_split(in, out, nbytes / 16, *k, ivw, st, &g_last_impl);
+    else if (g_last_impl == OTC_IMPL_BITSLICE)
+        e = otc_impl::bs_cfb_decrypt(in, out, nbytes / 16, *k, ivw, false, st);
+    else
+        e = otc_impl::tt_cfb_decrypt(in, out, nbytes / 16, *k, ivw, st);
     if (e != hipSuccess) return hip_fail(e, "cfb_decrypt launch");
     return OTC_OK;
+}
+
+extern "C" int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                                      const uint8_t iv[16], void *stream)
+{
+    return otc_aes_cfb128_decrypt_impl(in, out, nbytes, k, iv, OTC_IMPL_AUTO, stream);
 }
 
 extern "C" int otc_xor(const void *a, const void *b, void *out, size_t nbytes, void *stream)

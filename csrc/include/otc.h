@@ -59,17 +59,17 @@ int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 
 /* ---- implementation selection ------------------------------------------- */
 #define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for CTR calls >= 2 GiB (AES-256:
-                               >= 1 GiB), the split below for ECB / CBC-decrypt >= 1 GiB, T-table otherwise
+                               >= 1 GiB), the split below for ECB / CBC / CFB decrypt >= 1 GiB, T-table otherwise
                                (OTC_IMPL=ttable|bitslice|split env overrides for the whole process) */
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
 #define OTC_IMPL_BITSLICE 2 /* 32-block-per-lane bitsliced VALU kernel */
-#define OTC_IMPL_SPLIT 3    /* ECB and CBC-decrypt: both kernels CONCURRENTLY on disjoint ranges (the bitsliced
+#define OTC_IMPL_SPLIT 3    /* ECB, CBC-decrypt and CFB-decrypt: both kernels CONCURRENTLY on disjoint ranges (the bitsliced
                                one on an auxiliary stream), co-resident on every CU -- LDS and VALU busy at
                                once; "auto" for these calls >= 1 GiB.  CTR: as auto */
 
 /* The kernel family `impl` resolves to for a call of nbytes with a bits-bit
- * key (mode 1: CTR, 0: ECB encryption, 2: ECB / CBC decryption); -1 for an
- * invalid impl. */
+ * key (mode 1: CTR, 0: ECB encryption, 2: ECB / CBC decryption, 3: CFB128
+ * decryption); -1 for an invalid impl. */
 int otc_pick_impl(int impl, int bits, int mode, uint64_t nbytes);
 /* OTC_IMPL_TTABLE / OTC_IMPL_BITSLICE: what the calling thread's last
  * otc_aes_ctr / otc_aes_ecb call ran (OTC_IMPL_AUTO before any call). */
@@ -130,7 +130,6 @@ int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t seg_bytes, si
 int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                  const otc_aes_key *k, const uint8_t iv0[16], void *stream);
 
-/* CFB128 decryption (parallel): P_i = C_i ^ E(C_{i-1}); nbytes % 16 == 0. */
 /* CFB128 over nseg independent segments of seg_bytes (multiple of 16) with
  * IV_s = iv0 + s (128-bit BE add) -- the parallel form of the serial CFB
  * chain, like otc_aes_cbc_encrypt_segments.  Encryption keys for both
@@ -140,8 +139,14 @@ int otc_aes_cfb128_encrypt_segments(const void *in, void *out, size_t seg_bytes,
 int otc_aes_cfb128_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                     const otc_aes_key *k, const uint8_t iv0[16], void *stream);
 
+/* CFB128 decryption (parallel): P_i = C_i ^ E(C_{i-1}), C_{-1} = iv;
+ * nbytes % 16 == 0; encryption key.  _impl: with a kernel choice (the plain
+ * form is OTC_IMPL_AUTO: the T-table + bitsliced split from 1 GiB, like ECB
+ * encryption). */
 int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
                            const uint8_t iv[16], void *stream);
+int otc_aes_cfb128_decrypt_impl(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
+                                const uint8_t iv[16], int impl, void *stream);
 
 /* ---- batched CTR: many independent messages in ONE launch -----------------
  * The serving shape (packets, sectors, objects of a few KiB, each with its own

@@ -62,7 +62,7 @@ class AES:
 
     def decrypt(self, data, out=None):
         if isinstance(data, torch.Tensor):
-            return ops.ecb_decrypt(data, self._key, out=out)
+            return ops.ecb_decrypt(data, self._key, out=out, impl=self.impl)
         return cpu_ref.ecb(self._key, data, decrypt=True)
 
     # ---- modes -------------------------------------------------------------
@@ -101,7 +101,7 @@ class AES:
         if isinstance(data, torch.Tensor):
             if segment_bytes:
                 return ops.cbc_decrypt_segments(data, self._key, iv, segment_bytes, out=out)
-            return ops.cbc_decrypt(data, self._key, iv, out=out)
+            return ops.cbc_decrypt(data, self._key, iv, out=out, impl=self.impl)
         if segment_bytes:
             return cpu_ref.cbc_segments(self._key, iv, data, segment_bytes, decrypt=True)
         return cpu_ref.cbc(self._key, iv, data, decrypt=True)
@@ -110,7 +110,7 @@ class AES:
         if isinstance(data, torch.Tensor):
             if segment_bytes:
                 return ops.cfb128_decrypt_segments(data, self._key, iv, segment_bytes, out=out)
-            return ops.cfb128_decrypt(data, self._key, iv, out=out)
+            return ops.cfb128_decrypt(data, self._key, iv, out=out, impl=self.impl)
         if segment_bytes:
             return cpu_ref.cfb128_segments(self._key, iv, data, segment_bytes, decrypt=True)
         return cpu_ref.cfb128(self._key, iv, data, decrypt=True)

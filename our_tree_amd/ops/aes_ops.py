@@ -31,12 +31,12 @@ def _impl(impl) -> int:
 _IMPL_NAMES = {v: k for k, v in IMPLS.items()}
 
 
-_PICK_MODES = {"ctr": 1, "ecb": 0, "dec": 2, "ecb-dec": 2, "cbc-dec": 2}
+_PICK_MODES = {"ctr": 1, "ecb": 0, "dec": 2, "ecb-dec": 2, "cbc-dec": 2, "cfb-dec": 3}
 
 
 def pick_impl(impl="auto", bits: int = 128, mode: str = "ctr", nbytes: int = 0) -> str:
     """The kernel family ``impl`` resolves to for a ``mode`` call ("ctr",
-    "ecb" = ECB encryption, "dec" = ECB / CBC decryption) of ``nbytes`` with
+    "ecb" = ECB encryption, "dec" = ECB / CBC decryption, "cfb-dec") of ``nbytes`` with
     a ``bits``-bit key (the native routing rule)."""
     if mode not in _PICK_MODES:
         raise ValueError(f"mode must be one of {list(_PICK_MODES)}")
@@ -528,13 +528,17 @@ def cbc_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes:
     return out
 
 
-def cfb128_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None) -> torch.Tensor:
+def cfb128_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None, impl="auto") -> torch.Tensor:
+    """Parallel CFB128 decryption, P_i = C_i ^ E(C_{i-1}) (encryption key).
+    ``impl``: "ttable", "bitslice" (the forward bitsliced cipher on the input
+    shifted one block), "split" (both at once, as ECB encryption) or "auto"
+    (split from 1 GiB).  In place runs through a copy of the input."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     k = expand_key(key)
     with torch.cuda.device(x.device):
-        rc = _run(x, out, lambda ip, op: _lib().otc_aes_cfb128_decrypt(ip, op, _nbytes(x), ctypes.byref(k), _b16(iv, "iv"),
-            _stream(x)), inplace_ok=False)
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_cfb128_decrypt_impl(ip, op, _nbytes(x), ctypes.byref(k),
+            _b16(iv, "iv"), _impl(impl), _stream(x)), inplace_ok=False)
     _native.check(rc, "otc_aes_cfb128_decrypt")
     return out
 

@@ -46,7 +46,12 @@ class PowerMeter:
     this GPU -- no driver in the container, permissions -- and the caller
     reports that instead of numbers."""
 
-    def __init__(self, hip_index: int = 0, sample_s: float = 0.05):
+    def __init__(self, hip_index: int = 0, sample_s: float = 0.05, torch_bdf: bool = True):
+        """torch_bdf: find the GPU by the PCI address torch reports for HIP
+        device ``hip_index`` (imports torch and initialises HIP: seconds in a
+        fresh process); False: the amdsmi handle of the same index (right when
+        no device is hidden from HIP, e.g. a watcher process beside a
+        benchmark that owns the GPU)."""
         self.hip_index = hip_index
         self.sample_s = sample_s
         self.reason = ""
@@ -59,7 +64,7 @@ class PowerMeter:
             amdsmi.amdsmi_init()
             self._smi = amdsmi
             handles = amdsmi.amdsmi_get_processor_handles()
-            want = _bdf_of_torch_device(hip_index)
+            want = _bdf_of_torch_device(hip_index) if torch_bdf else None
             if want is not None:
                 for h in handles:
                     if amdsmi.amdsmi_get_gpu_device_bdf(h).lower().startswith(want):

@@ -551,6 +551,35 @@ def test_bitsliced_decrypt_matches_ttable(gpu, bits):
     assert ops.pick_impl("auto", bits, "dec", (1 << 30) - 16) == "ttable"
 
 
+@pytest.mark.parametrize("bits", [128, 192, 256])
+def test_bitsliced_cfb_decrypt_matches_ttable(gpu, bits):
+    """Bitsliced CFB128 decryption (the forward cipher on the input shifted one
+    block back, the IV in front of block 0) and the CFB split (its bitsliced
+    part enciphers block nt-1 of the input) equal the T-table kernel and the
+    CPU oracle, on sizes with partial first / last bitsliced tasks, a single
+    block and a size that splits."""
+    for n in (16, 16 * 2048 * 9 + 16 * 77, 16 * 100, 16 * 2048 * 40 + 16, 96 << 20):
+        key = os.urandom(bits // 8)
+        iv = os.urandom(16)
+        x = torch.empty(n, dtype=torch.uint8, device=gpu)
+        ops.fill_random_(x, seed=n ^ bits ^ 7)
+        t = ops.cfb128_decrypt(x, key, iv, impl="ttable")
+        for impl in ("bitslice", "split"):
+            y = ops.cfb128_decrypt(x, key, iv, impl=impl)
+            torch.cuda.synchronize()
+            assert torch.equal(y, t), ("cfb", impl, bits, n)
+        w = x.clone()
+        ops.cfb128_decrypt(w, key, iv, out=w, impl="bitslice")  # in place: through a copy
+        torch.cuda.synchronize()
+        assert torch.equal(w, t), ("cfb in place", bits, n)
+        S = min(n, 1 << 14)
+        assert host(t[:S]) == cpu_ref.cfb128(key, iv, host(x[:S]), decrypt=True)
+        if n > S:  # the tail, with its predecessor block as the IV
+            assert host(t[-S:]) == cpu_ref.cfb128(key, host(x[-S - 16:-S]), host(x[-S:]), decrypt=True)
+    assert ops.pick_impl("auto", bits, "cfb-dec", 1 << 30) == "split"
+    assert ops.pick_impl("auto", bits, "cfb-dec", (1 << 30) - 16) == "ttable"
+
+
 def test_ttable_modes_beyond_4gib(gpu):
     """T-table ECB encrypt / decrypt, CBC and CFB128 decrypt on a buffer
     above 4 GiB, checked against the oracle on samples at the head, across

@@ -33,13 +33,14 @@ def counts():
 
 
 def test_every_bulk_kernel_found(counts):
-    for mode in ("CTR", "ECB", "ECB-dec", "CBC-dec"):
+    for mode in ("CTR", "ECB", "ECB-dec", "CBC-dec", "CFB-dec"):
         for bits in ("AES-128", "AES-192", "AES-256"):
             assert (mode, bits) in counts, (mode, bits, sorted(counts))
 
 
 def test_bulk_kernels_spill_free(counts):
-    """Encryption kernels: no scratch at all.  The decryption kernels (L o
+    """Encryption kernels (CFB decryption runs the forward cipher): no scratch
+    at all.  The inverse-cipher kernels (L o
     InvMixColumns o L is 125 nodes per column against MixColumns' 55) keep a
     few 64-bit addresses in scratch across the rounds: at most 24 scratch
     instructions per 2048-block task (beside ~26k VALU), none in the rounds

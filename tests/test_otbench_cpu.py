@@ -17,13 +17,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "bin", "otbench_hostsim")
 
 MODES = ["ctr", "ecb", "ecb-dec", "cbc-dec", "cfb-dec", "cbc-enc-seg", "cfb-enc-seg", "cfb-dec-seg",
-         "ctr-stream", "xor", "rc4", "ecb-split", "ecbdec-split", "cbcdec-split"]
-NO_INPLACE = {"cbc-dec", "cfb-dec", "cfb-dec-seg", "cbcdec-split"}
+         "ctr-stream", "xor", "rc4", "ecb-split", "ecbdec-split", "cbcdec-split", "cfbdec-split"]
+NO_INPLACE = {"cbc-dec", "cfb-dec", "cfb-dec-seg", "cbcdec-split", "cfbdec-split"}
 
 
 @pytest.fixture(scope="module", autouse=True)
 def built():
-    subprocess.run(["make", "-C", ROOT, "-s", "bin/otbench_hostsim"], check=True, capture_output=True)
+    # one make at a time (pytest-xdist workers each run this fixture; two
+    # concurrent links of the same binary race)
+    import fcntl
+
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    with open(os.path.join(ROOT, "build", ".hostsim.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-C", ROOT, "-s", "bin/otbench_hostsim"], check=True, capture_output=True)
 
 
 def run(*args):

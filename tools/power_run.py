@@ -8,9 +8,14 @@ power, clocks and PPT residency over exactly its timed loop.
 otbench prints ``OTB_MARK start`` / ``OTB_MARK end`` on stderr around its
 timed loop; the meter (our_tree_amd/utils/power.py, amdsmi in process) is
 started / stopped on those lines.  The child is started FIRST, before this
-process touches amdsmi, and nothing here initialises HIP.  Prints otbench's
-JSON line extended with ``power`` (joules, avg_socket_w, ppt_residency,
-gfxclk_mhz_*) and ``joules_per_gb`` (energy / bytes processed in the loop).
+process touches amdsmi, and nothing here initialises HIP: the meter finds the
+GPU by amdsmi index, not through torch (importing torch and initialising HIP
+here took longer than a 4-32 GiB otbench needs to reach its loop, so the start
+line was read up to 1.3 s late and the energy window missed the loop's first
+second).  Prints otbench's JSON line extended with ``power`` (joules,
+avg_socket_w, ppt_residency, gfxclk_mhz_*), ``joules_per_gb`` (energy / bytes
+processed in the loop) and ``window_vs_loop`` (marks wall time / the loop's
+GPU time: a window that missed part of the loop reads < 0.97 and is flagged).
 Exit code: otbench's.
 """
 import argparse
@@ -37,7 +42,7 @@ def main():
 
     from our_tree_amd.utils.power import PowerMeter
 
-    meter = PowerMeter(a.gpu, sample_s=a.sample_s)
+    meter = PowerMeter(a.gpu, sample_s=a.sample_s, torch_bdf=False)
     stats = {"available": False, "reason": "no OTB_MARK lines (run otbench with --mark)"}
     err_tail = []
     t_start = None
@@ -69,6 +74,12 @@ def main():
     if stats.get("available") and d.get("bytes") and d.get("iters"):
         gb = d["bytes"] * d["iters"] / 1e9
         d["joules_per_gb"] = round(stats["joules"] / gb, 4)
+        loop_s = d["iters"] * d.get("ms", 0) / 1e3
+        if marks_s and loop_s > 0:
+            d["window_vs_loop"] = round(marks_s / loop_s, 4)
+            if d["window_vs_loop"] < 0.97:
+                d["window_short"] = True  # joules_per_gb undercounts; avg_socket_w / gbps stands
+                print(f"power_run: window {marks_s:.3f} s < loop {loop_s:.3f} s", file=sys.stderr)
     print(json.dumps(d), flush=True)
     return rc
 
