@@ -4,7 +4,7 @@
  * per configuration.
  *
  *   otbench --mode ctr|ecb|ecb-dec|cbc-dec|cbc-enc-seg|cfb-enc-seg|cfb-dec-seg|cfb-dec|ctr-stream|xor|rc4
- *                  |ecb-split|ecbdec-split|cbcdec-split|cfbdec-split
+ *                  |ecb-split|ecbdec-split|cbcdec-split|cfbdec-split|ctr-split
  *           [--bits 128] [--bytes 1G] [--iters 20] [--warmup 3]
  *           [--impl auto|ttable|bitslice] [--inplace] [--verify] [--clock]
  *           [--mark]                        "OTB_MARK start|end" on stderr around the timed loop
@@ -86,7 +86,7 @@ struct OpArg {
 
 static bool is_split(const std::string &m)
 {
-    return m == "ecb-split" || m == "ecbdec-split" || m == "cbcdec-split" || m == "cfbdec-split";
+    return m == "ecb-split" || m == "ecbdec-split" || m == "cbcdec-split" || m == "cfbdec-split" || m == "ctr-split";
 }
 
 /* *-split: T-table bytes (the bitsliced part is whole 2048-block tasks, as
@@ -111,6 +111,10 @@ static int run_op(void *p)
         if (c.mode == "cbcdec-split") {
             if (int r = otc_aes_cbc_decrypt_impl(a->in, a->out, nt, a->k, a->iv, OTC_IMPL_TTABLE, a->sa)) return r;
             return otc_aes_cbc_decrypt_impl(bi, bo, c.bytes - nt, a->k, a->prev, OTC_IMPL_BITSLICE, a->sb);
+        }
+        if (c.mode == "ctr-split") { /* the bitsliced part continues the counter at block nt/16 */
+            if (int r = otc_aes_ctr(a->in, a->out, nt, a->k, a->iv, 0, OTC_IMPL_TTABLE, a->sa)) return r;
+            return otc_aes_ctr(bi, bo, c.bytes - nt, a->k, a->iv, nt / 16, OTC_IMPL_BITSLICE, a->sb);
         }
         if (c.mode == "cfbdec-split") {
             if (int r = otc_aes_cfb128_decrypt_impl(a->in, a->out, nt, a->k, a->iv, OTC_IMPL_TTABLE, a->sa)) return r;
@@ -220,7 +224,7 @@ static bool oracle(const Cfg &c, const uint8_t key[32], const uint8_t iv0[16], c
     const uint8_t *in = s.in.data() + s.pre;
     aes_context ctx;
     const std::string &m = c.mode;
-    if (m == "ctr") {
+    if (m == "ctr" || m == "ctr-split") {
         aes_setkey_enc(&ctx, key, c.bits);
         uint8_t nc[16];
         memcpy(nc, iv0, 16);
@@ -366,7 +370,7 @@ int main(int argc, char **argv)
     }
     static const char *modes[] = {"ctr", "ecb", "ecb-dec", "cbc-dec", "cbc-enc-seg", "cfb-enc-seg", "cfb-dec-seg",
                                   "cfb-dec", "ctr-stream", "xor", "rc4", "ecb-split", "ecbdec-split", "cbcdec-split",
-                                  "cfbdec-split"};
+                                  "cfbdec-split", "ctr-split"};
     bool known = false;
     for (const char *m : modes) known |= c.mode == m;
     if (!known) {

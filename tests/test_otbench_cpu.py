@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "bin", "otbench_hostsim")
 
 MODES = ["ctr", "ecb", "ecb-dec", "cbc-dec", "cfb-dec", "cbc-enc-seg", "cfb-enc-seg", "cfb-dec-seg",
-         "ctr-stream", "xor", "rc4", "ecb-split", "ecbdec-split", "cbcdec-split", "cfbdec-split"]
+         "ctr-stream", "xor", "rc4", "ecb-split", "ecbdec-split", "cbcdec-split", "cfbdec-split", "ctr-split"]
 NO_INPLACE = {"cbc-dec", "cfb-dec", "cfb-dec-seg", "cbcdec-split", "cfbdec-split"}
 
 
