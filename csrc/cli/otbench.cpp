@@ -104,8 +104,15 @@ static int run_op(void *p)
     if (c.mode == "ctr") return otc_aes_ctr(a->in, a->out, c.bytes, a->k, a->iv, 0, c.impl, nullptr);
     if (c.mode == "ecb" || c.mode == "ecb-dec") return otc_aes_ecb(a->in, a->out, c.bytes, a->k, c.impl, nullptr);
     if (is_split(c.mode)) {
-        /* both streams are ordered with the default stream (otc_stream_create) */
+        /* both streams are ordered with the default stream (otc_stream_create);
+         * each call ends with a join (otc_stream_join), as the library's split
+         * does -- without it the two parts of successive calls drift apart and
+         * a badly balanced share hides its tail (profiles/r4/split_trace) */
         const size_t nt = split_nt(c);
+        struct Join {
+            const OpArg *a;
+            ~Join() { (void)otc_stream_join(a->sa, a->sb); }
+        } join{a};
         const uint8_t *bi = (const uint8_t *)a->in + nt;
         uint8_t *bo = (uint8_t *)a->out + nt;
         if (c.mode == "cbcdec-split") {

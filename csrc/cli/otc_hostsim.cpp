@@ -209,6 +209,7 @@ int otc_memcpy(void *d, const void *s, size_t n, int) { memcpy(d, s, n); return 
 int otc_device_sync(void) { return OTC_OK; }
 void *otc_stream_create(void) { return (void *)1; }
 void otc_stream_destroy(void *) {}
+int otc_stream_join(void *, void *) { return OTC_OK; }
 
 int otc_time_op(otc_op_fn op, void *arg, int iters, double *ms)
 {

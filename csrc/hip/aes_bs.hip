@@ -76,6 +76,7 @@ struct BsParams {
     uint32_t has_prev;    /* CBC / CFB decrypt: the 16 bytes before `in` are block 0's predecessor (a
                              split's second part); otherwise block 0's predecessor is iv */
     uint32_t iv[4];       /* CBC / CFB decrypt: IV as LE words */
+    SplitClaim cl;        /* k_aes_bs_claim: units taken from the front of the buffer */
 };
 
 /* Which tasks a launch runs.  The bulk launch (BS_FULL_ONLY) takes only tasks
@@ -86,11 +87,7 @@ struct BsParams {
  * runs the first and the last task (wave 0 / wave 1) if they are partial. */
 enum : uint32_t { BS_FULL_ONLY = 1, BS_EDGE_ONLY = 2 };
 
-/* BS_ECB: ECB encryption; BS_ECB_DEC / BS_CBC_DEC: the inverse cipher through
- * the forward S-box (S^-1 = L S L, otc_invmix.h) with a decryption key;
- * BS_CFB_DEC: CFB128 decryption, P_i = E(C_{i-1}) ^ C_i -- the forward cipher
- * on the input shifted back one block, XORed with the input */
-enum : int { BS_CTR = 0, BS_ECB = 1, BS_ECB_DEC = 2, BS_CBC_DEC = 3, BS_CFB_DEC = 4 };
+/* the modes BS_CTR .. BS_CFB_DEC: otc_device.h (engine.cpp names them too) */
 
 __device__ __forceinline__ W lane_mask(uint32_t lane, int n) { return (W)(0u - ((lane >> n) & 1u)); }
 
@@ -116,16 +113,25 @@ struct Task {
 };
 
 template <int MODE>
-__device__ __forceinline__ bool task_of(const BsParams &P, Task &t)
+__device__ __forceinline__ bool task_of(const BsParams &P, Task &t, int64_t claimed)
 {
-    t.lane = threadIdx.x & 63u;
-    t.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (claimed >= 0) {
+        /* k_aes_bs_claim loops over tasks: the lane from mbcnt, opaque per
+         * task, keeps hipcc from hoisting lane-derived values out of the loop
+         * (live across the rounds, they spill); no staging slots, no wave */
+        t.lane = lane_id();
+        asm volatile("" : "+v"(t.lane));
+        t.wave = 0;
+    } else {
+        t.lane = threadIdx.x & 63u;
+        t.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    }
     const uint64_t shift = (MODE == BS_CTR) ? P.shift : 0;
     /* one 2048-block task per wave, no grid-stride loop: a loop lets hipcc
      * hoist loop-invariant plane/mask values out of it, which costs more
      * registers than the 128-plane state leaves.  Full blocks only; the host
      * routes a trailing partial CTR block to the T-table kernel. */
-    uint64_t task = (uint64_t)blockIdx.x * 4u + t.wave;
+    uint64_t task = claimed >= 0 ? (uint64_t)claimed : (uint64_t)blockIdx.x * 4u + t.wave;
     if (P.part == BS_EDGE_ONLY) {
         if (t.wave > 1 || (t.wave == 1 && P.tasks < 2)) return false;
         task = t.wave == 0 ? 0 : P.tasks - 1;
@@ -310,10 +316,11 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
 #define OTC_BS_PRE 2
 #endif
 template <int NR, int MODE, int LS, bool CACHE, bool FO, int MIX = 2, int PRE = OTC_BS_PRE, int D = 8>
-__device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key &K, uint4 *stage)
+__device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key &K, uint4 *stage,
+                                            int64_t claimed = -1)
 {
     Task t;
-    if (!task_of<MODE>(P, t)) return;
+    if (!task_of<MODE>(P, t, claimed)) return;
     const uint32_t lane = t.lane, wave = t.wave;
     const uint64_t shift = (MODE == BS_CTR) ? P.shift : 0;
     const bool full = FO || t.full; /* FO: a BS_FULL_ONLY launch */
@@ -499,6 +506,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     aes_bs_task<NR, MODE, LS, CACHE, FO>(P, K, stage);
 }
 
+/* The bitsliced half of a claimed co-resident split (otc_device.h
+ * SplitClaim): each wave takes whole 2048-block units from the front of the
+ * buffer until none are left.  No LDS, so it fits beside the 160 KiB
+ * decryption T-table; the loop is the only one in a bitsliced kernel (the
+ * task body is unchanged: no hoisted state, same VGPRs -- tests/test_isa_cpu.py). */
+template <int NR, int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_aes_bs_claim(BsParams P,
+                                                                                               otc_aes_key K)
+{
+    for (;;) {
+        const int64_t u = claim_unit(P.cl, false);
+        if (u < 0) break;
+        /* the buffers opaque per task, as the lane (task_of): nothing derived
+         * from them is hoisted; laundered as global pointers, or the loads and
+         * stores become flat ones */
+        BsParams Q = P;
+        auto gin = (__attribute__((address_space(1))) const uint8_t *)P.in;
+        auto gout = (__attribute__((address_space(1))) uint8_t *)P.out;
+        asm volatile("" : "+s"(gin), "+s"(gout));
+        Q.in = (const uint8_t *)gin;
+        Q.out = (uint8_t *)gout;
+        aes_bs_task<NR, MODE, 0, false, true>(Q, K, nullptr, u);
+    }
+}
+
 template <int NR, int MODE>
 hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
 {
@@ -543,6 +575,14 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
      * profiles/r2/bitslice_out), CTR (64 GiB, with the key-term prefetch)
      * 1547/1551 vs 1606/1606 (profiles/r3/split). */
     const bool edge = (MODE == BS_CTR && P.shift != 0) || vt % 2048 != 0;
+    if constexpr (MODE != BS_CTR) {
+        if (P.cl.ctr) { /* claimed split: one workgroup per CU beside the T-table's */
+            hipLaunchKernelGGL((k_aes_bs_claim<NR, MODE>), dim3((unsigned)otc_dev::device_cus()), b, 0, st, Q, K);
+            e = hipGetLastError();
+            const hipError_t f = hipFreeAsync(tab, st);
+            return e != hipSuccess ? e : f;
+        }
+    }
     auto run = [&](auto cachec) {
         constexpr bool C = decltype(cachec)::value;
         Q.part = BS_FULL_ONLY;
@@ -669,6 +709,26 @@ hipError_t bs_cfb_decrypt(const void *in, void *out, uint64_t nblocks, const otc
     P.has_prev = has_prev ? 1u : 0u;
     for (int i = 0; i < 4; ++i) P.iv[i] = iv_le ? iv_le[i] : 0u;
     return launch<BS_CFB_DEC>(P, K, st);
+}
+
+/* The bitsliced halves of a claimed split: the whole buffer (block 0's
+ * predecessor is iv_le), units from the front of `cl` */
+hipError_t bs_claim(int mode, const void *in, void *out, uint64_t nblocks, const otc_aes_key &K,
+                    const uint32_t iv_le[4], SplitClaim cl, hipStream_t st)
+{
+    BsParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nblocks = nblocks;
+    for (int i = 0; i < 4; ++i) P.iv[i] = iv_le ? iv_le[i] : 0u;
+    P.cl = cl;
+    switch (mode) {
+    case BS_ECB: return launch<BS_ECB>(P, K, st);
+    case BS_ECB_DEC: return launch<BS_ECB_DEC>(P, K, st);
+    case BS_CBC_DEC: return launch<BS_CBC_DEC>(P, K, st);
+    case BS_CFB_DEC: return launch<BS_CFB_DEC>(P, K, st);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 } // namespace otc_impl

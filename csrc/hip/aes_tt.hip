@@ -248,6 +248,7 @@ struct EncParams {
     uint64_t seg_blocks; /* CFB_DEC_SEG: blocks per segment */
     uint32_t seg_shift;  /* CFB_DEC_SEG: log2(seg_blocks), or 64 if not a power of two */
     uint32_t pad2;
+    SplitClaim cl;       /* CLAIM kernels: units taken from the back of the buffer */
 };
 
 struct DecParams {
@@ -257,14 +258,18 @@ struct DecParams {
     uint32_t seg_shift; /* D_CBC_SEG: log2(blocks per segment) */
     uint32_t pad;
     Ctr128 iv;          /* CBC: IV (numeric BE); CBC_SEG: IV of segment 0 */
+    SplitClaim cl;      /* CLAIM kernels: units taken from the back of the buffer */
 };
 
 /* ---------------------------------------------------------------------------
  * Encryption-direction kernel: ECB-enc, CFB128-dec (CTR has its own
  * counter-caching kernel below)
  * ------------------------------------------------------------------------- */
-template <int NR, int MODE, int B, int THREADS>
-__global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key K)
+/* CLAIM: the T-table half of a co-resident split (otc_device.h SplitClaim):
+ * workgroup 0 first runs the blocks past the last full 2048-block unit, then
+ * every wave takes units from the back of the buffer until none are left. */
+template <int NR, int MODE, int B, int THREADS, bool CLAIM>
+__device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_key &K)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
     fill_tbl4<THREADS>(tbl, g_tab.te0);
@@ -314,9 +319,8 @@ __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key
         return;
     }
 
-    for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nfull; base += (uint64_t)gridDim.x * PER) {
-        const bool full = base + PER <= P.nfull; /* wave-uniform */
-        const uint64_t i0 = base + (uint64_t)wave * 64u * B + lane;
+    /* B blocks per lane: i0 + 64 b, b < B; `full`: all in range (wave-uniform) */
+    auto chunk = [&](uint64_t i0, bool full) {
         uint32_t s[B][4];
         uint4 x[B];
 #pragma unroll
@@ -358,7 +362,49 @@ __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key
             }
             if (full || i < P.nfull) st16(P.out, i, o);
         }
+    };
+
+    if constexpr (CLAIM) {
+        const uint64_t done = (uint64_t)P.cl.nunits * 2048u; /* the rest: workgroup 0, first */
+        if (blockIdx.x == 0)
+            for (uint64_t base = done; base < P.nfull; base += PER) chunk(base + (uint64_t)wave * 64u * B + lane, false);
+        for (;;) {
+            const int64_t u = claim_unit(P.cl, true);
+            if (u < 0) break;
+#pragma unroll 1
+            for (uint32_t it = 0; it < 2048u / (64u * B); ++it) chunk((uint64_t)u * 2048u + it * 64u * B + lane, true);
+        }
+        return;
     }
+    for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nfull; base += (uint64_t)gridDim.x * PER)
+        chunk(base + (uint64_t)wave * 64u * B + lane, base + PER <= P.nfull);
+}
+
+template <int NR, int MODE, int B, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key K)
+{
+    enc_tt_body<NR, MODE, B, THREADS, false>(P, K);
+}
+
+/* Claimed split: a bitsliced wave per SIMD (156-168 registers) must fit
+ * beside the workgroup's 4 T-table waves in the 512-register file, which
+ * leaves each T-table wave 80-88.  hipcc will not cap a kernel whose LDS
+ * already limits it to 4 waves per SIMD (amdgpu_num_vgpr is ignored,
+ * waves_per_eu "fails to meet" the target), so the blocks per lane are the
+ * lever: ECB encryption at B = 4 takes 82 (88 allocated + 160 = 512); the
+ * chained CFB decryption needs B = 2 (61; at 4: 101). */
+#ifndef OTC_TT_CLAIM_B
+#define OTC_TT_CLAIM_B 2
+#endif
+template <int NR>
+__global__ __launch_bounds__(1024) void k_aes_ecb_tt_claim(EncParams P, otc_aes_key K)
+{
+    enc_tt_body<NR, E_ECB, OTC_TT_ENC_B, 1024, true>(P, K);
+}
+template <int NR>
+__global__ __launch_bounds__(1024) void k_aes_cfb_tt_claim(EncParams P, otc_aes_key K)
+{
+    enc_tt_body<NR, E_CFB_DEC, OTC_TT_CLAIM_B, 1024, true>(P, K);
 }
 
 /* ---------------------------------------------------------------------------
@@ -463,8 +509,8 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_
  * Decryption-direction kernel: ECB-dec, CBC-dec (single stream or power-of-2
  * segments with per-segment IVs)
  * ------------------------------------------------------------------------- */
-template <int NR, int MODE, int B, int THREADS>
-__global__ __launch_bounds__(THREADS) void k_aes_dec_tt(DecParams P, otc_aes_key K)
+template <int NR, int MODE, int B, int THREADS, bool CLAIM>
+__device__ __forceinline__ void dec_tt_body(const DecParams &P, const otc_aes_key &K)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64 + 256 * 32]; /* 160 KiB */
     fill_dtbl4<THREADS>(tbl, g_tab.td0, g_tab.is4);
@@ -540,9 +586,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_dec_tt(DecParams P, otc_aes_key
         return;
     }
 
-    for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nfull; base += (uint64_t)gridDim.x * PER) {
-        const bool full = base + PER <= P.nfull;
-        const uint64_t i0 = base + (uint64_t)wave * 64u * B + lane;
+    auto chunk = [&](uint64_t i0, bool full) {
         uint32_t s[B][4];
         uint4 prev[B];
 #pragma unroll
@@ -584,7 +628,36 @@ __global__ __launch_bounds__(THREADS) void k_aes_dec_tt(DecParams P, otc_aes_key
             }
             if (full || i < P.nfull) st16(P.out, i, o);
         }
+    };
+
+    if constexpr (CLAIM) { /* as k_aes_enc_tt */
+        const uint64_t done = (uint64_t)P.cl.nunits * 2048u;
+        if (blockIdx.x == 0)
+            for (uint64_t base = done; base < P.nfull; base += PER) chunk(base + (uint64_t)wave * 64u * B + lane, false);
+        for (;;) {
+            const int64_t u = claim_unit(P.cl, true);
+            if (u < 0) break;
+#pragma unroll 1
+            for (uint32_t it = 0; it < 2048u / (64u * B); ++it) chunk((uint64_t)u * 2048u + it * 64u * B + lane, true);
+        }
+        return;
     }
+    for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nfull; base += (uint64_t)gridDim.x * PER)
+        chunk(base + (uint64_t)wave * 64u * B + lane, base + PER <= P.nfull);
+}
+
+template <int NR, int MODE, int B, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_aes_dec_tt(DecParams P, otc_aes_key K)
+{
+    dec_tt_body<NR, MODE, B, THREADS, false>(P, K);
+}
+
+/* Claimed split: the bitsliced inverse-cipher kernels take 168 registers,
+ * leaving 80 per T-table wave: B = 2 (ECB 51, CBC 66; at 4: 83 / 106) */
+template <int NR, int MODE>
+__global__ __launch_bounds__(1024) void k_aes_dec_tt_claim(DecParams P, otc_aes_key K)
+{
+    dec_tt_body<NR, MODE, OTC_TT_CLAIM_B, 1024, true>(P, K);
 }
 
 /* ---------------------------------------------------------------------------
@@ -1127,6 +1200,42 @@ hipError_t launch_dec(const DecParams &P, const otc_aes_key &K, hipStream_t st)
     }
 }
 
+/* the T-table half of a claimed split: one persistent workgroup per CU */
+template <int MODE>
+hipError_t launch_enc_claim(const EncParams &P, const otc_aes_key &K, hipStream_t st)
+{
+    const dim3 g((unsigned)num_cus()), b(ENC_THREADS);
+    switch (K.nr) {
+    case 10:
+        if constexpr (MODE == E_ECB) hipLaunchKernelGGL((k_aes_ecb_tt_claim<10>), g, b, 0, st, P, K);
+        else hipLaunchKernelGGL((k_aes_cfb_tt_claim<10>), g, b, 0, st, P, K);
+        break;
+    case 12:
+        if constexpr (MODE == E_ECB) hipLaunchKernelGGL((k_aes_ecb_tt_claim<12>), g, b, 0, st, P, K);
+        else hipLaunchKernelGGL((k_aes_cfb_tt_claim<12>), g, b, 0, st, P, K);
+        break;
+    case 14:
+        if constexpr (MODE == E_ECB) hipLaunchKernelGGL((k_aes_ecb_tt_claim<14>), g, b, 0, st, P, K);
+        else hipLaunchKernelGGL((k_aes_cfb_tt_claim<14>), g, b, 0, st, P, K);
+        break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t launch_dec_claim(const DecParams &P, const otc_aes_key &K, hipStream_t st)
+{
+    const dim3 g((unsigned)num_cus()), b(DEC_THREADS);
+    switch (K.nr) {
+    case 10: hipLaunchKernelGGL((k_aes_dec_tt_claim<10, MODE>), g, b, 0, st, P, K); break;
+    case 12: hipLaunchKernelGGL((k_aes_dec_tt_claim<12, MODE>), g, b, 0, st, P, K); break;
+    case 14: hipLaunchKernelGGL((k_aes_dec_tt_claim<14, MODE>), g, b, 0, st, P, K); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 template <int NR, bool CFB>
 hipError_t launch_seg_nr(const CbcSegParams &P, const otc_aes_key &K, hipStream_t st)
 {
@@ -1259,6 +1368,54 @@ hipError_t tt_cbc_decrypt(const void *in, void *out, uint64_t nblocks, const otc
     P.nfull = nblocks;
     P.iv = iv;
     return launch_dec<D_CBC>(P, K, st);
+}
+
+/* The T-table halves of a claimed co-resident split (engine.cpp): the whole
+ * buffer, units from the back of `cl`, plus the blocks past its last unit. */
+hipError_t tt_ecb_encrypt_claim(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, SplitClaim cl,
+                                hipStream_t st)
+{
+    EncParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nblocks;
+    P.cl = cl;
+    return launch_enc_claim<E_ECB>(P, K, st);
+}
+
+hipError_t tt_cfb_decrypt_claim(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K,
+                                const uint32_t iv_le[4], SplitClaim cl, hipStream_t st)
+{
+    EncParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nblocks;
+    for (int i = 0; i < 4; ++i) P.iv[i] = iv_le[i];
+    P.cl = cl;
+    return launch_enc_claim<E_CFB_DEC>(P, K, st);
+}
+
+hipError_t tt_ecb_decrypt_claim(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, SplitClaim cl,
+                                hipStream_t st)
+{
+    DecParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nblocks;
+    P.cl = cl;
+    return launch_dec_claim<D_ECB>(P, K, st);
+}
+
+hipError_t tt_cbc_decrypt_claim(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, Ctr128 iv,
+                                SplitClaim cl, hipStream_t st)
+{
+    DecParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nblocks;
+    P.iv = iv;
+    P.cl = cl;
+    return launch_dec_claim<D_CBC>(P, K, st);
 }
 
 hipError_t tt_cbc_decrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,

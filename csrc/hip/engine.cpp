@@ -37,6 +37,11 @@
 #include "engine_internal.h"
 
 using otc_dev::Ctr128;
+using otc_dev::SplitClaim;
+using otc_dev::BS_ECB;
+using otc_dev::BS_ECB_DEC;
+using otc_dev::BS_CBC_DEC;
+using otc_dev::BS_CFB_DEC;
 
 namespace otc_impl {
 hipError_t tt_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
@@ -55,6 +60,12 @@ hipError_t bs_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, h
 hipError_t bs_ecb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
 hipError_t bs_cbc_decrypt(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, bool, hipStream_t);
 hipError_t bs_cfb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, bool, hipStream_t);
+hipError_t bs_claim(int, const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, SplitClaim, hipStream_t);
+hipError_t tt_ecb_encrypt_claim(const void *, void *, uint64_t, const otc_aes_key &, SplitClaim, hipStream_t);
+hipError_t tt_cfb_decrypt_claim(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, SplitClaim,
+                                hipStream_t);
+hipError_t tt_ecb_decrypt_claim(const void *, void *, uint64_t, const otc_aes_key &, SplitClaim, hipStream_t);
+hipError_t tt_cbc_decrypt_claim(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, SplitClaim, hipStream_t);
 hipError_t tt_ctr_batch(const otc_ctr_msg *, const otc_aes_key *, const uint32_t *, const uint64_t *, uint64_t, int, int,
                         hipStream_t);
 hipError_t k_xor(const void *, const void *, void *, size_t, hipStream_t);
@@ -134,8 +145,9 @@ namespace {
 /* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  CTR calls of >= 2 GiB
  * (AES-256: >= 1 GiB) run bitsliced, the thresholds below; smaller CTR calls
  * (the bitsliced grid needs ~768 workgroups to fill the chip, plus two table
- * kernels per call) take the T-table.  ECB encryption: the co-resident split
- * (ecb_split below) from ecb_split_min() bytes, the T-table below that.
+ * kernels per call) take the T-table.  ECB, CBC / CFB decryption: the
+ * co-resident split (split_claim below) from split_min() bytes, the T-table
+ * below that.
  * ctr_bytes = 0 for non-CTR calls.  OTC_IMPL=ttable|bitslice|split overrides
  * "auto" for the whole process. */
 int env_impl()
@@ -176,20 +188,21 @@ int check_impl(int impl)
     return set_err(OTC_ERR_ARG, "impl must be OTC_IMPL_AUTO, OTC_IMPL_TTABLE, OTC_IMPL_BITSLICE or OTC_IMPL_SPLIT");
 }
 
-/* ---- ECB encryption: co-resident T-table + bitsliced split -----------------
- * The T-table kernel is LDS-bound (80% of the LDS array's cycles, 224 lookups
- * per AES-256 block, VALU 32% busy) and leaves power on the table: 1.27 kW
- * with the package power limit active half the time, where the VALU-bound
- * bitsliced kernels hold the ~1.38 kW cap (profiles/r4/power).  Its one
- * 1024-thread workgroup per CU (4 waves x 56 VGPRs per SIMD, 128 KiB LDS)
- * also leaves room in the register file: the bitsliced ECB kernel (0 LDS,
- * 80 VGPRs, 3 waves per SIMD) fits beside it (7 waves, 464 of 512 VGPRs).
- * So the last `share` of the blocks goes to the bitsliced kernel on an
- * auxiliary stream, launched right after the T-table kernel on the caller's
- * stream, and the two run concurrently on every CU -- LDS and VALU busy at
- * once.  The caller's stream waits for both (fork / join events).  Measured
- * AES-256 64 GiB: T-table 1040, bitsliced 1020, split 0.35 1154-1161 GB/s
- * (profiles/r4/ecb_split). */
+/* ---- co-resident T-table + bitsliced split (ECB, CBC / CFB decryption) -----
+ * The T-table kernels are LDS-bound (80% of the LDS array's cycles, 224
+ * lookups per AES-256 block, VALU a third busy) and leave power on the table:
+ * 1.23-1.29 kW with the package power limit active ~55-60% of the time, where
+ * the VALU-bound bitsliced kernels hold the ~1.37 kW cap (profiles/r4/power).
+ * A T-table workgroup (1024 threads = 4 waves per SIMD at 78-85 VGPRs, 128 or
+ * 160 KiB LDS) leaves room for one bitsliced wave per SIMD (152-168 VGPRs, no
+ * LDS).  So both kernels run at once on every CU over ONE buffer -- the
+ * T-table on the caller's stream, the bitsliced kernel on a pooled auxiliary
+ * stream (fork / join events) -- and take 2048-block units from a shared
+ * counter, the bitsliced kernel from the front and the T-table from the back
+ * (otc_device.h SplitClaim), so they finish together on any box: no share to
+ * tune, no tail where one kernel runs alone.  Measured: docs/PERF.md
+ * "Round 4" (the static shares this replaced: profiles/r4/ecb_split,
+ * dec_split, cfb_split). */
 struct AuxStream {
     int dev = -1;
     hipStream_t s = nullptr;
@@ -234,106 +247,86 @@ void aux_give(const AuxStream &a)
     g_aux_free.push_back(a);
 }
 
-/* bitsliced share of the blocks and the smallest call that splits, per key
- * size (profiles/r4/ecb_split: share sweeps at 1, 4 and 64 GiB) */
-double ecb_split_share(int bits) { return bits == 256 ? 0.25 : bits == 192 ? 0.25 : 0.2; }
-size_t ecb_split_min(int bits) { return bits == 256 ? ((size_t)1 << 30) : ((size_t)1 << 30); }
-/* decryption (ECB, CBC): the bitsliced inverse cipher costs ~1.17x the
- * encryption's VALU work (L o InvMixColumns o L: 121 nodes per column vs
- * MixColumns' 55), so it takes a smaller share */
-double dec_split_share(int bits, bool cbc) { return (!cbc && bits == 256) ? 0.2 : 0.15; }
-/* CFB128 decryption: the bitsliced forward cipher plus a second input load per
- * block (profiles/r4/cfb_split: 0.2 beat 0.25-0.35 at 4 and 32 GiB) */
-double cfb_split_share(int) { return 0.2; }
-size_t dec_split_min(int) { return (size_t)1 << 30; }
+/* the smallest call that splits (below: the T-table alone; a split's fork /
+ * join and counter cost a few us, and the bitsliced kernel needs many units) */
+size_t split_min(int) { return (size_t)1 << 30; }
 
 int pick_ecb_impl(int impl, int bits, size_t nbytes)
 {
     if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_SPLIT) return impl;
     const int env = env_impl();
     if (env != OTC_IMPL_AUTO) return env;
-    return nbytes >= ecb_split_min(bits) ? OTC_IMPL_SPLIT : OTC_IMPL_TTABLE;
+    return nbytes >= split_min(bits) ? OTC_IMPL_SPLIT : OTC_IMPL_TTABLE;
 }
 
-int pick_dec_impl(int impl, int bits, size_t nbytes)
-{
-    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_SPLIT) return impl;
-    const int env = env_impl();
-    if (env != OTC_IMPL_AUTO) return env;
-    return nbytes >= dec_split_min(bits) ? OTC_IMPL_SPLIT : OTC_IMPL_TTABLE;
-}
+int pick_dec_impl(int impl, int bits, size_t nbytes) { return pick_ecb_impl(impl, bits, nbytes); }
 
-/* The split itself: tt(nt) launches the T-table kernel over the first nt
- * blocks on st, bs(nt, nb, aux) the bitsliced kernel over the last nb on the
- * auxiliary stream.  nb is whole 2048-block bitsliced tasks (no edge
- * launch); a share that rounds to none runs the T-table alone.  *ran: the
- * kernels actually used. */
-template <class TT, class BS>
-hipError_t split_run(uint64_t nblocks, double share, hipStream_t st, int *ran, TT tt, BS bs)
+/* The split: tt(cl) launches the T-table claim kernel on st, bs(cl, aux) the
+ * bitsliced claim kernel on the auxiliary stream, both over the whole buffer;
+ * plain(n) is the T-table alone (calls under two units, or no memory for the
+ * counter).  *ran: the kernels actually used. */
+template <class TT, class BS, class PLAIN>
+hipError_t split_claim(uint64_t nblocks, hipStream_t st, int *ran, TT tt, BS bs, PLAIN plain)
 {
-    const uint64_t nb = (uint64_t)((double)nblocks * share) / 2048u * 2048u;
-    if (nb == 0 || nb >= nblocks) {
-        *ran = OTC_IMPL_TTABLE;
-        return tt(nblocks);
+    const uint64_t nunits = nblocks / 2048u;
+    *ran = OTC_IMPL_TTABLE;
+    if (nunits < 2 || nunits > 0x7FFFFFFFull) return plain(nblocks);
+    unsigned long long *ctr = nullptr;
+    hipError_t e = otc_dev::alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&ctr, sizeof *ctr, st);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return plain(nblocks);
     }
-    const uint64_t nt = nblocks - nb;
     int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
     AuxStream a;
-    if ((e = aux_take(dev, a)) != hipSuccess) return e;
-    /* fork: the aux stream starts after everything already queued on st */
-    if ((e = hipEventRecord(a.fork, st)) == hipSuccess && (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess &&
-        (e = tt(nt)) == hipSuccess && (e = bs(nt, nb, a.s)) == hipSuccess && (e = hipEventRecord(a.join, a.s)) == hipSuccess)
+    if ((e = hipGetDevice(&dev)) != hipSuccess || (e = aux_take(dev, a)) != hipSuccess) {
+        (void)hipFreeAsync(ctr, st);
+        return e;
+    }
+    const SplitClaim cl{ctr, (uint32_t)nunits, 0};
+    /* zeroed, then fork: the aux stream starts after everything queued on st */
+    if ((e = hipMemsetAsync(ctr, 0, sizeof *ctr, st)) == hipSuccess && (e = hipEventRecord(a.fork, st)) == hipSuccess &&
+        (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess && (e = tt(cl)) == hipSuccess &&
+        (e = bs(cl, a.s)) == hipSuccess && (e = hipEventRecord(a.join, a.s)) == hipSuccess)
         e = hipStreamWaitEvent(st, a.join, 0); /* join: st continues after both */
+    const hipError_t f = hipFreeAsync(ctr, st); /* after the join: both kernels are done with it */
     aux_give(a); /* reusable as soon as the work is enqueued: stream order */
-    *ran = OTC_IMPL_SPLIT;
-    return e;
+    if (e == hipSuccess) *ran = OTC_IMPL_SPLIT;
+    return e != hipSuccess ? e : f;
 }
 
 hipError_t ecb_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, hipStream_t st, int *ran)
 {
-    const uint8_t *pi = (const uint8_t *)in;
-    uint8_t *po = (uint8_t *)out;
     if (K.dir == OTC_DIR_ENCRYPT)
-        return split_run(
-            nblocks, ecb_split_share(K.bits), st, ran,
-            [&](uint64_t nt) { return otc_impl::tt_ecb_encrypt(pi, po, nt, K, st); },
-            [&](uint64_t nt, uint64_t nb, hipStream_t s) { return otc_impl::bs_ecb_encrypt(pi + 16 * nt, po + 16 * nt, nb, K, s); });
-    return split_run(
-        nblocks, dec_split_share(K.bits, false), st, ran,
-        [&](uint64_t nt) { return otc_impl::tt_ecb_decrypt(pi, po, nt, K, st); },
-        [&](uint64_t nt, uint64_t nb, hipStream_t s) { return otc_impl::bs_ecb_decrypt(pi + 16 * nt, po + 16 * nt, nb, K, s); });
+        return split_claim(
+            nblocks, st, ran, [&](SplitClaim cl) { return otc_impl::tt_ecb_encrypt_claim(in, out, nblocks, K, cl, st); },
+            [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_ECB, in, out, nblocks, K, nullptr, cl, s); },
+            [&](uint64_t n) { return otc_impl::tt_ecb_encrypt(in, out, n, K, st); });
+    return split_claim(
+        nblocks, st, ran, [&](SplitClaim cl) { return otc_impl::tt_ecb_decrypt_claim(in, out, nblocks, K, cl, st); },
+        [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_ECB_DEC, in, out, nblocks, K, nullptr, cl, s); },
+        [&](uint64_t n) { return otc_impl::tt_ecb_decrypt(in, out, n, K, st); });
 }
 
 hipError_t cbc_dec_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, const uint8_t iv[16],
                          hipStream_t st, int *ran)
 {
-    const uint8_t *pi = (const uint8_t *)in;
-    uint8_t *po = (uint8_t *)out;
-    return split_run(
-        nblocks, dec_split_share(K.bits, true), st, ran,
-        [&](uint64_t nt) { return otc_impl::tt_cbc_decrypt(pi, po, nt, K, ctr_from_bytes(iv), st); },
-        /* the bitsliced part's block 0 XORs with block nt-1 of the input */
-        [&](uint64_t nt, uint64_t nb, hipStream_t s) {
-            return otc_impl::bs_cbc_decrypt(pi + 16 * nt, po + 16 * nt, nb, K, nullptr, true, s);
-        });
+    uint32_t ivw[4];
+    memcpy(ivw, iv, 16); /* the bitsliced kernel's IV: LE words of the bytes */
+    const Ctr128 ivc = ctr_from_bytes(iv);
+    return split_claim(
+        nblocks, st, ran, [&](SplitClaim cl) { return otc_impl::tt_cbc_decrypt_claim(in, out, nblocks, K, ivc, cl, st); },
+        [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_CBC_DEC, in, out, nblocks, K, ivw, cl, s); },
+        [&](uint64_t n) { return otc_impl::tt_cbc_decrypt(in, out, n, K, ivc, st); });
 }
 
-/* CFB128 decryption enciphers the previous ciphertext block: ECB encryption's
- * work plus one more input load per block */
 hipError_t cfb_dec_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, const uint32_t ivw[4],
                          hipStream_t st, int *ran)
 {
-    const uint8_t *pi = (const uint8_t *)in;
-    uint8_t *po = (uint8_t *)out;
-    return split_run(
-        nblocks, cfb_split_share(K.bits), st, ran,
-        [&](uint64_t nt) { return otc_impl::tt_cfb_decrypt(pi, po, nt, K, ivw, st); },
-        /* the bitsliced part's block 0 enciphers block nt-1 of the input */
-        [&](uint64_t nt, uint64_t nb, hipStream_t s) {
-            return otc_impl::bs_cfb_decrypt(pi + 16 * nt, po + 16 * nt, nb, K, nullptr, true, s);
-        });
+    return split_claim(
+        nblocks, st, ran, [&](SplitClaim cl) { return otc_impl::tt_cfb_decrypt_claim(in, out, nblocks, K, ivw, cl, st); },
+        [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_CFB_DEC, in, out, nblocks, K, ivw, cl, s); },
+        [&](uint64_t n) { return otc_impl::tt_cfb_decrypt(in, out, n, K, ivw, st); });
 }
 
 /* the kernel family the calling thread's last AES call ran (otc_last_impl) */
@@ -885,6 +878,22 @@ extern "C" void *otc_stream_create(void)
     }
     return (void *)s;
 }
+/* a and b each wait for what the other has queued so far: a join point for
+ * work split by hand over two streams (otbench's *-split modes) */
+extern "C" int otc_stream_join(void *a, void *b)
+{
+    hipEvent_t ea = nullptr, eb = nullptr;
+    hipError_t e = hipEventCreateWithFlags(&ea, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&eb, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ea, (hipStream_t)a);
+    if (e == hipSuccess) e = hipEventRecord(eb, (hipStream_t)b);
+    if (e == hipSuccess) e = hipStreamWaitEvent((hipStream_t)a, eb, 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent((hipStream_t)b, ea, 0);
+    if (ea) (void)hipEventDestroy(ea); /* released once the waits are satisfied */
+    if (eb) (void)hipEventDestroy(eb);
+    return e == hipSuccess ? OTC_OK : hip_fail(e, "stream join");
+}
+
 extern "C" void otc_stream_destroy(void *s)
 {
     if (s) (void)hipStreamDestroy((hipStream_t)s);

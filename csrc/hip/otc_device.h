@@ -103,6 +103,49 @@ __device__ __forceinline__ void ctr_words(const Ctr128 &c, uint64_t idx, bool wr
     w3 = bswap32((uint32_t)lo);
 }
 
+/* Bitsliced kernel modes (aes_bs.hip): BS_ECB: ECB encryption; BS_ECB_DEC /
+ * BS_CBC_DEC: the inverse cipher through the forward S-box (S^-1 = L S L,
+ * otc_invmix.h) with a decryption key; BS_CFB_DEC: CFB128 decryption, P_i =
+ * E(C_{i-1}) ^ C_i -- the forward cipher on the input shifted back one block,
+ * XORed with the input */
+enum : int { BS_CTR = 0, BS_ECB = 1, BS_ECB_DEC = 2, BS_CBC_DEC = 3, BS_CFB_DEC = 4 };
+
+/* Work claiming of a co-resident split (engine.cpp split_claim): the T-table
+ * and the bitsliced kernel take 2048-block units of ONE buffer from a shared
+ * 64-bit counter -- the bitsliced kernel from the front (count in the low 32
+ * bits), the T-table kernel from the back (high 32 bits) -- so both run until
+ * the buffer is done and finish together, whatever rate each gets on the box.
+ * Every claim is one atomic on the whole word: claim k is valid iff
+ * front + back claims before it < nunits, so the two ends never overlap.  A
+ * wave claims with one lane (a vector-memory atomic) and broadcasts. */
+struct SplitClaim {
+    unsigned long long *ctr; /* zeroed (stream-ordered) before the launches */
+    uint32_t nunits;         /* full 2048-block units */
+    uint32_t pad;
+};
+
+/* lane id from the exec-mask count: nothing to keep live across a loop
+ * (threadIdx.x lives in v0 from kernel entry; read in every trip of a long
+ * loop body, hipcc keeps it -- and spills it) */
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+/* unit index, or -1 when the buffer is exhausted (wave-uniform) */
+__device__ __forceinline__ int64_t claim_unit(const SplitClaim &c, bool back)
+{
+    unsigned long long old = 0;
+    if (lane_id() == 0) {
+        /* built per claim: hoisted out of a caller's loop, the operand pair
+         * would stay live (and spill) across the whole loop body */
+        unsigned long long inc = back ? (1ull << 32) : 1ull;
+        asm volatile("" : "+v"(inc));
+        old = __hip_atomic_fetch_add(c.ctr, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint32_t f = __builtin_amdgcn_readfirstlane((uint32_t)old);
+    const uint32_t b = __builtin_amdgcn_readfirstlane((uint32_t)(old >> 32));
+    if ((uint64_t)f + b >= c.nunits) return -1;
+    return back ? (int64_t)(c.nunits - 1u - b) : (int64_t)f;
+}
+
 /* Allocation fault injection, a test hook (otc_fault_inject_alloc): true
  * when the runtime allocation about to be made should fail.  One atomic
  * countdown; off (no cost beyond a relaxed load) unless armed. */

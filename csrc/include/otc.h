@@ -246,6 +246,9 @@ int otc_device_sync(void);
  * the default stream bracket work queued on it); NULL on failure. */
 void *otc_stream_create(void);
 void otc_stream_destroy(void *stream);
+/* a and b each wait for the work the other has queued so far (a join point
+ * for work split by hand over two streams) */
+int otc_stream_join(void *a, void *b);
 
 /* ---- L3 engine: host-memory streaming pipeline -----------------------------
  * Encrypt/decrypt a HOST buffer through one GPU with a pinned staging ring:

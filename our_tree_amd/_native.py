@@ -173,6 +173,7 @@ def _declare_gpu(lib):
         "otc_dev_free": (None, [c_vp]),
         "otc_memcpy": (c_int, [c_vp, c_vp, c_sz, c_int]),
         "otc_stream_destroy": (None, [c_vp]),
+        "otc_stream_join": (c_int, [c_vp, c_vp]),
         "otc_aes_cbc_encrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cbc_decrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cfb128_decrypt": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_vp]),

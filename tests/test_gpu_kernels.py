@@ -456,11 +456,13 @@ def test_auto_routing_rule(gpu):
 @pytest.mark.parametrize("bits", [128, 192, 256])
 def test_ecb_split_matches_ttable(gpu, bits):
     """The co-resident split (T-table kernel on the caller's stream, bitsliced
-    kernel on the auxiliary stream over the last share of the blocks) is
-    byte-identical to the T-table alone, out of place and in place, on sizes
-    whose split point is not task aligned on the T-table side; a size whose
-    share rounds to no full bitsliced task runs the T-table alone."""
-    for n, want in ((64 * 2048 * 16 * 3 + 48, "split"), (2048 * 16 + 16, "ttable"), (160 << 20, "split")):
+    kernel on the auxiliary stream, both taking 2048-block units of the whole
+    buffer from a shared counter) is byte-identical to the T-table alone, out
+    of place and in place: two units exactly, units plus a partial remainder
+    (run by the T-table's workgroup 0), and a bulk size; under two units the
+    T-table runs alone."""
+    for n, want in ((64 * 2048 * 16 * 3 + 48, "split"), (2048 * 16 + 16, "ttable"), (160 << 20, "split"),
+                    (2 * 2048 * 16, "split"), (2 * 2048 * 16 + 2047 * 16, "split")):
         key = os.urandom(bits // 8)
         x = torch.empty(n, dtype=torch.uint8, device=gpu)
         ops.fill_random_(x, seed=n + bits)
@@ -492,6 +494,31 @@ def test_ecb_split_stream_order(gpu):
     s.synchronize()
     exp = cpu_ref.ecb(key, cpu_ref.ecb(key, host(x[n - 4096:])))
     assert host(z[n - 4096:]) == exp
+
+
+def test_split_concurrent_calls(gpu):
+    """Two splits in flight at once on two streams (each call has its own
+    work counter and takes its own auxiliary stream from the pool), with ECB
+    encryption, ECB / CBC / CFB decryption, equal to the T-table."""
+    n = (96 << 20) + 4096 + 32
+    key, iv = os.urandom(32), os.urandom(16)
+    xs = [torch.empty(n, dtype=torch.uint8, device=gpu) for _ in range(2)]
+    for i, x in enumerate(xs):
+        ops.fill_random_(x, seed=900 + i)
+    torch.cuda.synchronize()
+    calls = [lambda x, impl: ops.ecb_encrypt(x, key, impl=impl), lambda x, impl: ops.ecb_decrypt(x, key, impl=impl),
+             lambda x, impl: ops.cbc_decrypt(x, key, iv, impl=impl),
+             lambda x, impl: ops.cfb128_decrypt(x, key, iv, impl=impl)]
+    for f in calls:
+        streams = [torch.cuda.Stream() for _ in xs]
+        outs = []
+        for x, st in zip(xs, streams):
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st):
+                outs.append(f(x, "split"))
+        torch.cuda.synchronize()
+        for x, y in zip(xs, outs):
+            assert torch.equal(y, f(x, "ttable"))
 
 
 @pytest.mark.parametrize("bits,n", [(128, (2 << 30) + 3), (192, (2 << 30) + 3), (256, (1 << 30) + 3)])

@@ -5,7 +5,8 @@ Extracts the gfx950 code object from a hipcc object's .hip_fatbin section
 (llvm-objcopy + clang-offload-bundler), disassembles it and prints, for every
 k_aes_bs_t3 instantiation compiled for full tasks only (the bulk launch: one
 2048-block task per wave, straight-line code), the VALU / SALU / SMEM /
-vector-memory instruction counts, VGPRs and scratch bytes (CTR-nocache: the
+vector-memory instruction counts, VGPRs and scratch bytes, and the same for
+the split's claim kernels (MODE-claim: one task per loop trip) (CTR-nocache: the
 kernel CTR falls back to when its counter-caching tables cannot be allocated).  The kernel has no
 loops, so the static VALU count is the VALU per task that rocprofv3's
 SQ_INSTS_VALU / SQ_WAVES reports (profiles/r3/sbox79: 13,058 vs 13,056.5).
@@ -56,15 +57,20 @@ def main():
             meta = metadata(co)
         for f in re.split(r"\n(?=[0-9a-f]+ <)", asm):
             m = re.match(r"[0-9a-f]+ <(.*?)>:", f)
-            if not m or "k_aes_bs_t3" not in m.group(1) or not re.search(r"Lb[01]ELb1EEE", m.group(1)):
+            if not m:
                 continue
             name = m.group(1)
+            claim = "k_aes_bs_claim" in name  # the bitsliced half of a claimed split (one loop over tasks)
+            if not claim and ("k_aes_bs_t3" not in name or not re.search(r"Lb[01]ELb1EEE", name)):
+                continue
             ins = re.findall(r"^\s+([a-z_0-9]+)", f, re.M)
             cnt = lambda p: sum(1 for i in ins if i.startswith(p))
-            tm = re.search(r"t3ILi(\d+)ELi(\d)E", name)
+            tm = re.search(r"(?:t3|claim)ILi(\d+)ELi(\d)E", name)
             mode = {"0": "CTR", "1": "ECB", "2": "ECB-dec", "3": "CBC-dec", "4": "CFB-dec"}.get(tm.group(2), "?") if tm else "?"
             if mode == "CTR" and re.search(r"Lb0ELb1EEE", name):
                 mode = "CTR-nocache"  # fallback when the counter-caching tables do not fit
+            if claim:
+                mode += "-claim"
             bits = NAMES.get(f"Li{tm.group(1)}E", "?") if tm else "?"
             vg, scr = meta.get(name + ".kd", meta.get(name, (-1, -1)))
             print(f"{obj}: {mode} {bits} VALU {cnt('v_')} SALU {cnt('s_') - cnt('s_load') - cnt('s_buffer')} "
