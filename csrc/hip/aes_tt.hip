@@ -43,6 +43,9 @@ using namespace otc_dev;
 #ifndef OTC_TT_PF
 #define OTC_TT_PF 0 /* software-pipelined input loads in the ECB / decrypt kernels */
 #endif
+#ifndef OTC_TT_CTR_B
+#define OTC_TT_CTR_B 4 /* blocks per lane, bulk CTR kernel (A/B knob: 2 fits a bitsliced wave beside it) */
+#endif
 #ifndef OTC_TT_ENC_B
 #define OTC_TT_ENC_B 4 /* blocks per lane, bulk ECB-encrypt / CFB-decrypt kernel */
 #endif
@@ -1317,7 +1320,7 @@ hipError_t launch_ctr_cached(CtrParams P, const otc_aes_key &K, uint64_t ctr_lo,
     switch (small_shape(P.nfull + (P.tail ? 1 : 0))) {
     case SHAPE_256x1: return launch_ctr_cached_tb<NR, 256, 1>(P, K, ctr_lo, st);
     case SHAPE_1024x1: return launch_ctr_cached_tb<NR, 1024, 1>(P, K, ctr_lo, st);
-    default: return launch_ctr_cached_tb<NR, 1024, 4>(P, K, ctr_lo, st);
+    default: return launch_ctr_cached_tb<NR, 1024, OTC_TT_CTR_B>(P, K, ctr_lo, st);
     }
 }
 
