@@ -6,7 +6,7 @@
  *   otbench --mode ctr|ecb|ecb-dec|cbc-dec|cbc-enc-seg|cfb-enc-seg|cfb-dec-seg|cfb-dec|ctr-stream|xor|rc4
  *                  |ecb-split|ecbdec-split|cbcdec-split|cfbdec-split|ctr-split
  *           [--bits 128] [--bytes 1G] [--iters 20] [--warmup 3]
- *           [--impl auto|ttable|bitslice] [--inplace] [--verify] [--clock]
+ *           [--impl auto|ttable|bitslice|split] [--inplace] [--verify] [--clock]
  *           [--mark]                        "OTB_MARK start|end" on stderr around the timed loop
  *           [--corrupt-at OFF]              test hook: flip output byte OFF after the
  *                                           verified op (verification must then fail)
@@ -354,7 +354,12 @@ int main(int argc, char **argv)
         else if (a == "--warmup") c.warmup = atoi(nx());
         else if (a == "--impl") {
             std::string v = nx();
-            c.impl = v == "ttable" ? OTC_IMPL_TTABLE : v == "bitslice" ? OTC_IMPL_BITSLICE : OTC_IMPL_AUTO;
+            if (v != "auto" && v != "ttable" && v != "bitslice" && v != "split") {
+                fprintf(stderr, "--impl must be auto, ttable, bitslice or split\n");
+                return 2;
+            }
+            c.impl = v == "ttable" ? OTC_IMPL_TTABLE : v == "bitslice" ? OTC_IMPL_BITSLICE
+                   : v == "split"  ? OTC_IMPL_SPLIT  : OTC_IMPL_AUTO;
         } else if (a == "--inplace") c.inplace = true;
         else if (a == "--verify") c.verify = true;
         else if (a == "--clock") c.clock = true;
@@ -554,7 +559,8 @@ int main(int argc, char **argv)
            "\"ms\": %.4f, \"gbps\": %.2f, \"cycles_per_byte_per_cu\": %.3f, \"cus\": %d, \"clock_mhz\": %.0f, %s"
            "\"verified\": %s}\n",
            c.mode.c_str(), c.bits, c.bytes,
-           c.impl == OTC_IMPL_TTABLE ? "ttable" : c.impl == OTC_IMPL_BITSLICE ? "bitslice" : "auto",
+           c.impl == OTC_IMPL_TTABLE ? "ttable" : c.impl == OTC_IMPL_BITSLICE ? "bitslice"
+           : c.impl == OTC_IMPL_SPLIT    ? "split"  : "auto",
            c.inplace ? "true" : "false", c.iters, ms, gbps, cpb, cus, clk_hz / 1e6, clk, verdict(c.verify, v));
     otc_dev_free(a.in);
     if (!c.inplace) otc_dev_free(a.out);
