@@ -319,15 +319,17 @@ def main():
 
         meter = PowerMeter(local)
 
-    def timed(nsteps, k, impl=args.impl, measure=False):
+    def timed(nsteps, k, impl=args.impl, measure=False, fn=None):
         """returns (MAX over ranks of the barrier-to-barrier time, this rank's
         own time to its last synchronize, power stats of this rank or None).
         With ``measure`` the energy window opens with the timed steps and,
         if they took less than --energy-min-s, stays open over identical
         untimed steps after the clock has stopped: the socket energy counter
-        updates about every millisecond, so a short window reads ~0 J."""
+        updates about every millisecond, so a short window reads ~0 J.
+        ``fn(k, impl)``: the op timed (default: the headline's CTR step)."""
+        fn = fn or step
         for _ in range(args.warmup):
-            step(k, impl)
+            fn(k, impl)
         sync()
         if torch.distributed.is_initialized():
             torch.distributed.barrier()
@@ -336,7 +338,7 @@ def main():
             meter.start()
         t0 = time.perf_counter()
         for _ in range(nsteps):
-            step(k, impl)
+            fn(k, impl)
         sync()
         mine = time.perf_counter() - t0
         if torch.distributed.is_initialized():
@@ -346,7 +348,7 @@ def main():
         if measure and meter is not None:
             done = nsteps
             while time.perf_counter() - t0 < args.energy_min_s:
-                step(k, impl)
+                fn(k, impl)
                 done += 1
             sync()
             pw = meter.stop(nbytes * done)
@@ -414,8 +416,26 @@ def main():
         extra["aes256_ctr_gbps_whole_node"] = round(nbytes * world * k256_steps / el256 / 1e9, 3)
         extra["aes256_ctr_verified"] = v_ok
         extra["aes256_vs_cpu_aesni_ctr256"] = round(extra["aes256_ctr_gbps_whole_node"] / BASELINE_GBPS, 1)
+    if not args.no_aes256 and not cpu:
+        # AES-256 ECB encryption, in place on the same shard: the reference's
+        # own GPU workload (aes-gpu/Source/main_ecb_e.cu) at this scale --
+        # "auto" runs the co-resident T-table + bitsliced split here
+        def ecb_step(k, impl):
+            ops.ecb_encrypt(buf, k, out=buf, impl=impl)
 
-    bad = [k for k in ("ttable_ctr_verified", "bitsliced_ctr_verified", "aes256_ctr_verified")
+        head, tail = buf[:S].cpu().numpy().tobytes(), buf[nbytes - S:].cpu().numpy().tobytes()
+        ecb_step(key256, args.impl)
+        sync()
+        e_ok = (buf[:S].cpu().numpy().tobytes() == cpu_ref.ecb(key256, head)
+                and buf[nbytes - S:].cpu().numpy().tobytes() == cpu_ref.ecb(key256, tail))
+        e_ok = pdist.allreduce_max(0.0 if e_ok else 1.0) == 0.0
+        e_steps = max(1, min(args.steps, 5))
+        el_e, _, _ = timed(e_steps, key256, fn=ecb_step)
+        extra["aes256_ecb_gbps_whole_node"] = round(nbytes * world * e_steps / el_e / 1e9, 3)
+        extra["aes256_ecb_verified"] = e_ok
+        extra["aes256_ecb_impl"] = ops.pick_impl(args.impl, 256, "ecb", nbytes)
+
+    bad = [k for k in ("ttable_ctr_verified", "bitsliced_ctr_verified", "aes256_ctr_verified", "aes256_ecb_verified")
            if extra.get(k) is False]
     if bad:
         if rank == 0:

@@ -135,6 +135,8 @@ def test_bench_json_line(gpu):
     assert d["verified_sample"] is True
     assert d["config"]["impl_resolved"] == "ttable"  # 0.25 GiB: below the bitsliced threshold
     assert d["bitsliced_ctr_verified"] is True and d["aes256_ctr_verified"] is True  # the extras, checked
+    assert d["aes256_ecb_verified"] is True and d["aes256_ecb_gbps_whole_node"] > 0
+    assert d["aes256_ecb_impl"] in ("split", "ttable")  # the reference's workload: AES-256 ECB
     nbytes = d["config"]["per_gpu_bytes"]
     assert nbytes == int(0.25 * (1 << 30))
     # value (GB/s) and ms_per_step describe the same timed region
