@@ -286,12 +286,18 @@ hipError_t split_claim(uint64_t nblocks, hipStream_t st, int *ran, TT tt, BS bs,
     const SplitClaim cl{ctr, (uint32_t)nunits, 0};
     /* zeroed, then fork: the aux stream starts after everything queued on st */
     if ((e = hipMemsetAsync(ctr, 0, sizeof *ctr, st)) == hipSuccess && (e = hipEventRecord(a.fork, st)) == hipSuccess &&
-        (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess && (e = tt(cl)) == hipSuccess &&
-        (e = bs(cl, a.s)) == hipSuccess && (e = hipEventRecord(a.join, a.s)) == hipSuccess)
-        e = hipStreamWaitEvent(st, a.join, 0); /* join: st continues after both */
+        (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess && (e = tt(cl)) == hipSuccess) {
+        /* the bitsliced half failing (no memory for its key table) leaves the
+         * T-table claim kernel to take every unit: the output is complete, so
+         * the call succeeds as a T-table run.  The join is recorded either way
+         * (a failure after its launch must still be waited for). */
+        const hipError_t eb = bs(cl, a.s);
+        if (eb != hipSuccess) (void)hipGetLastError();
+        if ((e = hipEventRecord(a.join, a.s)) == hipSuccess) e = hipStreamWaitEvent(st, a.join, 0);
+        if (e == hipSuccess) *ran = eb == hipSuccess ? OTC_IMPL_SPLIT : OTC_IMPL_TTABLE;
+    }
     const hipError_t f = hipFreeAsync(ctr, st); /* after the join: both kernels are done with it */
     aux_give(a); /* reusable as soon as the work is enqueued: stream order */
-    if (e == hipSuccess) *ran = OTC_IMPL_SPLIT;
     return e != hipSuccess ? e : f;
 }
 

@@ -98,3 +98,27 @@ def test_bitslice_ecb_table_failure_is_an_error(inject, gpu):
     y = ops.ecb_encrypt(x, key, impl="bitslice")
     torch.cuda.synchronize()
     assert y.cpu().numpy().tobytes() == cpu_ref.ecb(key, x.cpu().numpy().tobytes())
+
+
+@pytest.mark.parametrize("k,want", [(0, "ttable"), (1, "ttable")])
+def test_split_under_alloc_faults(inject, gpu, k, want):
+    """The claimed split's work counter (allocation 0) or the bitsliced half's
+    key table (allocation 1) cannot be allocated: the T-table runs every unit
+    (plain, or as the split's only claimant) and the output is complete."""
+    key, iv = os.urandom(32), os.urandom(16)
+    x = torch.from_numpy(_rnd(16 * 2048 * 40 + 48, 5)).to(gpu)
+    ref_ecb = cpu_ref.ecb(key, x.cpu().numpy().tobytes())
+    inject(k)
+    y = ops.ecb_encrypt(x, key, impl="split")
+    torch.cuda.synchronize()
+    assert ops.last_impl() == want
+    assert y.cpu().numpy().tobytes() == ref_ecb
+    inject(-1)
+    inject(k)
+    z = ops.cbc_decrypt(x, key, iv, impl="split")
+    torch.cuda.synchronize()
+    assert z.cpu().numpy().tobytes() == cpu_ref.cbc(key, iv, x.cpu().numpy().tobytes(), decrypt=True)
+    inject(-1)
+    y = ops.ecb_encrypt(x, key, impl="split")
+    torch.cuda.synchronize()
+    assert ops.last_impl() == "split" and y.cpu().numpy().tobytes() == ref_ecb
