@@ -67,3 +67,39 @@ def test_claim_kernels_fit_beside_ttable(counts):
 def test_ctr_valu_budget(counts):
     for key, budget in BUDGET.items():
         assert counts[key][0] <= budget, (key, counts[key][0], budget)
+
+
+def test_split_pairs_share_a_simd():
+    """Co-residency of the claimed split, from the code objects: for every
+    split mode, 4 waves of the T-table claim kernel plus 1 wave of the
+    bitsliced claim kernel fit in a SIMD's 512 registers at the hardware's
+    8-register allocation granule (docs/PERF.md round 4) -- a T-table change
+    that adds a few registers would silently turn the split into time
+    slicing."""
+    tt_obj = os.path.join(ROOT, "build", "obj", "hip", "aes_tt.o")
+    if not os.path.exists(tt_obj) or not os.path.exists(OBJ) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):
+        pytest.skip("no built objects (make) or no ROCm LLVM tools")
+    import tempfile
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_count
+
+    def vgprs(obj):
+        with tempfile.TemporaryDirectory() as tmp:
+            return {k: v[0] for k, v in isa_count.metadata(isa_count.code_object(obj, tmp)).items()}
+
+    tt, bs = vgprs(tt_obj), vgprs(OBJ)
+    alloc = lambda n: -(-n // 8) * 8
+    # split mode: (T-table claim kernel name part, bitsliced claim mode number)
+    pairs = {"ECB": ("k_aes_ecb_tt_claim", 1), "ECB-dec": ("k_aes_dec_tt_claimILi{nr}ELi0E", 2),
+             "CBC-dec": ("k_aes_dec_tt_claimILi{nr}ELi1E", 3), "CFB-dec": ("k_aes_cfb_tt_claim", 4)}
+    seen = 0
+    for mode, (tpat, bmode) in pairs.items():
+        for nr in (10, 12, 14):
+            tnames = [k for k in tt if tpat.format(nr=nr) in k and f"ILi{nr}E" in k]
+            bnames = [k for k in bs if f"k_aes_bs_claimILi{nr}ELi{bmode}E" in k]
+            assert tnames and bnames, (mode, nr)
+            t, b = max(tt[k] for k in tnames), max(bs[k] for k in bnames)
+            assert 4 * alloc(t) + alloc(b) <= 512, (mode, nr, t, b)
+            seen += 1
+    assert seen == 12
