@@ -43,6 +43,12 @@ using namespace otc_dev;
 #ifndef OTC_TT_PF
 #define OTC_TT_PF 0 /* software-pipelined input loads in the ECB / decrypt kernels */
 #endif
+#ifndef OTC_SEG_GB
+#define OTC_SEG_GB 1 /* segments per lane, grouped CBC / CFB segment encryption (A/B knob) */
+#endif
+#ifndef OTC_SEG_G
+#define OTC_SEG_G 8 /* blocks per load burst, grouped segment encryption (A/B knob) */
+#endif
 #ifndef OTC_TT_CTR_B
 #define OTC_TT_CTR_B 4 /* blocks per lane, bulk CTR kernel (A/B knob: 2 fits a bitsliced wave beside it) */
 #endif
@@ -1247,9 +1253,9 @@ hipError_t launch_seg_nr(const CbcSegParams &P, const otc_aes_key &K, hipStream_
      * profiles/r1/otbench_cbcenc_group_ab.jsonl); B = 1: two 8-block buffers
      * per segment fit without spills.  Segments shorter than 8 blocks take the
      * per-block kernel. */
-    if (P.seg_blocks >= 8)
-        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, 1, SEG_THREADS, 8, CFB>),
-                           dim3(grid_for(P.nseg, (uint64_t)SEG_THREADS, 1)), dim3(SEG_THREADS), 0, st, P, K);
+    if (P.seg_blocks >= OTC_SEG_G)
+        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, OTC_SEG_GB, SEG_THREADS, OTC_SEG_G, CFB>),
+                           dim3(grid_for(P.nseg, (uint64_t)SEG_THREADS * OTC_SEG_GB, 1)), dim3(SEG_THREADS), 0, st, P, K);
     else
         hipLaunchKernelGGL((k_aes_cbc_enc_seg<NR, SEG_B, SEG_THREADS, CFB>), dim3(grid), dim3(SEG_THREADS), 0, st, P,
                            K);
