@@ -247,9 +247,12 @@ void aux_give(const AuxStream &a)
     g_aux_free.push_back(a);
 }
 
-/* the smallest call that splits (below: the T-table alone; a split's fork /
- * join and counter cost a few us, and the bitsliced kernel needs many units) */
-size_t split_min(int) { return (size_t)1 << 30; }
+/* the smallest call that splits: 896 MiB.  Below it the T-table alone wins:
+ * a claim unit is ~130 us of one T-table wave's work, so a short call ends
+ * with idle waves (profiles/r4/claim_split/small_sizes.jsonl,
+ * mid_sizes.jsonl: 512 MiB loses 2-6%, 896 MiB ties ECB and wins decryption
+ * 4-7%, 1000 MiB -- the reference's own size -- wins 3-11%) */
+size_t split_min(int) { return (size_t)896 << 20; }
 
 int pick_ecb_impl(int impl, int bits, size_t nbytes)
 {

@@ -59,13 +59,13 @@ int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 
 /* ---- implementation selection ------------------------------------------- */
 #define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for CTR calls >= 2 GiB (AES-256:
-                               >= 1 GiB), the split below for ECB / CBC / CFB decrypt >= 1 GiB, T-table otherwise
+                               >= 1 GiB), the split below for ECB / CBC / CFB decrypt >= 896 MiB, T-table otherwise
                                (OTC_IMPL=ttable|bitslice|split env overrides for the whole process) */
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
 #define OTC_IMPL_BITSLICE 2 /* 32-block-per-lane bitsliced VALU kernel */
 #define OTC_IMPL_SPLIT 3    /* ECB, CBC-decrypt and CFB-decrypt: both kernels CONCURRENTLY on disjoint ranges (the bitsliced
                                one on an auxiliary stream), co-resident on every CU -- LDS and VALU busy at
-                               once; "auto" for these calls >= 1 GiB.  CTR: as auto */
+                               once; "auto" for these calls >= 896 MiB.  CTR: as auto */
 
 /* The kernel family `impl` resolves to for a call of nbytes with a bits-bit
  * key (mode 1: CTR, 0: ECB encryption, 2: ECB / CBC decryption, 3: CFB128
@@ -141,7 +141,7 @@ int otc_aes_cfb128_decrypt_segments(const void *in, void *out, size_t seg_bytes,
 
 /* CFB128 decryption (parallel): P_i = C_i ^ E(C_{i-1}), C_{-1} = iv;
  * nbytes % 16 == 0; encryption key.  _impl: with a kernel choice (the plain
- * form is OTC_IMPL_AUTO: the T-table + bitsliced split from 1 GiB, like ECB
+ * form is OTC_IMPL_AUTO: the T-table + bitsliced split from 896 MiB, like ECB
  * encryption). */
 int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
                            const uint8_t iv[16], void *stream);

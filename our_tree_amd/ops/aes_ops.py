@@ -470,7 +470,7 @@ def ecb_encrypt(x: torch.Tensor, key: bytes, out=None, impl="auto") -> torch.Ten
 def ecb_decrypt(x: torch.Tensor, key: bytes, out=None, impl="auto") -> torch.Tensor:
     """ECB decryption: the T-table inverse cipher, the bitsliced one (the
     forward S-box as S^-1 = L S L), or both concurrently ("split", auto from
-    1 GiB)."""
+    896 MiB)."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     k = expand_key(key, decrypt=True)
@@ -532,7 +532,7 @@ def cfb128_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None, impl="auto"
     """Parallel CFB128 decryption, P_i = C_i ^ E(C_{i-1}) (encryption key).
     ``impl``: "ttable", "bitslice" (the forward bitsliced cipher on the input
     shifted one block), "split" (both at once, as ECB encryption) or "auto"
-    (split from 1 GiB).  In place runs through a copy of the input."""
+    (split from 896 MiB).  In place runs through a copy of the input."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     k = expand_key(key)

@@ -5,7 +5,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=gpurun_out/${1:-r4_small_split}
 mkdir -p $O
-for sz in 64M 256M 512M 1000M 2G; do
+for sz in ${SIZES:-64M 256M 512M 1000M 2G}; do
     for m in ecb ecb-dec cbc-dec; do
         ip=--inplace; [ $m = cbc-dec ] && ip=
         for i in ttable split; do

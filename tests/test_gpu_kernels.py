@@ -435,14 +435,14 @@ def test_bitslice_launch_structures(gpu, bits):
 def test_auto_routing_rule(gpu):
     """impl="auto" by size (docs/PERF.md, profiles/r3/auto_impl,
     profiles/r4/ecb_split): bitsliced CTR from 2 GiB (AES-128/192) or 1 GiB
-    (AES-256), the co-resident split for ECB encryption from 1 GiB, T-table
+    (AES-256), the co-resident split for ECB encryption from 896 MiB, T-table
     for everything else; the boundaries are exact.  "split" is an
     ECB-encryption form: for CTR it routes as auto."""
     G = 1 << 30
     cases = [(128, "ctr", 64 * G, "bitslice"), (128, "ctr", 2 * G - 16, "ttable"), (128, "ctr", 2 * G, "bitslice"),
              (256, "ctr", 1 * G, "bitslice"), (256, "ctr", 1 * G - 16, "ttable"), (256, "ctr", 4 * G, "bitslice"),
              (192, "ctr", 2 * G, "bitslice"), (192, "ctr", 2 * G - 16, "ttable"), (192, "ctr", 1 * G, "ttable"),
-             (256, "ecb", 64 * G, "split"), (128, "ecb", 1 * G, "split"), (192, "ecb", 1 * G - 16, "ttable"),
+             (256, "ecb", 64 * G, "split"), (128, "ecb", 896 << 20, "split"), (192, "ecb", (896 << 20) - 16, "ttable"),
              (128, "ctr", 16, "ttable")]
     for bits, mode, n, want in cases:
         assert ops.pick_impl("auto", bits, mode, n) == want, (bits, mode, n)
@@ -574,8 +574,8 @@ def test_bitsliced_decrypt_matches_ttable(gpu, bits):
         S = min(n, 1 << 14)
         assert host(t[:S]) == cpu_ref.ecb(key, host(x[:S]), decrypt=True)
         assert host(tc[:S]) == cpu_ref.cbc(key, iv, host(x[:S]), decrypt=True)
-    assert ops.pick_impl("auto", bits, "dec", 1 << 30) == "split"
-    assert ops.pick_impl("auto", bits, "dec", (1 << 30) - 16) == "ttable"
+    assert ops.pick_impl("auto", bits, "dec", 896 << 20) == "split"
+    assert ops.pick_impl("auto", bits, "dec", (896 << 20) - 16) == "ttable"
 
 
 @pytest.mark.parametrize("bits", [128, 192, 256])
@@ -603,8 +603,8 @@ def test_bitsliced_cfb_decrypt_matches_ttable(gpu, bits):
         assert host(t[:S]) == cpu_ref.cfb128(key, iv, host(x[:S]), decrypt=True)
         if n > S:  # the tail, with its predecessor block as the IV
             assert host(t[-S:]) == cpu_ref.cfb128(key, host(x[-S - 16:-S]), host(x[-S:]), decrypt=True)
-    assert ops.pick_impl("auto", bits, "cfb-dec", 1 << 30) == "split"
-    assert ops.pick_impl("auto", bits, "cfb-dec", (1 << 30) - 16) == "ttable"
+    assert ops.pick_impl("auto", bits, "cfb-dec", 896 << 20) == "split"
+    assert ops.pick_impl("auto", bits, "cfb-dec", (896 << 20) - 16) == "ttable"
 
 
 def test_ttable_modes_beyond_4gib(gpu):
