@@ -3,7 +3,7 @@
  * gfx950 kernels (the profiling target for rocprofv3).  Prints one JSON line
  * per configuration.
  *
- *   otbench --mode ctr|ecb|ecb-dec|cbc-dec|cbc-enc-seg|cfb-enc-seg|cfb-dec-seg|cfb-dec|ctr-stream|xor|rc4
+ *   otbench --mode ctr|ecb|ecb-dec|cbc-dec|cbc-enc-seg|cfb-enc-seg|cfb-dec-seg|cbc-dec-seg|cfb-dec|ctr-stream|xor|rc4
  *                  |ecb-split|ecbdec-split|cbcdec-split|cfbdec-split|ctr-split
  *           [--bits 128] [--bytes 1G] [--iters 20] [--warmup 3]
  *           [--impl auto|ttable|bitslice|split] [--inplace] [--verify] [--clock]
@@ -143,7 +143,9 @@ static int run_op(void *p)
     if (c.mode == "cfb-enc-seg")
         return otc_aes_cfb128_encrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
     if (c.mode == "cfb-dec-seg")
-        return otc_aes_cfb128_decrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
+        return otc_aes_cfb128_decrypt_segments_impl(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, c.impl, nullptr);
+    if (c.mode == "cbc-dec-seg")
+        return otc_aes_cbc_decrypt_segments_impl(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, c.impl, nullptr);
     if (c.mode == "cfb-dec") return otc_aes_cfb128_decrypt_impl(a->in, a->out, c.bytes, a->k, a->iv, c.impl, nullptr);
     if (c.mode == "xor") return otc_xor(a->in, a->out, a->out, c.bytes, nullptr);
     if (c.mode == "rc4") return otc_rc4_multi(a->keys, (int)c.keylen, c.streams, c.len, c.drop, a->in, a->out, nullptr);
@@ -162,7 +164,10 @@ struct Sample {
     uint64_t seg0 = 0;           /* segment modes: index of the first segment */
 };
 
-static bool is_seg_mode(const std::string &m) { return m == "cbc-enc-seg" || m == "cfb-enc-seg" || m == "cfb-dec-seg"; }
+static bool is_seg_mode(const std::string &m)
+{
+    return m == "cbc-enc-seg" || m == "cfb-enc-seg" || m == "cfb-dec-seg" || m == "cbc-dec-seg";
+}
 static bool chained_dec(const std::string &m)
 {
     return m == "cbc-dec" || m == "cfb-dec" || m == "cbcdec-split" || m == "cfbdec-split";
@@ -269,15 +274,18 @@ static bool oracle(const Cfg &c, const uint8_t key[32], const uint8_t iv0[16], c
         }
     } else if (is_seg_mode(m)) {
         /* segment q: IV_q = iv0 + q (128-bit BE add), its own chain */
-        aes_setkey_enc(&ctx, key, c.bits); /* CBC encrypt; CFB uses E() both ways */
+        if (m == "cbc-dec-seg")
+            aes_setkey_dec(&ctx, key, c.bits);
+        else
+            aes_setkey_enc(&ctx, key, c.bits); /* CBC encrypt; CFB uses E() both ways */
         for (size_t q = 0; q < s.len / c.seg; ++q) {
             uint8_t iv[16];
             memcpy(iv, iv0, 16);
             aes_ctr128_add(iv, s.seg0 + q);
             const uint8_t *qi = in + q * c.seg;
             uint8_t *qo = ref.data() + q * c.seg;
-            if (m == "cbc-enc-seg") {
-                aes_crypt_cbc(&ctx, AES_ENCRYPT, c.seg, iv, qi, qo);
+            if (m == "cbc-enc-seg" || m == "cbc-dec-seg") {
+                aes_crypt_cbc(&ctx, m == "cbc-enc-seg" ? AES_ENCRYPT : AES_DECRYPT, c.seg, iv, qi, qo);
             } else {
                 int iv_off = 0;
                 aes_crypt_cfb128(&ctx, m == "cfb-enc-seg" ? AES_ENCRYPT : AES_DECRYPT, c.seg, &iv_off, iv, qi, qo);
@@ -381,6 +389,7 @@ int main(int argc, char **argv)
         }
     }
     static const char *modes[] = {"ctr", "ecb", "ecb-dec", "cbc-dec", "cbc-enc-seg", "cfb-enc-seg", "cfb-dec-seg",
+                                  "cbc-dec-seg",
                                   "cfb-dec", "ctr-stream", "xor", "rc4", "ecb-split", "ecbdec-split", "cbcdec-split",
                                   "cfbdec-split", "ctr-split"};
     bool known = false;
@@ -402,7 +411,7 @@ int main(int argc, char **argv)
         fprintf(stderr, "--bytes leaves nothing to process\n");
         return 2;
     }
-    if (c.inplace && (chained_dec(c.mode) || c.mode == "cfb-dec-seg")) {
+    if (c.inplace && (chained_dec(c.mode) || c.mode == "cfb-dec-seg" || c.mode == "cbc-dec-seg")) {
         /* these read the previous ciphertext block: the library refuses in-place */
         fprintf(stderr, "%s cannot run in place\n", c.mode.c_str());
         return 2;
@@ -416,7 +425,7 @@ int main(int argc, char **argv)
     srand(1337);
     for (int i = 0; i < 32; ++i) key[i] = (uint8_t)rand();
     const bool dec = (c.mode == "ecb-dec" || c.mode == "cbc-dec" || c.mode == "ecbdec-split" ||
-                      c.mode == "cbcdec-split");
+                      c.mode == "cbcdec-split" || c.mode == "cbc-dec-seg");
     otc_aes_key k;
     if (otc_aes_key_init(&k, key, c.bits, dec ? OTC_DIR_DECRYPT : OTC_DIR_ENCRYPT)) {
         fprintf(stderr, "key: %s\n", otc_last_error());

@@ -130,6 +130,7 @@ static int segs(int which, const void *in, void *out, size_t seg, size_t nseg, c
         uint8_t *po = (uint8_t *)out + s * seg;
         int iv_off = 0;
         if (which == 0) aes_crypt_cbc(&c, AES_ENCRYPT, seg, iv, pi, po);
+        else if (which == 3) aes_crypt_cbc(&c, AES_DECRYPT, seg, iv, pi, po);
         else aes_crypt_cfb128(&c, which == 1 ? AES_ENCRYPT : AES_DECRYPT, seg, &iv_off, iv, pi, po);
     }
     return OTC_OK;
@@ -150,6 +151,17 @@ int otc_aes_cfb128_decrypt_segments(const void *in, void *out, size_t seg, size_
 {
     if (in == out) return fail(OTC_ERR_ARG, "cfb decrypt in place");
     return segs(2, in, out, seg, nseg, k, iv0);
+}
+int otc_aes_cfb128_decrypt_segments_impl(const void *in, void *out, size_t seg, size_t nseg, const otc_aes_key *k,
+                                         const uint8_t iv0[16], int, void *st)
+{
+    return otc_aes_cfb128_decrypt_segments(in, out, seg, nseg, k, iv0, st);
+}
+int otc_aes_cbc_decrypt_segments_impl(const void *in, void *out, size_t seg, size_t nseg, const otc_aes_key *k,
+                                      const uint8_t iv0[16], int, void *)
+{
+    if (in == out) return fail(OTC_ERR_ARG, "cbc decrypt in place");
+    return segs(3, in, out, seg, nseg, k, iv0);
 }
 
 int otc_aes_cfb128_decrypt(const void *in, void *out, size_t n, const otc_aes_key *k, const uint8_t iv[16], void *);

@@ -77,7 +77,14 @@ struct BsParams {
                              split's second part); otherwise block 0's predecessor is iv */
     uint32_t iv[4];       /* CBC / CFB decrypt: IV as LE words */
     SplitClaim cl;        /* k_aes_bs_claim: units taken from the front of the buffer */
+    Ctr128 iv0;           /* *_SEG: IV of segment 0 (numeric BE; IV_s = iv0 + s) */
+    uint32_t seg_shift;   /* *_SEG: log2(blocks per segment) */
 };
+
+/* mode families: the CBC / CFB decryptions, whole-stream or per segment */
+template <int MODE> constexpr bool is_cbcd = MODE == BS_CBC_DEC || MODE == BS_CBC_DEC_SEG;
+template <int MODE> constexpr bool is_cfbd = MODE == BS_CFB_DEC || MODE == BS_CFB_DEC_SEG;
+template <int MODE> constexpr bool is_seg = MODE == BS_CBC_DEC_SEG || MODE == BS_CFB_DEC_SEG;
 
 /* Which tasks a launch runs.  The bulk launch (BS_FULL_ONLY) takes only tasks
  * whose 2048 slots are all in range and is compiled knowing it: its load and
@@ -102,6 +109,27 @@ __device__ __forceinline__ uint4 blend_iv(uint4 v, bool first, const BsParams &P
     v.y = (v.y & ~m) | (P.iv[1] & m);
     v.z = (v.z & ~m) | (P.iv[2] & m);
     v.w = (v.w & ~m) | (P.iv[3] & m);
+    return v;
+}
+
+/* *_SEG: the block a slot reads one block back, or -- for lanes at a segment
+ * start -- its own block with IV_s blended in.  The IV is built only when a
+ * lane of the wave is at a segment start in this slot (a uniform branch: with
+ * segments of >= 64 blocks, one slot in seg/64). */
+template <int MODE>
+__device__ __forceinline__ uint4 seg_prev(const BsParams &P, const uint8_t *own, uint64_t i, bool ok)
+{
+    const bool first = (i & ((1ull << P.seg_shift) - 1)) == 0;
+    uint4 v = ok ? *(const uint4 *)(own - (first ? 0 : 16)) : make_uint4(0, 0, 0, 0);
+    if (__builtin_amdgcn_ballot_w64(first)) {
+        uint32_t w0, w1, w2, w3;
+        ctr_words(P.iv0, i >> P.seg_shift, false, w0, w1, w2, w3);
+        const uint32_t m = 0u - (uint32_t)first;
+        v.x = (v.x & ~m) | (w0 & m);
+        v.y = (v.y & ~m) | (w1 & m);
+        v.z = (v.z & ~m) | (w2 & m);
+        v.w = (v.w & ~m) | (w3 & m);
+    }
     return v;
 }
 
@@ -152,14 +180,16 @@ __device__ __forceinline__ bool task_of(const BsParams &P, Task &t, int64_t clai
 template <int MODE>
 __device__ __forceinline__ void ecb_load_planes(const BsParams &P, const Task &t, W *s, bool full)
 {
-    constexpr int64_t BACK = MODE == BS_CFB_DEC ? 16 : 0;
+    constexpr int64_t BACK = MODE == BS_CFB_DEC ? 16 : 0; /* the segment form reads through seg_prev */
     const uint8_t *tb = P.in + (int64_t)(t.vbase * 16) - BACK;
     const uint32_t lo = t.lane * 16u;
     uint4 blk[32];
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
         const uint64_t i = t.vbase + t.lane + 64u * k;
-        if (MODE == BS_CFB_DEC && k == 0) {
+        if constexpr (MODE == BS_CFB_DEC_SEG) {
+            blk[k] = seg_prev<MODE>(P, tb + lo + 1024u * k, i, full || i < P.nblocks);
+        } else if (MODE == BS_CFB_DEC && k == 0) {
             /* only slot 0 of lane 0 of task 0 can be block 0: it loads block 0
              * itself (a valid address) and takes the IV instead */
             const bool first = !P.has_prev && i == 0;
@@ -403,7 +433,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
     } else {
         ecb_load_planes<MODE>(P, t, s, full);
     }
-    constexpr bool DEC = MODE == BS_ECB_DEC || MODE == BS_CBC_DEC;
+    constexpr bool DEC = MODE == BS_ECB_DEC || is_cbcd<MODE>;
     if (DEC) {
         dec_premap(s); /* L on every ciphertext byte */
         pin_n(s, 128);
@@ -432,12 +462,14 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
     /* the block XORed into the output: CTR the plaintext, CBC decrypt the
      * previous ciphertext block (the IV for block 0 of a whole-stream call),
      * CFB decrypt the ciphertext block itself */
-    constexpr bool XIN = MODE == BS_CTR || MODE == BS_CBC_DEC || MODE == BS_CFB_DEC;
+    constexpr bool XIN = MODE == BS_CTR || is_cbcd<MODE> || is_cfbd<MODE>;
     constexpr int XOFF = MODE == BS_CBC_DEC ? -16 : 0;
     uint4 pt[32];
     auto issue = [&](int j) {
         if (XIN && j >= LS && j < 32) {
-            if (MODE == BS_CBC_DEC && j == 0) {
+            if constexpr (MODE == BS_CBC_DEC_SEG) {
+                pt[j] = seg_prev<MODE>(P, ib + lo + 1024u * j, (uint64_t)(tstart + lane + 64 * j), slot_ok(j));
+            } else if (MODE == BS_CBC_DEC && j == 0) {
                 /* block 0 of a whole-stream call XORs with the IV: it loads
                  * itself (a valid address) and blends the IV in */
                 const bool first = !P.has_prev && tstart + lane == 0;
@@ -451,8 +483,8 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
     /* CBC / CFB decrypt load all 32 XOR blocks into registers (CTR stages 8 in
      * LDS): few slots ahead (CBC 4, CFB 2: 163 VGPRs, no scratch; 4 spills),
      * none early, or the output phase spills */
-    constexpr bool REG_XIN = MODE == BS_CBC_DEC || MODE == BS_CFB_DEC;
-    constexpr int PRE_ = REG_XIN ? 0 : PRE, D_ = MODE == BS_CFB_DEC ? OTC_BS_CFB_D : REG_XIN ? 4 : D;
+    constexpr bool REG_XIN = is_cbcd<MODE> || is_cfbd<MODE>;
+    constexpr int PRE_ = REG_XIN ? 0 : PRE, D_ = is_cfbd<MODE> ? OTC_BS_CFB_D : REG_XIN ? 4 : D;
 #pragma unroll
     for (int j = 0; j < LS + PRE_; ++j) issue(j);
     sched_fence();
@@ -563,7 +595,7 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     }
     if (!cache) e = alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&tab, kt_words * 4, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_bs_key_table<MODE == BS_ECB_DEC || MODE == BS_CBC_DEC>, dim3(1), dim3(256), 0, st, K, tab);
+    hipLaunchKernelGGL(k_bs_key_table<MODE == BS_ECB_DEC || is_cbcd<MODE>>, dim3(1), dim3(256), 0, st, K, tab);
     BsParams Q = P;
     Q.ktab = tab;
     Q.tasks = tasks;
@@ -583,33 +615,40 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
             return e != hipSuccess ? e : f;
         }
     }
-    auto run = [&](auto cachec) {
-        constexpr bool C = decltype(cachec)::value;
-        Q.part = BS_FULL_ONLY;
-        hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, true>), g, b, 0, st, Q, K);
-        if (edge) {
-            Q.part = BS_EDGE_ONLY;
-            hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, false>), dim3(1), b, 0, st, Q, K);
-        }
-    };
-    /* counter caching exists for CTR only: no ECB kernels are instantiated
-     * with it */
-    if constexpr (MODE == BS_CTR) {
-        if (cache) {
-            uint32_t *gt = tab + kt_words, *e0 = gt + ngroups * OTC_BS_CTR_GRP_WORDS,
-                     *e1 = e0 + ngroups * OTC_BS_CTR_E0_WORDS;
-            Q.ctab = gt;
-            Q.e0tab = e0;
-            Q.e1tab = e1;
-            const uint64_t n = ngroups * 65 + tasks;
-            hipLaunchKernelGGL(k_bs_ctr_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, P.cbase,
-                               P.wrap64, ngroups, tasks, gt, e0, e1);
-            run(std::true_type{});
+    if constexpr (is_seg<MODE>) {
+        /* the segment modes run only as the claimed split's bitsliced half */
+        (void)edge;
+        (void)hipFreeAsync(tab, st);
+        return hipErrorInvalidValue;
+    } else {
+        auto run = [&](auto cachec) {
+            constexpr bool C = decltype(cachec)::value;
+            Q.part = BS_FULL_ONLY;
+            hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, true>), g, b, 0, st, Q, K);
+            if (edge) {
+                Q.part = BS_EDGE_ONLY;
+                hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, false>), dim3(1), b, 0, st, Q, K);
+            }
+        };
+        /* counter caching exists for CTR only: no ECB kernels are instantiated
+         * with it */
+        if constexpr (MODE == BS_CTR) {
+            if (cache) {
+                uint32_t *gt = tab + kt_words, *e0 = gt + ngroups * OTC_BS_CTR_GRP_WORDS,
+                         *e1 = e0 + ngroups * OTC_BS_CTR_E0_WORDS;
+                Q.ctab = gt;
+                Q.e0tab = e0;
+                Q.e1tab = e1;
+                const uint64_t n = ngroups * 65 + tasks;
+                hipLaunchKernelGGL(k_bs_ctr_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, P.cbase,
+                                   P.wrap64, ngroups, tasks, gt, e0, e1);
+                run(std::true_type{});
+            } else {
+                run(std::false_type{});
+            }
         } else {
             run(std::false_type{});
         }
-    } else {
-        run(std::false_type{});
     }
     e = hipGetLastError();
     const hipError_t f = hipFreeAsync(tab, st);
@@ -727,6 +766,25 @@ hipError_t bs_claim(int mode, const void *in, void *out, uint64_t nblocks, const
     case BS_ECB_DEC: return launch<BS_ECB_DEC>(P, K, st);
     case BS_CBC_DEC: return launch<BS_CBC_DEC>(P, K, st);
     case BS_CFB_DEC: return launch<BS_CFB_DEC>(P, K, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+/* ... and of a claimed split over independent segments of 2^seg_shift
+ * blocks, segment s chained from IV_s = iv0 + s */
+hipError_t bs_claim_seg(int mode, const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, Ctr128 iv0,
+                        uint32_t seg_shift, SplitClaim cl, hipStream_t st)
+{
+    BsParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nblocks = nblocks;
+    P.iv0 = iv0;
+    P.seg_shift = seg_shift;
+    P.cl = cl;
+    switch (mode) {
+    case BS_CBC_DEC_SEG: return launch<BS_CBC_DEC_SEG>(P, K, st);
+    case BS_CFB_DEC_SEG: return launch<BS_CFB_DEC_SEG>(P, K, st);
     default: return hipErrorInvalidValue;
     }
 }

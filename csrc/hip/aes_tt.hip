@@ -415,6 +415,11 @@ __global__ __launch_bounds__(1024) void k_aes_cfb_tt_claim(EncParams P, otc_aes_
 {
     enc_tt_body<NR, E_CFB_DEC, OTC_TT_CLAIM_B, 1024, true>(P, K);
 }
+template <int NR>
+__global__ __launch_bounds__(1024) void k_aes_cfbseg_tt_claim(EncParams P, otc_aes_key K)
+{
+    enc_tt_body<NR, E_CFB_DEC_SEG, OTC_TT_CLAIM_B, 1024, true>(P, K);
+}
 
 /* ---------------------------------------------------------------------------
  * CTR with counter-mode caching.
@@ -1217,15 +1222,18 @@ hipError_t launch_enc_claim(const EncParams &P, const otc_aes_key &K, hipStream_
     switch (K.nr) {
     case 10:
         if constexpr (MODE == E_ECB) hipLaunchKernelGGL((k_aes_ecb_tt_claim<10>), g, b, 0, st, P, K);
-        else hipLaunchKernelGGL((k_aes_cfb_tt_claim<10>), g, b, 0, st, P, K);
+        else if constexpr (MODE == E_CFB_DEC) hipLaunchKernelGGL((k_aes_cfb_tt_claim<10>), g, b, 0, st, P, K);
+        else hipLaunchKernelGGL((k_aes_cfbseg_tt_claim<10>), g, b, 0, st, P, K);
         break;
     case 12:
         if constexpr (MODE == E_ECB) hipLaunchKernelGGL((k_aes_ecb_tt_claim<12>), g, b, 0, st, P, K);
-        else hipLaunchKernelGGL((k_aes_cfb_tt_claim<12>), g, b, 0, st, P, K);
+        else if constexpr (MODE == E_CFB_DEC) hipLaunchKernelGGL((k_aes_cfb_tt_claim<12>), g, b, 0, st, P, K);
+        else hipLaunchKernelGGL((k_aes_cfbseg_tt_claim<12>), g, b, 0, st, P, K);
         break;
     case 14:
         if constexpr (MODE == E_ECB) hipLaunchKernelGGL((k_aes_ecb_tt_claim<14>), g, b, 0, st, P, K);
-        else hipLaunchKernelGGL((k_aes_cfb_tt_claim<14>), g, b, 0, st, P, K);
+        else if constexpr (MODE == E_CFB_DEC) hipLaunchKernelGGL((k_aes_cfb_tt_claim<14>), g, b, 0, st, P, K);
+        else hipLaunchKernelGGL((k_aes_cfbseg_tt_claim<14>), g, b, 0, st, P, K);
         break;
     default: return hipErrorInvalidValue;
     }
@@ -1425,6 +1433,35 @@ hipError_t tt_cbc_decrypt_claim(const void *in, void *out, uint64_t nblocks, con
     P.iv = iv;
     P.cl = cl;
     return launch_dec_claim<D_CBC>(P, K, st);
+}
+
+/* the T-table halves of a claimed split over power-of-two segments
+ * (2^seg_shift blocks, IV_s = iv0 + s) */
+hipError_t tt_cbc_decrypt_seg_claim(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, Ctr128 iv0,
+                                    uint32_t seg_shift, SplitClaim cl, hipStream_t st)
+{
+    DecParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nblocks;
+    P.iv = iv0;
+    P.seg_shift = seg_shift;
+    P.cl = cl;
+    return launch_dec_claim<D_CBC_SEG>(P, K, st);
+}
+
+hipError_t tt_cfb_decrypt_seg_claim(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, Ctr128 iv0,
+                                    uint32_t seg_shift, SplitClaim cl, hipStream_t st)
+{
+    EncParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nblocks;
+    P.ctr = iv0;
+    P.seg_blocks = 1ull << seg_shift;
+    P.seg_shift = seg_shift;
+    P.cl = cl;
+    return launch_enc_claim<E_CFB_DEC_SEG>(P, K, st);
 }
 
 hipError_t tt_cbc_decrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,

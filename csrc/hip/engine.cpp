@@ -42,6 +42,8 @@ using otc_dev::BS_ECB;
 using otc_dev::BS_ECB_DEC;
 using otc_dev::BS_CBC_DEC;
 using otc_dev::BS_CFB_DEC;
+using otc_dev::BS_CBC_DEC_SEG;
+using otc_dev::BS_CFB_DEC_SEG;
 
 namespace otc_impl {
 hipError_t tt_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
@@ -66,6 +68,12 @@ hipError_t tt_cfb_decrypt_claim(const void *, void *, uint64_t, const otc_aes_ke
                                 hipStream_t);
 hipError_t tt_ecb_decrypt_claim(const void *, void *, uint64_t, const otc_aes_key &, SplitClaim, hipStream_t);
 hipError_t tt_cbc_decrypt_claim(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, SplitClaim, hipStream_t);
+hipError_t bs_claim_seg(int, const void *, void *, uint64_t, const otc_aes_key &, Ctr128, uint32_t, SplitClaim,
+                        hipStream_t);
+hipError_t tt_cbc_decrypt_seg_claim(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, uint32_t, SplitClaim,
+                                    hipStream_t);
+hipError_t tt_cfb_decrypt_seg_claim(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, uint32_t, SplitClaim,
+                                    hipStream_t);
 hipError_t tt_ctr_batch(const otc_ctr_msg *, const otc_aes_key *, const uint32_t *, const uint64_t *, uint64_t, int, int,
                         hipStream_t);
 hipError_t k_xor(const void *, const void *, void *, size_t, hipStream_t);
@@ -336,6 +344,47 @@ hipError_t cfb_dec_split(const void *in, void *out, uint64_t nblocks, const otc_
         nblocks, st, ran, [&](SplitClaim cl) { return otc_impl::tt_cfb_decrypt_claim(in, out, nblocks, K, ivw, cl, st); },
         [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_CFB_DEC, in, out, nblocks, K, ivw, cl, s); },
         [&](uint64_t n) { return otc_impl::tt_cfb_decrypt(in, out, n, K, ivw, st); });
+}
+
+/* Segment decryption (CBC / CFB128 over independent segments of 2^shift
+ * blocks, IV_s = iv0 + s): the same split, each kernel computing the segment
+ * IVs itself.  Non-power-of-two segments and short calls: the T-table. */
+int seg_shift_of(size_t seg_blocks)
+{
+    if (seg_blocks == 0 || (seg_blocks & (seg_blocks - 1))) return -1;
+    int sh = 0;
+    while (((size_t)1 << sh) < seg_blocks) ++sh;
+    return sh;
+}
+
+int pick_seg_impl(int impl, int bits, size_t nbytes, size_t seg_blocks)
+{
+    if (seg_shift_of(seg_blocks) < 0) return OTC_IMPL_TTABLE;
+    /* the bitsliced segment kernels run only as the split's half */
+    if (impl == OTC_IMPL_BITSLICE) return OTC_IMPL_SPLIT;
+    const int p = pick_ecb_impl(impl, bits, nbytes);
+    return p == OTC_IMPL_BITSLICE ? OTC_IMPL_SPLIT : p;
+}
+
+hipError_t seg_dec_split(bool cfb, const void *in, void *out, size_t seg_blocks, size_t nseg, const otc_aes_key &K,
+                         Ctr128 iv0, hipStream_t st, int *ran)
+{
+    const uint64_t nblocks = (uint64_t)seg_blocks * nseg;
+    const uint32_t sh = (uint32_t)seg_shift_of(seg_blocks);
+    auto plain = [&](uint64_t) {
+        return cfb ? otc_impl::tt_cfb_decrypt_seg(in, out, seg_blocks, nseg, K, iv0, st)
+                   : otc_impl::tt_cbc_decrypt_seg(in, out, seg_blocks, nseg, K, iv0, st);
+    };
+    return split_claim(
+        nblocks, st, ran,
+        [&](SplitClaim cl) {
+            return cfb ? otc_impl::tt_cfb_decrypt_seg_claim(in, out, nblocks, K, iv0, sh, cl, st)
+                       : otc_impl::tt_cbc_decrypt_seg_claim(in, out, nblocks, K, iv0, sh, cl, st);
+        },
+        [&](SplitClaim cl, hipStream_t s) {
+            return otc_impl::bs_claim_seg(cfb ? BS_CFB_DEC_SEG : BS_CBC_DEC_SEG, in, out, nblocks, K, iv0, sh, cl, s);
+        },
+        plain);
 }
 
 /* the kernel family the calling thread's last AES call ran (otc_last_impl) */
@@ -637,8 +686,8 @@ extern "C" int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t se
     return OTC_OK;
 }
 
-extern "C" int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
-                                            const otc_aes_key *k, const uint8_t iv0[16], void *stream)
+extern "C" int otc_aes_cbc_decrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                                 const otc_aes_key *k, const uint8_t iv0[16], int impl, void *stream)
 {
     Range rg("otc_aes_cbc_decrypt_segments");
     int r = check_key(k, OTC_DIR_DECRYPT);
@@ -649,10 +698,22 @@ extern "C" int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t se
     if (!iv0) return set_err(OTC_ERR_ARG, "null iv");
     if (nseg && seg_bytes > SIZE_MAX / nseg) return set_err(OTC_ERR_ARG, "size overflow");
     if ((r = check_bufs(in, out, seg_bytes * nseg, false, "aes_cbc_decrypt_segments"))) return r;
+    if ((r = check_impl(impl))) return r;
     if (nseg == 0) return OTC_OK;
-    hipError_t e = otc_impl::tt_cbc_decrypt_seg(in, out, sb, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream);
+    hipError_t e;
+    g_last_impl = pick_seg_impl(impl, k->bits, seg_bytes * nseg, sb);
+    if (g_last_impl == OTC_IMPL_SPLIT)
+        e = seg_dec_split(false, in, out, sb, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream, &g_last_impl);
+    else
+        e = otc_impl::tt_cbc_decrypt_seg(in, out, sb, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "cbc_decrypt_segments launch");
     return OTC_OK;
+}
+
+extern "C" int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                            const otc_aes_key *k, const uint8_t iv0[16], void *stream)
+{
+    return otc_aes_cbc_decrypt_segments_impl(in, out, seg_bytes, nseg, k, iv0, OTC_IMPL_AUTO, stream);
 }
 
 /* CFB128 over independent segments (IV_s = iv0 + s, like the CBC sector
@@ -660,7 +721,8 @@ extern "C" int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t se
  * sector kernel with the CFB chain step); decryption is fully parallel with
  * IV_s at every segment start.  Both use the ENCRYPTION key schedule. */
 static int cfb_seg_common(const void *in, void *out, size_t seg_bytes, size_t nseg, const otc_aes_key *k,
-                          const uint8_t iv0[16], void *stream, bool decrypt, const char *what)
+                          const uint8_t iv0[16], void *stream, bool decrypt, const char *what,
+                          int impl = OTC_IMPL_AUTO)
 {
     int r = check_key(k, OTC_DIR_ENCRYPT);
     if (r) return r;
@@ -670,11 +732,20 @@ static int cfb_seg_common(const void *in, void *out, size_t seg_bytes, size_t ns
     /* decrypt reads block i-1 of the input while another lane writes block
      * i-1 of the output: in place only for encryption (lane-private chains) */
     if ((r = check_bufs(in, out, seg_bytes * nseg, !decrypt, what))) return r;
+    if ((r = check_impl(impl))) return r;
     if (nseg == 0 || seg_bytes == 0) return OTC_OK;
-    hipError_t e = decrypt ? otc_impl::tt_cfb_decrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
-                                                          (hipStream_t)stream)
-                           : otc_impl::tt_cfb_encrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
-                                                          (hipStream_t)stream);
+    hipError_t e;
+    if (decrypt) {
+        g_last_impl = pick_seg_impl(impl, k->bits, seg_bytes * nseg, seg_bytes / 16);
+        if (g_last_impl == OTC_IMPL_SPLIT)
+            e = seg_dec_split(true, in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream,
+                              &g_last_impl);
+        else
+            e = otc_impl::tt_cfb_decrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
+                                             (hipStream_t)stream);
+    } else {
+        e = otc_impl::tt_cfb_encrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream);
+    }
     if (e != hipSuccess) return hip_fail(e, what);
     return OTC_OK;
 }
@@ -686,11 +757,18 @@ extern "C" int otc_aes_cfb128_encrypt_segments(const void *in, void *out, size_t
     return cfb_seg_common(in, out, seg_bytes, nseg, k, iv0, stream, false, "cfb128_encrypt_segments");
 }
 
+extern "C" int otc_aes_cfb128_decrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                                    const otc_aes_key *k, const uint8_t iv0[16], int impl,
+                                                    void *stream)
+{
+    Range rg("otc_aes_cfb128_decrypt_segments");
+    return cfb_seg_common(in, out, seg_bytes, nseg, k, iv0, stream, true, "cfb128_decrypt_segments", impl);
+}
+
 extern "C" int otc_aes_cfb128_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                                const otc_aes_key *k, const uint8_t iv0[16], void *stream)
 {
-    Range rg("otc_aes_cfb128_decrypt_segments");
-    return cfb_seg_common(in, out, seg_bytes, nseg, k, iv0, stream, true, "cfb128_decrypt_segments");
+    return otc_aes_cfb128_decrypt_segments_impl(in, out, seg_bytes, nseg, k, iv0, OTC_IMPL_AUTO, stream);
 }
 
 extern "C" int otc_aes_cfb128_decrypt_impl(const void *in, void *out, size_t nbytes, const otc_aes_key *k,

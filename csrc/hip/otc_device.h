@@ -108,7 +108,11 @@ __device__ __forceinline__ void ctr_words(const Ctr128 &c, uint64_t idx, bool wr
  * otc_invmix.h) with a decryption key; BS_CFB_DEC: CFB128 decryption, P_i =
  * E(C_{i-1}) ^ C_i -- the forward cipher on the input shifted back one block,
  * XORed with the input */
-enum : int { BS_CTR = 0, BS_ECB = 1, BS_ECB_DEC = 2, BS_CBC_DEC = 3, BS_CFB_DEC = 4 };
+enum : int { BS_CTR = 0, BS_ECB = 1, BS_ECB_DEC = 2, BS_CBC_DEC = 3, BS_CFB_DEC = 4,
+              /* CBC / CFB decryption of independent power-of-two segments:
+               * block i of a segment start takes IV_s = iv0 + s (128-bit BE)
+               * instead of block i-1 */
+              BS_CBC_DEC_SEG = 5, BS_CFB_DEC_SEG = 6 };
 
 /* Work claiming of a co-resident split (engine.cpp split_claim): the T-table
  * and the bitsliced kernel take 2048-block units of ONE buffer from a shared

@@ -126,9 +126,14 @@ int otc_aes_cbc_decrypt_impl(const void *in, void *out, size_t nbytes, const otc
  * A single segment (nseg == 1) is exact single-stream CBC, serial. */
 int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                  const otc_aes_key *k, const uint8_t iv0[16], void *stream);
-/* Same, decryption side (fully parallel). */
+/* Same, decryption side (fully parallel).  _impl: with a kernel choice --
+ * "auto" runs the T-table + bitsliced split for >= 896 MiB of power-of-two
+ * segments (OTC_IMPL_BITSLICE means the split here: the bitsliced segment
+ * kernels run only beside the T-table); other segment sizes: T-table. */
 int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                  const otc_aes_key *k, const uint8_t iv0[16], void *stream);
+int otc_aes_cbc_decrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                      const otc_aes_key *k, const uint8_t iv0[16], int impl, void *stream);
 
 /* CFB128 over nseg independent segments of seg_bytes (multiple of 16) with
  * IV_s = iv0 + s (128-bit BE add) -- the parallel form of the serial CFB
@@ -138,6 +143,8 @@ int otc_aes_cfb128_encrypt_segments(const void *in, void *out, size_t seg_bytes,
                                     const otc_aes_key *k, const uint8_t iv0[16], void *stream);
 int otc_aes_cfb128_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                     const otc_aes_key *k, const uint8_t iv0[16], void *stream);
+int otc_aes_cfb128_decrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                         const otc_aes_key *k, const uint8_t iv0[16], int impl, void *stream);
 
 /* CFB128 decryption (parallel): P_i = C_i ^ E(C_{i-1}), C_{-1} = iv;
  * nbytes % 16 == 0; encryption key.  _impl: with a kernel choice (the plain

@@ -180,6 +180,8 @@ def _declare_gpu(lib):
         "otc_aes_cfb128_decrypt_impl": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_int, c_vp]),
         "otc_aes_cfb128_encrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cfb128_decrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
+        "otc_aes_cfb128_decrypt_segments_impl": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_int, c_vp]),
+        "otc_aes_cbc_decrypt_segments_impl": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_int, c_vp]),
         "otc_aes_ctr_batch": (c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_int, c_int, c_vp]),
         "otc_xor": (c_int, [c_vp, c_vp, c_vp, c_sz, c_vp]),
         "otc_rc4_multi": (c_int, [c_vp, c_int, c_sz, c_sz, c_sz, c_vp, c_vp, c_vp]),

@@ -514,7 +514,12 @@ def cbc_encrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes:
     return out
 
 
-def cbc_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None) -> torch.Tensor:
+def cbc_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None,
+                         impl="auto") -> torch.Tensor:
+    """Inverse of ``cbc_encrypt_segments``: fully parallel.  ``impl``:
+    "ttable", or "split" / "bitslice" (the T-table + bitsliced split: the
+    bitsliced segment kernel runs only beside the T-table), "auto" = split
+    from 896 MiB of power-of-two segments."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     n = _nbytes(x)
@@ -522,8 +527,8 @@ def cbc_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes:
         raise ValueError("byte size must be a multiple of segment_bytes")
     k = expand_key(key, decrypt=True)
     with torch.cuda.device(x.device):
-        rc = _run(x, out, lambda ip, op: _lib().otc_aes_cbc_decrypt_segments(ip, op, segment_bytes, n // segment_bytes,
-            ctypes.byref(k), _b16(iv0, "iv0"), _stream(x)), inplace_ok=False)
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_cbc_decrypt_segments_impl(ip, op, segment_bytes,
+            n // segment_bytes, ctypes.byref(k), _b16(iv0, "iv0"), _impl(impl), _stream(x)), inplace_ok=False)
     _native.check(rc, "otc_aes_cbc_decrypt_segments")
     return out
 
@@ -563,6 +568,18 @@ def cfb128_encrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_byt
     return _seg_call("otc_aes_cfb128_encrypt_segments", x, key, iv0, segment_bytes, out, True)
 
 
-def cfb128_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None) -> torch.Tensor:
-    """Inverse of ``cfb128_encrypt_segments``: fully parallel."""
-    return _seg_call("otc_aes_cfb128_decrypt_segments", x, key, iv0, segment_bytes, out, False)
+def cfb128_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None,
+                            impl="auto") -> torch.Tensor:
+    """Inverse of ``cfb128_encrypt_segments``: fully parallel (``impl`` as
+    ``cbc_decrypt_segments``)."""
+    _check_dev(x, "x")
+    out = _out_like(x, out)
+    n = _nbytes(x)
+    if segment_bytes <= 0 or segment_bytes % 16 or n % segment_bytes:
+        raise ValueError("segment_bytes must be a positive multiple of 16 dividing the byte size")
+    k = expand_key(key)
+    with torch.cuda.device(x.device):
+        rc = _run(x, out, lambda ip, op: _lib().otc_aes_cfb128_decrypt_segments_impl(ip, op, segment_bytes,
+            n // segment_bytes, ctypes.byref(k), _b16(iv0, "iv0"), _impl(impl), _stream(x)), inplace_ok=False)
+    _native.check(rc, "otc_aes_cfb128_decrypt_segments")
+    return out

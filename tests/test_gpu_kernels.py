@@ -607,6 +607,39 @@ def test_bitsliced_cfb_decrypt_matches_ttable(gpu, bits):
     assert ops.pick_impl("auto", bits, "cfb-dec", (896 << 20) - 16) == "ttable"
 
 
+@pytest.mark.parametrize("bits", [128, 256])
+def test_segment_decrypt_split_matches_ttable(gpu, bits):
+    """CBC / CFB128 decryption of independent segments (IV_s = iv0 + s, a
+    carry across the low 64 bits of the IV included) through the claimed
+    split equals the T-table kernel and the CPU oracle, for segments of 1, 32,
+    256 and 4096 blocks, with a partial last unit; a non-power-of-two segment
+    size runs the T-table."""
+    key = os.urandom(bits // 8)
+    iv0 = os.urandom(8) + (2**64 - 3).to_bytes(8, "big")
+    for seg in (16, 512, 4096, 65536):
+        n = 16 * 2048 * 40 + (seg if seg <= 16 * 2048 else 0) * 3
+        n -= n % seg
+        x = torch.empty(n, dtype=torch.uint8, device=gpu)
+        ops.fill_random_(x, seed=seg ^ bits)
+        for name in ("cbc", "cfb"):
+            f = ops.cbc_decrypt_segments if name == "cbc" else ops.cfb128_decrypt_segments
+            t = f(x, key, iv0, seg, impl="ttable")
+            y = f(x, key, iv0, seg, impl="split")
+            torch.cuda.synchronize()
+            assert ops.last_impl() == "split", (name, seg)
+            assert torch.equal(y, t), (name, bits, seg)
+            hx, hy = host(x[:4 * seg]), host(y[:4 * seg])
+            ref = (cpu_ref.cbc_segments(key, iv0, hx, seg, decrypt=True) if name == "cbc"
+                   else cpu_ref.cfb128_segments(key, iv0, hx, seg, decrypt=True))
+            assert hy == ref, (name, bits, seg)
+    x = torch.empty(48 * 4096, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(x, seed=3)
+    y = ops.cbc_decrypt_segments(x, key, iv0, 48, impl="split")
+    torch.cuda.synchronize()
+    assert ops.last_impl() == "ttable"
+    assert host(y[:480]) == cpu_ref.cbc_segments(key, iv0, host(x[:480]), 48, decrypt=True)
+
+
 def test_ttable_modes_beyond_4gib(gpu):
     """T-table ECB encrypt / decrypt, CBC and CFB128 decrypt on a buffer
     above 4 GiB, checked against the oracle on samples at the head, across

@@ -16,9 +16,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "bin", "otbench_hostsim")
 
-MODES = ["ctr", "ecb", "ecb-dec", "cbc-dec", "cfb-dec", "cbc-enc-seg", "cfb-enc-seg", "cfb-dec-seg",
+MODES = ["ctr", "ecb", "ecb-dec", "cbc-dec", "cfb-dec", "cbc-enc-seg", "cfb-enc-seg", "cfb-dec-seg", "cbc-dec-seg",
          "ctr-stream", "xor", "rc4", "ecb-split", "ecbdec-split", "cbcdec-split", "cfbdec-split", "ctr-split"]
-NO_INPLACE = {"cbc-dec", "cfb-dec", "cfb-dec-seg", "cbcdec-split", "cfbdec-split"}
+NO_INPLACE = {"cbc-dec", "cfb-dec", "cfb-dec-seg", "cbc-dec-seg", "cbcdec-split", "cfbdec-split"}
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -65,7 +65,7 @@ def test_corrupted_sample_fails(mode, where):
         n, pos = 96 * 4096, {"head": 5, "mid": 48 * 4096 + 7, "tail": 96 * 4096 - 1}[where]
     else:
         n = 1000000 - (1000000 % 16 if mode not in ("ctr", "ctr-stream", "xor") else 0)
-        if mode in ("cbc-enc-seg", "cfb-enc-seg", "cfb-dec-seg"):
+        if mode in ("cbc-enc-seg", "cfb-enc-seg", "cfb-dec-seg", "cbc-dec-seg"):
             n -= n % 4096
         pos = {"head": 3, "mid": n // 2 + 1, "tail": n - 1}[where]
     inplace = [] if mode in NO_INPLACE else ["--inplace"]

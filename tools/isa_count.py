@@ -66,7 +66,8 @@ def main():
             ins = re.findall(r"^\s+([a-z_0-9]+)", f, re.M)
             cnt = lambda p: sum(1 for i in ins if i.startswith(p))
             tm = re.search(r"(?:t3|claim)ILi(\d+)ELi(\d)E", name)
-            mode = {"0": "CTR", "1": "ECB", "2": "ECB-dec", "3": "CBC-dec", "4": "CFB-dec"}.get(tm.group(2), "?") if tm else "?"
+            mode = {"0": "CTR", "1": "ECB", "2": "ECB-dec", "3": "CBC-dec", "4": "CFB-dec", "5": "CBC-dec-seg",
+                    "6": "CFB-dec-seg"}.get(tm.group(2), "?") if tm else "?"
             if mode == "CTR" and re.search(r"Lb0ELb1EEE", name):
                 mode = "CTR-nocache"  # fallback when the counter-caching tables do not fit
             if claim:
