@@ -7,10 +7,10 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=gpurun_out/${1:-r4_energy_table}
 mkdir -p $O
-for m in ctr ecb ecb-dec cbc-dec cfb-dec cbc-enc-seg cfb-enc-seg; do
+for m in ctr ecb ecb-dec cbc-dec cfb-dec cbc-enc-seg cfb-enc-seg cbc-dec-seg cfb-dec-seg; do
     for b in 128 192 256; do
         ip=--inplace
-        case $m in cbc-dec|cfb-dec) ip= ;; esac
+        case $m in cbc-dec|cfb-dec|cbc-dec-seg|cfb-dec-seg) ip= ;; esac
         timeout -k 10 150 python3 tools/power_run.py --label auto -- ./bin/otbench --mode $m --bits $b --bytes 4G $ip \
             --iters 700 --warmup 20 --verify --mark >> $O/energy.jsonl 2>> $O/err.txt || { tail -5 $O/err.txt; exit 1; }
     done

@@ -9,9 +9,9 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=gpurun_out/${1:-sweep}; mkdir -p $O
-for m in ctr ecb ecb-dec cbc-dec cfb-dec cbc-enc-seg cfb-enc-seg; do for b in 128 192 256; do
+for m in ctr ecb ecb-dec cbc-dec cfb-dec cbc-enc-seg cfb-enc-seg cbc-dec-seg cfb-dec-seg; do for b in 128 192 256; do
     ip=--inplace  # the chained decrypts read the previous ciphertext block: out of place
-    case $m in cbc-dec|cfb-dec) ip= ;; esac
+    case $m in cbc-dec|cfb-dec|cbc-dec-seg|cfb-dec-seg) ip= ;; esac
     timeout -k 10 120 ./bin/otbench --mode $m --bits $b --bytes 4G $ip --iters 100 --warmup 10 --clock --verify >> $O/sweep.jsonl || exit 1
 done; done
 # the ECB / decrypt paths at 64 GiB (32 GiB out of place for CBC), auto = the co-resident split
