@@ -339,6 +339,9 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
  * 81-LUT S-box (27 live planes at its peak) 4 early slots spilled in the
  * output phase; with the 79-LUT one (24) they no longer spill but measured
  * 1-1.5% slower, profiles/r3/sbox79; the 77-LUT one peaks at 23) */
+#ifndef OTC_BS_CBC_D
+#define OTC_BS_CBC_D 4
+#endif
 #ifndef OTC_BS_CFB_D
 #define OTC_BS_CFB_D 2
 #endif
@@ -484,7 +487,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
      * LDS): few slots ahead (CBC 4, CFB 2: 163 VGPRs, no scratch; 4 spills),
      * none early, or the output phase spills */
     constexpr bool REG_XIN = is_cbcd<MODE> || is_cfbd<MODE>;
-    constexpr int PRE_ = REG_XIN ? 0 : PRE, D_ = is_cfbd<MODE> ? OTC_BS_CFB_D : REG_XIN ? 4 : D;
+    constexpr int PRE_ = REG_XIN ? 0 : PRE, D_ = is_cfbd<MODE> ? OTC_BS_CFB_D : REG_XIN ? OTC_BS_CBC_D : D;
 #pragma unroll
     for (int j = 0; j < LS + PRE_; ++j) issue(j);
     sched_fence();
