@@ -339,6 +339,9 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
  * 81-LUT S-box (27 live planes at its peak) 4 early slots spilled in the
  * output phase; with the 79-LUT one (24) they no longer spill but measured
  * 1-1.5% slower, profiles/r3/sbox79; the 77-LUT one peaks at 23) */
+#ifndef OTC_BS_CLAIM_WGS
+#define OTC_BS_CLAIM_WGS 1 /* bitsliced claim workgroups per CU (one wave per SIMD beside the T-table's 4) */
+#endif
 #ifndef OTC_BS_CBC_D
 #define OTC_BS_CBC_D 4
 #endif
@@ -612,7 +615,8 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
     const bool edge = (MODE == BS_CTR && P.shift != 0) || vt % 2048 != 0;
     if constexpr (MODE != BS_CTR) {
         if (P.cl.ctr) { /* claimed split: one workgroup per CU beside the T-table's */
-            hipLaunchKernelGGL((k_aes_bs_claim<NR, MODE>), dim3((unsigned)otc_dev::device_cus()), b, 0, st, Q, K);
+            hipLaunchKernelGGL((k_aes_bs_claim<NR, MODE>), dim3((unsigned)otc_dev::device_cus() * OTC_BS_CLAIM_WGS), b,
+                               0, st, Q, K);
             e = hipGetLastError();
             const hipError_t f = hipFreeAsync(tab, st);
             return e != hipSuccess ? e : f;

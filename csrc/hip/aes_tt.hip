@@ -405,10 +405,13 @@ __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key
 #ifndef OTC_TT_CLAIM_B
 #define OTC_TT_CLAIM_B 2
 #endif
+#ifndef OTC_TT_ECB_CLAIM_B
+#define OTC_TT_ECB_CLAIM_B OTC_TT_ENC_B
+#endif
 template <int NR>
 __global__ __launch_bounds__(1024) void k_aes_ecb_tt_claim(EncParams P, otc_aes_key K)
 {
-    enc_tt_body<NR, E_ECB, OTC_TT_ENC_B, 1024, true>(P, K);
+    enc_tt_body<NR, E_ECB, OTC_TT_ECB_CLAIM_B, 1024, true>(P, K);
 }
 template <int NR>
 __global__ __launch_bounds__(1024) void k_aes_cfb_tt_claim(EncParams P, otc_aes_key K)
