@@ -305,7 +305,10 @@ hipError_t split_claim(uint64_t nblocks, hipStream_t st, int *ran, TT tt, BS bs,
         const hipError_t eb = bs(cl, a.s);
         if (eb != hipSuccess) (void)hipGetLastError();
         if ((e = hipEventRecord(a.join, a.s)) == hipSuccess) e = hipStreamWaitEvent(st, a.join, 0);
-        if (e == hipSuccess) *ran = eb == hipSuccess ? OTC_IMPL_SPLIT : OTC_IMPL_TTABLE;
+        if (e == hipSuccess)
+            *ran = eb == hipSuccess ? OTC_IMPL_SPLIT : OTC_IMPL_TTABLE;
+        else
+            (void)hipStreamSynchronize(a.s); /* no join on st: the counter must outlive the bitsliced kernel */
     }
     const hipError_t f = hipFreeAsync(ctr, st); /* after the join: both kernels are done with it */
     aux_give(a); /* reusable as soon as the work is enqueued: stream order */
