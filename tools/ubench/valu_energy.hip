@@ -4,20 +4,26 @@
 // (amd-smi) while it runs and derive energy per wave-instruction.
 //
 //   valu_energy OP SECONDS      OP in: xor_vv bitop3_vvv bitop3_vvs and_vv
-//                               bfi_vvv perm_vvv lshl_vi and_or_vvv ds_read_b32 nop
+//                               bfi_vvv perm_vvv lshl_vi and_or_vvv ds_read_b32 ds_read_u8
+//                               ds_addr nop
 // Prints one JSON line: wave-instructions per second of the chip.
 // Question it answers for the bitsliced AES kernel (power-limited): does a
 // 3-VGPR-operand v_bitop3_b32 cost more energy than a 2-operand v_xor_b32,
 // i.e. is the LUT3 cover (fewer, wider ops) also the lower-energy circuit?
+// Round 4 adds ds_read_u8 (the same conflict-free lookups, one byte each) and
+// ds_addr (their address arithmetic alone, no LDS access) to split a T-table
+// lookup's energy into LDS access and VALU, and to price a byte-table (S-box
+// in LDS, MixColumns in VALU) AES against the 32-bit T-table.
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
-enum { XOR_VV, BITOP3_VVV, BITOP3_VVS, AND_VV, BFI_VVV, PERM_VVV, LSHL_VI, AND_OR_VVV, DS_READ, NOP, NOPS };
-static const char *names[NOPS] = {"xor_vv",  "bitop3_vvv", "bitop3_vvs", "and_vv",      "bfi_vvv",
-                                  "perm_vvv", "lshl_vi",    "and_or_vvv", "ds_read_b32", "nop"};
+enum { XOR_VV, BITOP3_VVV, BITOP3_VVS, AND_VV, BFI_VVV, PERM_VVV, LSHL_VI, AND_OR_VVV, DS_READ, DS_READ_U8, DS_ADDR,
+       NOP, NOPS };
+static const char *names[NOPS] = {"xor_vv",  "bitop3_vvv", "bitop3_vvs", "and_vv",      "bfi_vvv",    "perm_vvv",
+                                  "lshl_vi", "and_or_vvv", "ds_read_b32", "ds_read_u8", "ds_addr",    "nop"};
 
 template <int OP>
 __global__ __launch_bounds__(256) void k_op(unsigned *out, int iters, unsigned sk)
@@ -29,7 +35,7 @@ __global__ __launch_bounds__(256) void k_op(unsigned *out, int iters, unsigned s
     /* ds_read_b32: 32 KiB per workgroup, lane l reads bank l mod 32 of a
      * data-dependent row (conflict-free, like the T-table kernel's lookups) */
     __shared__ unsigned lds[8192];
-    if (OP == DS_READ) {
+    if (OP == DS_READ || OP == DS_READ_U8) {
         for (int q = threadIdx.x; q < 8192; q += 256) lds[q] = q * 2654435761u;
         __syncthreads();
     }
@@ -49,6 +55,14 @@ __global__ __launch_bounds__(256) void k_op(unsigned *out, int iters, unsigned s
                 if (OP == AND_OR_VVV) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b), "v"(c));
                 if (OP == DS_READ) /* 8 chains in flight, one wait per round of them (hipcc) */
                     a[j] = lds[((a[j] & 0xFFu) << 5) | lane_off];
+                if (OP == DS_READ_U8) /* byte (a >> 8) & 3 of the same dword: same bank, one byte */
+                    a[j] = ((const unsigned char *)lds)[((((a[j] & 0xFFu) << 5) | lane_off) << 2) | ((a[j] >> 8) & 3u)] +
+                           (a[j] << 8);
+                if (OP == DS_ADDR) { /* the ds_read_b32 chain's address arithmetic alone */
+                    unsigned ad = ((a[j] & 0xFFu) << 5) | lane_off;
+                    asm volatile("" : "+v"(ad));
+                    a[j] = ad ^ (a[j] >> 3);
+                }
                 if (OP == NOP) asm volatile("s_nop 0" : "+v"(a[j]));
             }
         }
@@ -104,6 +118,8 @@ int main(int argc, char **argv)
     case LSHL_VI: r = run<LSHL_VI>(cus, out, secs); break;
     case AND_OR_VVV: r = run<AND_OR_VVV>(cus, out, secs); break;
     case DS_READ: r = run<DS_READ>(cus, out, secs); break;
+    case DS_READ_U8: r = run<DS_READ_U8>(cus, out, secs); break;
+    case DS_ADDR: r = run<DS_ADDR>(cus, out, secs); break;
     case NOP: r = run<NOP>(cus, out, secs); break;
     }
     if (r < 0) return 1;
