@@ -640,11 +640,13 @@ def test_segment_decrypt_split_matches_ttable(gpu, bits):
     assert host(y[:480]) == cpu_ref.cbc_segments(key, iv0, host(x[:480]), 48, decrypt=True)
 
 
-def test_ttable_modes_beyond_4gib(gpu):
-    """T-table ECB encrypt / decrypt, CBC and CFB128 decrypt on a buffer
-    above 4 GiB, checked against the oracle on samples at the head, across
-    byte offset 2^32 (a 32-bit byte or block offset would wrap there) and at
-    the tail (round-3 review: no GPU test ran these kernels above ~3 MB)."""
+@pytest.mark.parametrize("impl", ["ttable", "split"])
+def test_ttable_modes_beyond_4gib(gpu, impl):
+    """T-table (and claimed-split) ECB encrypt / decrypt, CBC and CFB128
+    decrypt on a buffer above 4 GiB, checked against the oracle on samples at
+    the head, across byte offset 2^32 (a 32-bit byte, block or unit offset
+    would wrap there) and at the tail (round-3 review: no GPU test ran these
+    kernels above ~3 MB)."""
     n = (4 << 30) + (1 << 20) + 48
     key = os.urandom(32)
     iv = os.urandom(16)
@@ -661,16 +663,17 @@ def test_ttable_modes_beyond_4gib(gpu):
     def prev(off):
         return iv if off == 0 else host(x[off - 16:off])
 
-    y = ops.ecb_encrypt(x, key, impl="ttable")
+    y = ops.ecb_encrypt(x, key, impl=impl)
     check(y, lambda off: cpu_ref.ecb(key, host(x[off:off + S])))
     del y
-    y = ops.ecb_decrypt(x, key, impl="ttable")
+    y = ops.ecb_decrypt(x, key, impl=impl)
     check(y, lambda off: cpu_ref.ecb(key, host(x[off:off + S]), decrypt=True))
     del y
-    y = ops.cbc_decrypt(x, key, iv, impl="ttable")
+    y = ops.cbc_decrypt(x, key, iv, impl=impl)
     check(y, lambda off: cpu_ref.cbc(key, prev(off), host(x[off:off + S]), decrypt=True))
     del y
-    y = ops.cfb128_decrypt(x, key, iv)
+    y = ops.cfb128_decrypt(x, key, iv, impl=impl)
+    assert ops.last_impl() == impl
     check(y, lambda off: cpu_ref.cfb128(key, prev(off), host(x[off:off + S]), decrypt=True))
     del y, x
     torch.cuda.empty_cache()
