@@ -138,6 +138,14 @@ struct Task {
     uint32_t lane, wave;
     uint64_t vbase; /* virtual block index of slot 0, lane 0 */
     bool full;      /* every slot of the task is in range (uniform) */
+    /* a half-claimed task (otc_device.h CLAIM_HALF): 16384 -- slots 16-31
+     * load and store slots 0-15's blocks again (identical values; ECB in place
+     * loads everything before its first store, CBC / CFB decryption is never
+     * in place) -- else 0 */
+    uint32_t hoff;
+    /* byte / block offsets of slot k's redirect (uniform) */
+    __device__ __forceinline__ uint32_t hsub(int k) const { return k >= 16 ? hoff : 0u; }
+    __device__ __forceinline__ uint32_t hsubb(int k) const { return k >= 16 ? hoff >> 4 : 0u; }
 };
 
 template <int MODE>
@@ -150,9 +158,12 @@ __device__ __forceinline__ bool task_of(const BsParams &P, Task &t, int64_t clai
         t.lane = lane_id();
         asm volatile("" : "+v"(t.lane));
         t.wave = 0;
+        t.hoff = (claimed & CLAIM_HALF) ? 16384u : 0u;
+        claimed &= CLAIM_HALF - 1;
     } else {
         t.lane = threadIdx.x & 63u;
         t.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        t.hoff = 0;
     }
     const uint64_t shift = (MODE == BS_CTR) ? P.shift : 0;
     /* one 2048-block task per wave, no grid-stride loop: a loop lets hipcc
@@ -186,9 +197,9 @@ __device__ __forceinline__ void ecb_load_planes(const BsParams &P, const Task &t
     uint4 blk[32];
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
-        const uint64_t i = t.vbase + t.lane + 64u * k;
+        const uint64_t i = t.vbase + t.lane + 64u * k - t.hsubb(k);
         if constexpr (MODE == BS_CFB_DEC_SEG) {
-            blk[k] = seg_prev<MODE>(P, tb + lo + 1024u * k, i, full || i < P.nblocks);
+            blk[k] = seg_prev<MODE>(P, tb + lo + 1024u * k - t.hsub(k), i, full || i < P.nblocks);
         } else if (MODE == BS_CFB_DEC && k == 0) {
             /* only slot 0 of lane 0 of task 0 can be block 0: it loads block 0
              * itself (a valid address) and takes the IV instead */
@@ -196,7 +207,7 @@ __device__ __forceinline__ void ecb_load_planes(const BsParams &P, const Task &t
             const uint8_t *src = P.in + (int64_t)(t.vbase * 16) + lo - (first ? 0 : 16);
             blk[k] = blend_iv((full || i < P.nblocks) ? *(const uint4 *)src : make_uint4(0, 0, 0, 0), first, P);
         } else {
-            blk[k] = (full || i < P.nblocks) ? *(const uint4 *)(tb + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
+            blk[k] = (full || i < P.nblocks) ? *(const uint4 *)(tb + lo + 1024u * k - t.hsub(k)) : make_uint4(0, 0, 0, 0);
         }
     }
 #pragma unroll
@@ -474,7 +485,8 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
     auto issue = [&](int j) {
         if (XIN && j >= LS && j < 32) {
             if constexpr (MODE == BS_CBC_DEC_SEG) {
-                pt[j] = seg_prev<MODE>(P, ib + lo + 1024u * j, (uint64_t)(tstart + lane + 64 * j), slot_ok(j));
+                pt[j] = seg_prev<MODE>(P, ib + lo + 1024u * j - t.hsub(j), (uint64_t)(tstart + lane + 64 * j) - t.hsubb(j),
+                                       slot_ok(j));
             } else if (MODE == BS_CBC_DEC && j == 0) {
                 /* block 0 of a whole-stream call XORs with the IV: it loads
                  * itself (a valid address) and blends the IV in */
@@ -482,7 +494,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
                 const uint4 v = slot_ok(j) ? *(const uint4 *)(ib + lo + (first ? 0 : XOFF)) : make_uint4(0, 0, 0, 0);
                 pt[j] = blend_iv(v, first, P);
             } else {
-                pt[j] = slot_ok(j) ? *(const uint4 *)(ib + lo + 1024u * j + XOFF) : make_uint4(0, 0, 0, 0);
+                pt[j] = slot_ok(j) ? *(const uint4 *)(ib + lo + 1024u * j + XOFF - t.hsub(j)) : make_uint4(0, 0, 0, 0);
             }
         }
     };
@@ -523,7 +535,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
         if (slot_ok(k)) {
             const uint4 o = XIN ? ks_xor(k, k < LS ? stage[(wave * LS + k) * 64 + (lo >> 4)] : pt[k])
                                 : make_uint4(s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3);
-            *(uint4 *)(ob + lo + 1024u * k) = o;
+            *(uint4 *)(ob + lo + 1024u * k - t.hsub(k)) = o;
         }
     }
 }
@@ -545,7 +557,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 }
 
 /* The bitsliced half of a claimed co-resident split (otc_device.h
- * SplitClaim): each wave takes whole 2048-block units from the front of the
+ * SplitClaim): each wave takes whole 2048-block tasks from the front of the
  * buffer until none are left.  No LDS, so it fits beside the 160 KiB
  * decryption T-table; the loop is the only one in a bitsliced kernel (the
  * task body is unchanged: no hoisted state, same VGPRs -- tests/test_isa_cpu.py). */

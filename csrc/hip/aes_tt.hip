@@ -374,14 +374,14 @@ __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_ke
     };
 
     if constexpr (CLAIM) {
-        const uint64_t done = (uint64_t)P.cl.nunits * 2048u; /* the rest: workgroup 0, first */
+        const uint64_t done = (uint64_t)P.cl.nunits * CLAIM_UNIT; /* the rest: workgroup 0, first */
         if (blockIdx.x == 0)
             for (uint64_t base = done; base < P.nfull; base += PER) chunk(base + (uint64_t)wave * 64u * B + lane, false);
         for (;;) {
             const int64_t u = claim_unit(P.cl, true);
             if (u < 0) break;
 #pragma unroll 1
-            for (uint32_t it = 0; it < 2048u / (64u * B); ++it) chunk((uint64_t)u * 2048u + it * 64u * B + lane, true);
+            for (uint32_t it = 0; it < CLAIM_UNIT / (64u * B); ++it) chunk((uint64_t)u * CLAIM_UNIT + it * 64u * B + lane, true);
         }
         return;
     }
@@ -648,14 +648,14 @@ __device__ __forceinline__ void dec_tt_body(const DecParams &P, const otc_aes_ke
     };
 
     if constexpr (CLAIM) { /* as k_aes_enc_tt */
-        const uint64_t done = (uint64_t)P.cl.nunits * 2048u;
+        const uint64_t done = (uint64_t)P.cl.nunits * CLAIM_UNIT;
         if (blockIdx.x == 0)
             for (uint64_t base = done; base < P.nfull; base += PER) chunk(base + (uint64_t)wave * 64u * B + lane, false);
         for (;;) {
             const int64_t u = claim_unit(P.cl, true);
             if (u < 0) break;
 #pragma unroll 1
-            for (uint32_t it = 0; it < 2048u / (64u * B); ++it) chunk((uint64_t)u * 2048u + it * 64u * B + lane, true);
+            for (uint32_t it = 0; it < CLAIM_UNIT / (64u * B); ++it) chunk((uint64_t)u * CLAIM_UNIT + it * 64u * B + lane, true);
         }
         return;
     }

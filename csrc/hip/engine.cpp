@@ -272,6 +272,20 @@ int pick_ecb_impl(int impl, int bits, size_t nbytes)
 
 int pick_dec_impl(int impl, int bits, size_t nbytes) { return pick_ecb_impl(impl, bits, nbytes); }
 
+/* Units the bitsliced side of a split leaves to the T-table
+ * (otc_device.h claim_unit): OTC_SPLIT_RESERVE_MIB, read per call, default
+ * 0 -- reserves of 32-160 MiB measured 0.5-8% slower (docs/PERF.md round 4,
+ * "claim unit") */
+#ifndef OTC_SPLIT_RESERVE_MIB
+#define OTC_SPLIT_RESERVE_MIB 0
+#endif
+uint32_t split_reserve_units()
+{
+    const char *e = getenv("OTC_SPLIT_RESERVE_MIB");
+    const unsigned long mib = e && *e ? strtoul(e, nullptr, 10) : OTC_SPLIT_RESERVE_MIB;
+    return (uint32_t)std::min<unsigned long>(mib * ((1ul << 20) / (16ul * otc_dev::CLAIM_UNIT)), 1ul << 30);
+}
+
 /* The split: tt(cl) launches the T-table claim kernel on st, bs(cl, aux) the
  * bitsliced claim kernel on the auxiliary stream, both over the whole buffer;
  * plain(n) is the T-table alone (calls under two units, or no memory for the
@@ -279,11 +293,17 @@ int pick_dec_impl(int impl, int bits, size_t nbytes) { return pick_ecb_impl(impl
 template <class TT, class BS, class PLAIN>
 hipError_t split_claim(uint64_t nblocks, hipStream_t st, int *ran, TT tt, BS bs, PLAIN plain)
 {
-    const uint64_t nunits = nblocks / 2048u;
+    const uint64_t nunits = nblocks / otc_dev::CLAIM_UNIT;
     *ran = OTC_IMPL_TTABLE;
-    if (nunits < 2 || nunits > 0x7FFFFFFFull) return plain(nblocks);
+    if (nunits < 2 * otc_dev::TASK_UNITS || nunits > 0x7FFFFFFFull) return plain(nblocks);
     unsigned long long *ctr = nullptr;
-    hipError_t e = otc_dev::alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&ctr, sizeof *ctr, st);
+    /* word 1: the T-table's counter under OTC_SPLIT_TEST_BS_ONLY, a test hook
+     * -- preset to "every unit taken from the back", so the bitsliced kernel
+     * alone takes every unit (its half task at an odd unit count included)
+     * and the T-table kernel does only the remainder past the last unit */
+    const char *bs_only_env = getenv("OTC_SPLIT_TEST_BS_ONLY");
+    const bool bs_only = bs_only_env && *bs_only_env == '1';
+    hipError_t e = otc_dev::alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&ctr, 2 * sizeof *ctr, st);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         return plain(nblocks);
@@ -294,10 +314,13 @@ hipError_t split_claim(uint64_t nblocks, hipStream_t st, int *ran, TT tt, BS bs,
         (void)hipFreeAsync(ctr, st);
         return e;
     }
-    const SplitClaim cl{ctr, (uint32_t)nunits, 0};
+    const SplitClaim cl{ctr, (uint32_t)nunits, bs_only ? 0u : split_reserve_units()};
+    const SplitClaim cl_tt{bs_only ? ctr + 1 : ctr, (uint32_t)nunits, 0};
     /* zeroed, then fork: the aux stream starts after everything queued on st */
-    if ((e = hipMemsetAsync(ctr, 0, sizeof *ctr, st)) == hipSuccess && (e = hipEventRecord(a.fork, st)) == hipSuccess &&
-        (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess && (e = tt(cl)) == hipSuccess) {
+    if ((e = hipMemsetAsync(ctr, 0, 2 * sizeof *ctr, st)) == hipSuccess &&
+        (!bs_only || (e = hipMemsetD32Async((hipDeviceptr_t)((uint32_t *)(ctr + 1) + 1), (int)nunits, 1, st)) == hipSuccess) &&
+        (e = hipEventRecord(a.fork, st)) == hipSuccess && (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess &&
+        (e = tt(cl_tt)) == hipSuccess) {
         /* the bitsliced half failing (no memory for its key table) leaves the
          * T-table claim kernel to take every unit: the output is complete, so
          * the call succeeds as a T-table run.  The join is recorded either way

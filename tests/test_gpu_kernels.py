@@ -479,6 +479,47 @@ def test_ecb_split_matches_ttable(gpu, bits):
             assert host(y[off:off + S]) == cpu_ref.ecb(key, host(x[off:off + S])), (bits, n, off)
 
 
+@pytest.mark.parametrize("k", [4, 5, 7, 64 * 5 + 1])
+def test_split_bitsliced_alone(gpu, k, monkeypatch):
+    """With OTC_SPLIT_TEST_BS_ONLY the T-table claim kernel claims nothing (it
+    only runs the remainder past the last unit), so the bitsliced claim
+    kernel takes every unit of the buffer.  Every split mode (ECB in place,
+    ECB / CBC / CFB decryption, segment decryption) still equals the T-table;
+    so does a run with a reserve left to the T-table (OTC_SPLIT_RESERVE_MIB).
+    In a 1024-block-unit build (scripts/r4_unit_ab.sh) an odd k makes the
+    bitsliced kernel's last claim a half task: slots 16-31 redo slots 0-15
+    instead of touching the blocks past the unit."""
+    key, iv = os.urandom(32), os.urandom(16)
+    nunits = k
+    n = (k * 1024 + 300) * 16
+    x = torch.empty(n, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(x, seed=nunits)
+    calls = {
+        "ecb": lambda x, impl: ops.ecb_encrypt(x, key, impl=impl),
+        "ecb-dec": lambda x, impl: ops.ecb_decrypt(x, key, impl=impl),
+        "cbc-dec": lambda x, impl: ops.cbc_decrypt(x, key, iv, impl=impl),
+        "cfb-dec": lambda x, impl: ops.cfb128_decrypt(x, key, iv, impl=impl),
+        "cbc-dec-seg": lambda x, impl: ops.cbc_decrypt_segments(x[:n - n % 4096], key, iv, 4096, impl=impl),
+        "cfb-dec-seg": lambda x, impl: ops.cfb128_decrypt_segments(x[:n - n % 4096], key, iv, 4096, impl=impl),
+    }
+    for env in ({"OTC_SPLIT_TEST_BS_ONLY": "1"}, {"OTC_SPLIT_RESERVE_MIB": "1"}):
+        for name, f in calls.items():
+            t = f(x, "ttable")
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            y = f(x, "split")
+            assert ops.last_impl() == "split", (name, env)
+            if name == "ecb":
+                w = x.clone()
+                ops.ecb_encrypt(w, key, out=w, impl="split")
+            for k in env:
+                monkeypatch.delenv(k)
+            torch.cuda.synchronize()
+            assert torch.equal(y, t), (name, nunits, env)
+            if name == "ecb":
+                assert torch.equal(w, t), (nunits, env, "in place")
+
+
 def test_ecb_split_stream_order(gpu):
     """The caller's stream waits for BOTH kernels: work queued behind the
     split on the same stream sees the whole output, and the split starts only
