@@ -133,7 +133,7 @@ static int run_op(void *p)
     if (c.mode == "cbc-dec")
         return otc_aes_cbc_decrypt_impl(a->in, a->out, c.bytes, a->k, a->iv, c.impl, nullptr);
     if (c.mode == "cbc-enc-seg")
-        return otc_aes_cbc_encrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
+        return otc_aes_cbc_encrypt_segments_impl(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, c.impl, nullptr);
     if (c.mode == "ctr-stream") { /* resumed mid-block: 1-byte head, then a body misaligned by 1 */
         otc_aes_ctr_ctx ctx;
         otc_aes_ctr_ctx_init(&ctx, a->iv);
@@ -141,7 +141,8 @@ static int run_op(void *p)
         return otc_aes_ctr_stream(&ctx, a->k, c.bytes, a->in, a->out, c.impl, nullptr);
     }
     if (c.mode == "cfb-enc-seg")
-        return otc_aes_cfb128_encrypt_segments(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, nullptr);
+        return otc_aes_cfb128_encrypt_segments_impl(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, c.impl,
+                                                    nullptr);
     if (c.mode == "cfb-dec-seg")
         return otc_aes_cfb128_decrypt_segments_impl(a->in, a->out, c.seg, c.bytes / c.seg, a->k, a->iv, c.impl, nullptr);
     if (c.mode == "cbc-dec-seg")
@@ -564,12 +565,15 @@ int main(int argc, char **argv)
                  (ms * 1e-3) * held * 1e9 * cus / (double)c.bytes);
     if (c.mode.size() > 6 && c.mode.compare(c.mode.size() - 6, 6, "-split") == 0)
         snprintf(clk + strlen(clk), sizeof clk - strlen(clk), "\"share\": %.3f, ", c.share);
-    printf("{\"mode\": \"%s\", \"bits\": %d, \"bytes\": %zu, \"impl\": \"%s\", \"inplace\": %s, \"iters\": %d, "
-           "\"ms\": %.4f, \"gbps\": %.2f, \"cycles_per_byte_per_cu\": %.3f, \"cus\": %d, \"clock_mhz\": %.0f, %s"
+    const int ran = otc_last_impl(); /* what the last timed call ran (this thread) */
+    printf("{\"mode\": \"%s\", \"bits\": %d, \"bytes\": %zu, \"impl\": \"%s\", \"ran\": \"%s\", \"inplace\": %s, "
+           "\"iters\": %d, \"ms\": %.4f, \"gbps\": %.2f, \"cycles_per_byte_per_cu\": %.3f, \"cus\": %d, \"clock_mhz\": %.0f, %s"
            "\"verified\": %s}\n",
            c.mode.c_str(), c.bits, c.bytes,
            c.impl == OTC_IMPL_TTABLE ? "ttable" : c.impl == OTC_IMPL_BITSLICE ? "bitslice"
            : c.impl == OTC_IMPL_SPLIT    ? "split"  : "auto",
+           ran == OTC_IMPL_TTABLE ? "ttable" : ran == OTC_IMPL_BITSLICE ? "bitslice" : ran == OTC_IMPL_SPLIT ? "split"
+                                                                                                          : "auto",
            c.inplace ? "true" : "false", c.iters, ms, gbps, cpb, cus, clk_hz / 1e6, clk, verdict(c.verify, v));
     otc_dev_free(a.in);
     if (!c.inplace) otc_dev_free(a.out);

@@ -73,9 +73,7 @@ struct BsParams {
     const uint32_t *e1tab; /* CTR counter caching: E1 plane words per task */
     uint64_t tasks;       /* 2048-block tasks of the call */
     uint32_t part;        /* BS_FULL_ONLY or BS_EDGE_ONLY */
-    uint32_t has_prev;    /* CBC / CFB decrypt: the 16 bytes before `in` are block 0's predecessor (a
-                             split's second part); otherwise block 0's predecessor is iv */
-    uint32_t iv[4];       /* CBC / CFB decrypt: IV as LE words */
+    uint32_t iv[4];       /* CBC / CFB decrypt: IV as LE words (block 0's predecessor) */
     SplitClaim cl;        /* k_aes_bs_claim: units taken from the front of the buffer */
     Ctr128 iv0;           /* *_SEG: IV of segment 0 (numeric BE; IV_s = iv0 + s) */
     uint32_t seg_shift;   /* *_SEG: log2(blocks per segment) */
@@ -138,14 +136,6 @@ struct Task {
     uint32_t lane, wave;
     uint64_t vbase; /* virtual block index of slot 0, lane 0 */
     bool full;      /* every slot of the task is in range (uniform) */
-    /* a half-claimed task (otc_device.h CLAIM_HALF): 16384 -- slots 16-31
-     * load and store slots 0-15's blocks again (identical values; ECB in place
-     * loads everything before its first store, CBC / CFB decryption is never
-     * in place) -- else 0 */
-    uint32_t hoff;
-    /* byte / block offsets of slot k's redirect (uniform) */
-    __device__ __forceinline__ uint32_t hsub(int k) const { return k >= 16 ? hoff : 0u; }
-    __device__ __forceinline__ uint32_t hsubb(int k) const { return k >= 16 ? hoff >> 4 : 0u; }
 };
 
 template <int MODE>
@@ -158,12 +148,9 @@ __device__ __forceinline__ bool task_of(const BsParams &P, Task &t, int64_t clai
         t.lane = lane_id();
         asm volatile("" : "+v"(t.lane));
         t.wave = 0;
-        t.hoff = (claimed & CLAIM_HALF) ? 16384u : 0u;
-        claimed &= CLAIM_HALF - 1;
     } else {
         t.lane = threadIdx.x & 63u;
         t.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        t.hoff = 0;
     }
     const uint64_t shift = (MODE == BS_CTR) ? P.shift : 0;
     /* one 2048-block task per wave, no grid-stride loop: a loop lets hipcc
@@ -197,17 +184,17 @@ __device__ __forceinline__ void ecb_load_planes(const BsParams &P, const Task &t
     uint4 blk[32];
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
-        const uint64_t i = t.vbase + t.lane + 64u * k - t.hsubb(k);
+        const uint64_t i = t.vbase + t.lane + 64u * k;
         if constexpr (MODE == BS_CFB_DEC_SEG) {
-            blk[k] = seg_prev<MODE>(P, tb + lo + 1024u * k - t.hsub(k), i, full || i < P.nblocks);
+            blk[k] = seg_prev<MODE>(P, tb + lo + 1024u * k, i, full || i < P.nblocks);
         } else if (MODE == BS_CFB_DEC && k == 0) {
             /* only slot 0 of lane 0 of task 0 can be block 0: it loads block 0
              * itself (a valid address) and takes the IV instead */
-            const bool first = !P.has_prev && i == 0;
+            const bool first = i == 0;
             const uint8_t *src = P.in + (int64_t)(t.vbase * 16) + lo - (first ? 0 : 16);
             blk[k] = blend_iv((full || i < P.nblocks) ? *(const uint4 *)src : make_uint4(0, 0, 0, 0), first, P);
         } else {
-            blk[k] = (full || i < P.nblocks) ? *(const uint4 *)(tb + lo + 1024u * k - t.hsub(k)) : make_uint4(0, 0, 0, 0);
+            blk[k] = (full || i < P.nblocks) ? *(const uint4 *)(tb + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
         }
     }
 #pragma unroll
@@ -350,9 +337,6 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
  * 81-LUT S-box (27 live planes at its peak) 4 early slots spilled in the
  * output phase; with the 79-LUT one (24) they no longer spill but measured
  * 1-1.5% slower, profiles/r3/sbox79; the 77-LUT one peaks at 23) */
-#ifndef OTC_BS_CLAIM_WGS
-#define OTC_BS_CLAIM_WGS 1 /* bitsliced claim workgroups per CU (one wave per SIMD beside the T-table's 4) */
-#endif
 #ifndef OTC_BS_CBC_D
 #define OTC_BS_CBC_D 4
 #endif
@@ -485,16 +469,16 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
     auto issue = [&](int j) {
         if (XIN && j >= LS && j < 32) {
             if constexpr (MODE == BS_CBC_DEC_SEG) {
-                pt[j] = seg_prev<MODE>(P, ib + lo + 1024u * j - t.hsub(j), (uint64_t)(tstart + lane + 64 * j) - t.hsubb(j),
+                pt[j] = seg_prev<MODE>(P, ib + lo + 1024u * j, (uint64_t)(tstart + lane + 64 * j),
                                        slot_ok(j));
             } else if (MODE == BS_CBC_DEC && j == 0) {
                 /* block 0 of a whole-stream call XORs with the IV: it loads
                  * itself (a valid address) and blends the IV in */
-                const bool first = !P.has_prev && tstart + lane == 0;
+                const bool first = tstart + lane == 0;
                 const uint4 v = slot_ok(j) ? *(const uint4 *)(ib + lo + (first ? 0 : XOFF)) : make_uint4(0, 0, 0, 0);
                 pt[j] = blend_iv(v, first, P);
             } else {
-                pt[j] = slot_ok(j) ? *(const uint4 *)(ib + lo + 1024u * j + XOFF - t.hsub(j)) : make_uint4(0, 0, 0, 0);
+                pt[j] = slot_ok(j) ? *(const uint4 *)(ib + lo + 1024u * j + XOFF) : make_uint4(0, 0, 0, 0);
             }
         }
     };
@@ -535,7 +519,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
         if (slot_ok(k)) {
             const uint4 o = XIN ? ks_xor(k, k < LS ? stage[(wave * LS + k) * 64 + (lo >> 4)] : pt[k])
                                 : make_uint4(s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3);
-            *(uint4 *)(ob + lo + 1024u * k - t.hsub(k)) = o;
+            *(uint4 *)(ob + lo + 1024u * k) = o;
         }
     }
 }
@@ -624,22 +608,20 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
      * measured slower for both modes: ECB 1178 vs 1240 GB/s (4 GiB,
      * profiles/r2/bitslice_out), CTR (64 GiB, with the key-term prefetch)
      * 1547/1551 vs 1606/1606 (profiles/r3/split). */
-    const bool edge = (MODE == BS_CTR && P.shift != 0) || vt % 2048 != 0;
     if constexpr (MODE != BS_CTR) {
-        if (P.cl.ctr) { /* claimed split: one workgroup per CU beside the T-table's */
-            hipLaunchKernelGGL((k_aes_bs_claim<NR, MODE>), dim3((unsigned)otc_dev::device_cus() * OTC_BS_CLAIM_WGS), b,
-                               0, st, Q, K);
-            e = hipGetLastError();
-            const hipError_t f = hipFreeAsync(tab, st);
-            return e != hipSuccess ? e : f;
+        /* ECB and the decryptions run only as claim kernels: beside the
+         * T-table (the split: one workgroup per CU), or alone (impl
+         * "bitslice": cl.wgs = 3 per CU, the T-table claim kernel does the
+         * blocks past the last unit) */
+        (void)g;
+        if (!P.cl.ctr) {
+            (void)hipFreeAsync(tab, st);
+            return hipErrorInvalidValue;
         }
-    }
-    if constexpr (is_seg<MODE>) {
-        /* the segment modes run only as the claimed split's bitsliced half */
-        (void)edge;
-        (void)hipFreeAsync(tab, st);
-        return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_aes_bs_claim<NR, MODE>),
+                           dim3(P.cl.wgs ? P.cl.wgs : (unsigned)otc_dev::device_cus()), b, 0, st, Q, K);
     } else {
+        const bool edge = P.shift != 0 || vt % 2048 != 0;
         auto run = [&](auto cachec) {
             constexpr bool C = decltype(cachec)::value;
             Q.part = BS_FULL_ONLY;
@@ -649,22 +631,16 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
                 hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, false>), dim3(1), b, 0, st, Q, K);
             }
         };
-        /* counter caching exists for CTR only: no ECB kernels are instantiated
-         * with it */
-        if constexpr (MODE == BS_CTR) {
-            if (cache) {
-                uint32_t *gt = tab + kt_words, *e0 = gt + ngroups * OTC_BS_CTR_GRP_WORDS,
-                         *e1 = e0 + ngroups * OTC_BS_CTR_E0_WORDS;
-                Q.ctab = gt;
-                Q.e0tab = e0;
-                Q.e1tab = e1;
-                const uint64_t n = ngroups * 65 + tasks;
-                hipLaunchKernelGGL(k_bs_ctr_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, P.cbase,
-                                   P.wrap64, ngroups, tasks, gt, e0, e1);
-                run(std::true_type{});
-            } else {
-                run(std::false_type{});
-            }
+        if (cache) {
+            uint32_t *gt = tab + kt_words, *e0 = gt + ngroups * OTC_BS_CTR_GRP_WORDS,
+                     *e1 = e0 + ngroups * OTC_BS_CTR_E0_WORDS;
+            Q.ctab = gt;
+            Q.e0tab = e0;
+            Q.e1tab = e1;
+            const uint64_t n = ngroups * 65 + tasks;
+            hipLaunchKernelGGL(k_bs_ctr_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, P.cbase,
+                               P.wrap64, ngroups, tasks, gt, e0, e1);
+            run(std::true_type{});
         } else {
             run(std::false_type{});
         }
@@ -717,56 +693,6 @@ hipError_t bs_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K
     P.cbase.lo = c.lo & ~(uint64_t)2047u;
     P.cbase.hi = c.hi;
     return launch<BS_CTR>(P, K, st);
-}
-
-hipError_t bs_ecb_encrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, hipStream_t st)
-{
-    BsParams P{};
-    P.in = (const uint8_t *)in;
-    P.out = (uint8_t *)out;
-    P.nblocks = nblocks;
-    return launch<BS_ECB>(P, K, st);
-}
-
-/* K: the decryption (equivalent inverse cipher) schedule, as the T-table
- * decrypt kernel takes it */
-hipError_t bs_ecb_decrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, hipStream_t st)
-{
-    BsParams P{};
-    P.in = (const uint8_t *)in;
-    P.out = (uint8_t *)out;
-    P.nblocks = nblocks;
-    return launch<BS_ECB_DEC>(P, K, st);
-}
-
-/* CBC decryption: block i XORs with block i-1 of `in`; block 0 with iv_le
- * (LE words), or -- has_prev -- with the 16 bytes before `in` (the second
- * part of a split call).  in != out. */
-hipError_t bs_cbc_decrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, const uint32_t iv_le[4],
-                          bool has_prev, hipStream_t st)
-{
-    BsParams P{};
-    P.in = (const uint8_t *)in;
-    P.out = (uint8_t *)out;
-    P.nblocks = nblocks;
-    P.has_prev = has_prev ? 1u : 0u;
-    for (int i = 0; i < 4; ++i) P.iv[i] = iv_le ? iv_le[i] : 0u;
-    return launch<BS_CBC_DEC>(P, K, st);
-}
-
-/* CFB128 decryption with the ENCRYPTION schedule: block i = E(block i-1 of
- * `in`) ^ block i; block 0's predecessor is iv_le or -- has_prev -- the 16
- * bytes before `in`.  in != out. */
-hipError_t bs_cfb_decrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, const uint32_t iv_le[4],
-                          bool has_prev, hipStream_t st)
-{
-    BsParams P{};
-    P.in = (const uint8_t *)in;
-    P.out = (uint8_t *)out;
-    P.nblocks = nblocks;
-    P.has_prev = has_prev ? 1u : 0u;
-    for (int i = 0; i < 4; ++i) P.iv[i] = iv_le ? iv_le[i] : 0u;
-    return launch<BS_CFB_DEC>(P, K, st);
 }
 
 /* The bitsliced halves of a claimed split: the whole buffer (block 0's

@@ -40,14 +40,11 @@
 using namespace otc_dev;
 
 /* compile-time A/B switches (make variant NAME=x VFLAGS=-D...; docs/PERF.md) */
-#ifndef OTC_TT_PF
-#define OTC_TT_PF 0 /* software-pipelined input loads in the ECB / decrypt kernels */
-#endif
-#ifndef OTC_SEG_GB
-#define OTC_SEG_GB 1 /* segments per lane, grouped CBC / CFB segment encryption (A/B knob) */
-#endif
 #ifndef OTC_SEG_G
 #define OTC_SEG_G 8 /* blocks per load burst, grouped segment encryption (A/B knob) */
+#endif
+#ifndef OTC_SEG_CLAIM_G
+#define OTC_SEG_CLAIM_G 4 /* the same, in the claim kernel of the segment-encryption split: 4 keeps it at <= 72 VGPRs, room for a 128-VGPR bs8 wave per SIMD */
 #endif
 #ifndef OTC_TT_CTR_B
 #define OTC_TT_CTR_B 4 /* blocks per lane, bulk CTR kernel (A/B knob: 2 fits a bitsliced wave beside it) */
@@ -290,44 +287,6 @@ __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_ke
     tbl4_lane_consts(lane, lk);
     constexpr uint64_t PER = (uint64_t)THREADS * B;
 
-    if constexpr (MODE == E_ECB && OTC_TT_PF) {
-        /* software-pipelined input: the next iteration's B blocks are loaded
-         * before this iteration's rounds, so no wave starts its rounds behind
-         * an HBM round trip (in place is safe: the blocks loaded ahead belong
-         * to the next iteration, stored only after it loaded them) */
-        const uint64_t stride = (uint64_t)gridDim.x * PER;
-        uint4 nx[B];
-        auto load = [&](uint64_t bs) {
-            const bool full = bs + PER <= P.nfull;
-            const uint64_t i0 = bs + (uint64_t)wave * 64u * B + lane;
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                const uint64_t i = i0 + 64u * b;
-                nx[b] = (full || i < P.nfull) ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
-            }
-        };
-        uint64_t base = (uint64_t)blockIdx.x * PER;
-        if (base < P.nfull) load(base);
-        for (; base < P.nfull; base += stride) {
-            const bool full = base + PER <= P.nfull;
-            const uint64_t i0 = base + (uint64_t)wave * 64u * B + lane;
-            uint32_t s[B][4];
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                s[b][0] = nx[b].x ^ K.rk[0]; s[b][1] = nx[b].y ^ K.rk[1];
-                s[b][2] = nx[b].z ^ K.rk[2]; s[b][3] = nx[b].w ^ K.rk[3];
-            }
-            if (base + stride < P.nfull) load(base + stride);
-            enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                const uint64_t i = i0 + 64u * b;
-                if (full || i < P.nfull) st16(P.out, i, make_uint4(s[b][0], s[b][1], s[b][2], s[b][3]));
-            }
-        }
-        return;
-    }
-
     /* B blocks per lane: i0 + 64 b, b < B; `full`: all in range (wave-uniform) */
     auto chunk = [&](uint64_t i0, bool full) {
         uint32_t s[B][4];
@@ -540,69 +499,6 @@ __device__ __forceinline__ void dec_tt_body(const DecParams &P, const otc_aes_ke
     const uint32_t lk_is2 = 0x40000u | ((lane & 31u) << 3);
     constexpr uint64_t PER = (uint64_t)THREADS * B;
 
-    if constexpr (OTC_TT_PF) {
-        /* software-pipelined input (see k_aes_enc_tt): block i and, for CBC,
-         * its predecessor (or the IV at a chain start) of the next iteration
-         * are loaded before this iteration's rounds */
-        const uint64_t stride = (uint64_t)gridDim.x * PER;
-        uint4 nx[B], np[B];
-        auto load = [&](uint64_t bs) {
-            const bool full = bs + PER <= P.nfull;
-            const uint64_t i0 = bs + (uint64_t)wave * 64u * B + lane;
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                const uint64_t i = i0 + 64u * b;
-                const bool ok = full || i < P.nfull;
-                nx[b] = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
-                if (MODE == D_CBC || MODE == D_CBC_SEG) {
-                    bool first;
-                    Ctr128 ivv = P.iv;
-                    if (MODE == D_CBC) {
-                        first = (i == 0);
-                    } else {
-                        first = (i & ((1ull << P.seg_shift) - 1)) == 0;
-                        const uint64_t seg = i >> P.seg_shift;
-                        ivv.lo = P.iv.lo + seg;
-                        ivv.hi = P.iv.hi + (ivv.lo < P.iv.lo ? 1 : 0);
-                    }
-                    if (first) {
-                        uint32_t w0, w1, w2, w3;
-                        ctr_words(ivv, 0, false, w0, w1, w2, w3);
-                        np[b] = make_uint4(w0, w1, w2, w3);
-                    } else {
-                        np[b] = ok ? ld16(P.in, i - 1) : make_uint4(0, 0, 0, 0);
-                    }
-                }
-            }
-        };
-        uint64_t base = (uint64_t)blockIdx.x * PER;
-        if (base < P.nfull) load(base);
-        for (; base < P.nfull; base += stride) {
-            const bool full = base + PER <= P.nfull;
-            const uint64_t i0 = base + (uint64_t)wave * 64u * B + lane;
-            uint32_t s[B][4];
-            uint4 prev[B];
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                s[b][0] = nx[b].x ^ K.rk[0]; s[b][1] = nx[b].y ^ K.rk[1];
-                s[b][2] = nx[b].z ^ K.rk[2]; s[b][3] = nx[b].w ^ K.rk[3];
-                if (MODE != D_ECB) prev[b] = np[b];
-            }
-            if (base + stride < P.nfull) load(base + stride);
-            dec_rounds4<NR, B>(tbl, lk, lk_is2, K, s);
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                const uint64_t i = i0 + 64u * b;
-                uint4 o = make_uint4(s[b][0], s[b][1], s[b][2], s[b][3]);
-                if (MODE != D_ECB) {
-                    o.x ^= prev[b].x; o.y ^= prev[b].y; o.z ^= prev[b].z; o.w ^= prev[b].w;
-                }
-                if (full || i < P.nfull) st16(P.out, i, o);
-            }
-        }
-        return;
-    }
-
     auto chunk = [&](uint64_t i0, bool full) {
         uint32_t s[B][4];
         uint4 prev[B];
@@ -692,6 +588,7 @@ struct CbcSegParams {
     uint64_t seg_blocks;
     uint64_t nseg;
     Ctr128 iv0;
+    SplitClaim cl; /* k_aes_seg_enc_tt_claim: 64-segment units from the back */
 };
 
 /* chain step on B lanes: s = cipher input ^ rk0 from the chain value c and
@@ -771,84 +668,89 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg(CbcSegParams P, otc
  * the ~2048 live segments per CU evict those lines from L2 between uses and
  * each 16-byte block re-fetches a whole line.  Group g+1 is prefetched while
  * group g is encrypted; ciphertext overwrites the plaintext registers and is
- * stored as a burst at the end of the group. */
-template <int NR, int B, int THREADS, int G, bool CFB = false>
+ * stored as a burst at the end of the group.  One segment per lane (two, with
+ * 4- or 8-block bursts, measured 1-27% slower: profiles/r4/seg_ab/). */
+template <int NR, int G, bool CFB>
+__device__ __forceinline__ void seg_chain_g(const CbcSegParams &P, const otc_aes_key &K, const uint32_t *tbl,
+                                            const uint32_t (&lk)[4], uint64_t seg, bool live)
+{
+    const uint64_t sb = P.seg_blocks;
+    const uint64_t ng = sb / G;
+    const uint64_t first = seg * sb; /* block index of the segment's first block */
+    uint32_t c[4];
+    uint4 cur[G], nxt[G];
+    Ctr128 ivv;
+    ivv.lo = P.iv0.lo + seg;
+    ivv.hi = P.iv0.hi + (ivv.lo < P.iv0.lo ? 1 : 0);
+    ctr_words(ivv, 0, false, c[0], c[1], c[2], c[3]);
+#pragma unroll
+    for (int t = 0; t < G; ++t) cur[t] = (live && ng) ? ld16(P.in, first + t) : make_uint4(0, 0, 0, 0);
+    for (uint64_t g = 0; g < ng; ++g) {
+        const bool more = g + 1 < ng;
+#pragma unroll
+        for (int t = 0; t < G; ++t)
+            nxt[t] = (live && more) ? ld16(P.in, first + (g + 1) * G + t) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < G; ++t) {
+            uint32_t s[1][4];
+            chain_in<CFB>(cur[t], c, K, s[0]);
+            enc_rounds4_from<1, NR, 1>(tbl, lk, K, s);
+            chain_out<CFB>(cur[t], s[0], c);
+            cur[t] = make_uint4(c[0], c[1], c[2], c[3]);
+        }
+#pragma unroll
+        for (int t = 0; t < G; ++t) {
+            if (live) st16(P.out, first + g * G + t, cur[t]);
+            cur[t] = nxt[t];
+        }
+    }
+    /* remaining sb % G blocks, one at a time */
+    for (uint64_t j = ng * G; j < sb; ++j) {
+        uint32_t s[1][4];
+        const uint4 p = live ? ld16(P.in, first + j) : make_uint4(0, 0, 0, 0);
+        chain_in<CFB>(p, c, K, s[0]);
+        enc_rounds4_from<1, NR, 1>(tbl, lk, K, s);
+        chain_out<CFB>(p, s[0], c);
+        if (live) st16(P.out, first + j, make_uint4(c[0], c[1], c[2], c[3]));
+    }
+}
+
+template <int NR, int THREADS, int G, bool CFB = false>
 __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg_g(CbcSegParams P, otc_aes_key K)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
     fill_tbl4<THREADS>(tbl, g_tab.te0);
     __syncthreads();
-
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
     uint32_t lk[4];
-    tbl4_lane_consts(lane, lk);
-    constexpr uint64_t PER = (uint64_t)THREADS * B;
-    const uint64_t sb = P.seg_blocks;
-    const uint64_t ng = sb / G;
+    tbl4_lane_consts(threadIdx.x & 63u, lk);
+    for (uint64_t base = (uint64_t)blockIdx.x * THREADS; base < P.nseg; base += (uint64_t)gridDim.x * THREADS) {
+        const uint64_t seg = base + threadIdx.x;
+        seg_chain_g<NR, G, CFB>(P, K, tbl, lk, seg, seg < P.nseg);
+    }
+}
 
-    for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nseg; base += (uint64_t)gridDim.x * PER) {
-        uint64_t first[B]; /* block index of the segment's first block */
-        bool live[B];
-        uint32_t c[B][4];
-        uint4 cur[B][G], nxt[B][G];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            const uint64_t seg = base + (uint64_t)wave * 64u * B + 64u * b + lane;
-            live[b] = seg < P.nseg;
-            first[b] = seg * sb;
-            Ctr128 ivv;
-            ivv.lo = P.iv0.lo + seg;
-            ivv.hi = P.iv0.hi + (ivv.lo < P.iv0.lo ? 1 : 0);
-            ctr_words(ivv, 0, false, c[b][0], c[b][1], c[b][2], c[b][3]);
-#pragma unroll
-            for (int t = 0; t < G; ++t)
-                cur[b][t] = (live[b] && ng) ? ld16(P.in, first[b] + t) : make_uint4(0, 0, 0, 0);
-        }
-        for (uint64_t g = 0; g < ng; ++g) {
-            const bool more = g + 1 < ng;
-#pragma unroll
-            for (int b = 0; b < B; ++b)
-#pragma unroll
-                for (int t = 0; t < G; ++t)
-                    nxt[b][t] = (live[b] && more) ? ld16(P.in, first[b] + (g + 1) * G + t) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (int t = 0; t < G; ++t) {
-                uint32_t s[B][4];
-#pragma unroll
-                for (int b = 0; b < B; ++b) chain_in<CFB>(cur[b][t], c[b], K, s[b]);
-                enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
-#pragma unroll
-                for (int b = 0; b < B; ++b) {
-                    chain_out<CFB>(cur[b][t], s[b], c[b]);
-                    cur[b][t] = make_uint4(c[b][0], c[b][1], c[b][2], c[b][3]);
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-#pragma unroll
-                for (int t = 0; t < G; ++t) {
-                    if (live[b]) st16(P.out, first[b] + g * G + t, cur[b][t]);
-                    cur[b][t] = nxt[b][t];
-                }
-            }
-        }
-        /* remaining sb % G blocks, one at a time */
-        for (uint64_t j = ng * G; j < sb; ++j) {
-            uint32_t s[B][4];
-            uint4 p[B];
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                p[b] = live[b] ? ld16(P.in, first[b] + j) : make_uint4(0, 0, 0, 0);
-                chain_in<CFB>(p[b], c[b], K, s[b]);
-            }
-            enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
-#pragma unroll
-            for (int b = 0; b < B; ++b) {
-                chain_out<CFB>(p[b], s[b], c[b]);
-                if (live[b]) st16(P.out, first[b] + j, make_uint4(c[b][0], c[b][1], c[b][2], c[b][3]));
-            }
-        }
+/* The T-table half of the chained segment encryption split (engine.cpp
+ * seg_enc_split): a claim unit is 64 segments, one per lane of a wave, taken
+ * from the back; workgroup 0 first runs the segments past the last full unit.
+ * The bitsliced half (aes_bs8.hip) takes 8 units at a time from the front. */
+constexpr uint32_t SEG_UNIT = 64;
+template <int NR, int G, bool CFB>
+__global__ __launch_bounds__(1024) void k_aes_seg_enc_tt_claim(CbcSegParams P, otc_aes_key K)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
+    fill_tbl4<1024>(tbl, g_tab.te0);
+    __syncthreads();
+    uint32_t lk[4];
+    tbl4_lane_consts(threadIdx.x & 63u, lk);
+    const uint64_t done = (uint64_t)P.cl.nunits * SEG_UNIT;
+    if (blockIdx.x == 0 && done + (threadIdx.x & ~63u) < P.nseg) { /* the remainder (< 64 segments): wave 0 */
+        const uint64_t seg = done + threadIdx.x;
+        seg_chain_g<NR, G, CFB>(P, K, tbl, lk, seg, seg < P.nseg);
+    }
+    for (;;) {
+        const int64_t u = claim_unit(P.cl, true);
+        if (u < 0) break;
+        seg_chain_g<NR, G, CFB>(P, K, tbl, lk, (uint64_t)u * SEG_UNIT + lane_id(), true);
     }
 }
 
@@ -1221,7 +1123,7 @@ hipError_t launch_dec(const DecParams &P, const otc_aes_key &K, hipStream_t st)
 template <int MODE>
 hipError_t launch_enc_claim(const EncParams &P, const otc_aes_key &K, hipStream_t st)
 {
-    const dim3 g((unsigned)num_cus()), b(ENC_THREADS);
+    const dim3 g(P.cl.wgs ? P.cl.wgs : (unsigned)num_cus()), b(ENC_THREADS);
     switch (K.nr) {
     case 10:
         if constexpr (MODE == E_ECB) hipLaunchKernelGGL((k_aes_ecb_tt_claim<10>), g, b, 0, st, P, K);
@@ -1246,7 +1148,7 @@ hipError_t launch_enc_claim(const EncParams &P, const otc_aes_key &K, hipStream_
 template <int MODE>
 hipError_t launch_dec_claim(const DecParams &P, const otc_aes_key &K, hipStream_t st)
 {
-    const dim3 g((unsigned)num_cus()), b(DEC_THREADS);
+    const dim3 g(P.cl.wgs ? P.cl.wgs : (unsigned)num_cus()), b(DEC_THREADS);
     switch (K.nr) {
     case 10: hipLaunchKernelGGL((k_aes_dec_tt_claim<10, MODE>), g, b, 0, st, P, K); break;
     case 12: hipLaunchKernelGGL((k_aes_dec_tt_claim<12, MODE>), g, b, 0, st, P, K); break;
@@ -1265,8 +1167,8 @@ hipError_t launch_seg_nr(const CbcSegParams &P, const otc_aes_key &K, hipStream_
      * per segment fit without spills.  Segments shorter than 8 blocks take the
      * per-block kernel. */
     if (P.seg_blocks >= OTC_SEG_G)
-        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, OTC_SEG_GB, SEG_THREADS, OTC_SEG_G, CFB>),
-                           dim3(grid_for(P.nseg, (uint64_t)SEG_THREADS * OTC_SEG_GB, 1)), dim3(SEG_THREADS), 0, st, P, K);
+        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, SEG_THREADS, OTC_SEG_G, CFB>),
+                           dim3(grid_for(P.nseg, (uint64_t)SEG_THREADS, 1)), dim3(SEG_THREADS), 0, st, P, K);
     else
         hipLaunchKernelGGL((k_aes_cbc_enc_seg<NR, SEG_B, SEG_THREADS, CFB>), dim3(grid), dim3(SEG_THREADS), 0, st, P,
                            K);
@@ -1551,6 +1453,33 @@ hipError_t tt_cfb_encrypt_seg(const void *in, void *out, uint64_t seg_blocks, ui
                               const otc_aes_key &K, Ctr128 iv0, hipStream_t st)
 {
     return chain_encrypt_seg<true>(in, out, seg_blocks, nseg, K, iv0, st);
+}
+
+/* the T-table half of the chained segment-encryption split: 64-segment
+ * units from the back of `cl` (cl.wgs workgroups, default one per CU) */
+hipError_t tt_seg_encrypt_claim(bool cfb, const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,
+                                const otc_aes_key &K, Ctr128 iv0, SplitClaim cl, hipStream_t st)
+{
+    CbcSegParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.seg_blocks = seg_blocks;
+    P.nseg = nseg;
+    P.iv0 = iv0;
+    P.cl = cl;
+    const dim3 g(cl.wgs ? cl.wgs : (unsigned)num_cus()), b(1024);
+    constexpr int G = OTC_SEG_CLAIM_G;
+#define OTC_SEG_CLAIM_LAUNCH(NR)                                                                   \
+    if (cfb) hipLaunchKernelGGL((k_aes_seg_enc_tt_claim<NR, G, true>), g, b, 0, st, P, K);        \
+    else hipLaunchKernelGGL((k_aes_seg_enc_tt_claim<NR, G, false>), g, b, 0, st, P, K)
+    switch (K.nr) {
+    case 10: OTC_SEG_CLAIM_LAUNCH(10); break;
+    case 12: OTC_SEG_CLAIM_LAUNCH(12); break;
+    case 14: OTC_SEG_CLAIM_LAUNCH(14); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef OTC_SEG_CLAIM_LAUNCH
+    return hipGetLastError();
 }
 
 hipError_t tt_cfb_decrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,

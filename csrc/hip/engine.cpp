@@ -55,13 +55,13 @@ hipError_t tt_cbc_decrypt_seg(const void *, void *, uint64_t, uint64_t, const ot
 hipError_t tt_cbc_encrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t tt_cfb_encrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t tt_cfb_decrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
+hipError_t tt_seg_encrypt_claim(bool, const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, SplitClaim,
+                                hipStream_t);
+hipError_t bs8_seg_encrypt_claim(bool, const void *, void *, uint64_t, const otc_aes_key &, Ctr128, SplitClaim,
+                                 hipStream_t);
 hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
 hipError_t tt_ctr_shift(const void *, void *, size_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t xor_small(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
-hipError_t bs_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
-hipError_t bs_ecb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
-hipError_t bs_cbc_decrypt(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, bool, hipStream_t);
-hipError_t bs_cfb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, bool, hipStream_t);
 hipError_t bs_claim(int, const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, SplitClaim, hipStream_t);
 hipError_t tt_ecb_encrypt_claim(const void *, void *, uint64_t, const otc_aes_key &, SplitClaim, hipStream_t);
 hipError_t tt_cfb_decrypt_claim(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, SplitClaim,
@@ -272,104 +272,105 @@ int pick_ecb_impl(int impl, int bits, size_t nbytes)
 
 int pick_dec_impl(int impl, int bits, size_t nbytes) { return pick_ecb_impl(impl, bits, nbytes); }
 
-/* Units the bitsliced side of a split leaves to the T-table
- * (otc_device.h claim_unit): OTC_SPLIT_RESERVE_MIB, read per call, default
- * 0 -- reserves of 32-160 MiB measured 0.5-8% slower (docs/PERF.md round 4,
- * "claim unit") */
-#ifndef OTC_SPLIT_RESERVE_MIB
-#define OTC_SPLIT_RESERVE_MIB 0
-#endif
-uint32_t split_reserve_units()
-{
-    const char *e = getenv("OTC_SPLIT_RESERVE_MIB");
-    const unsigned long mib = e && *e ? strtoul(e, nullptr, 10) : OTC_SPLIT_RESERVE_MIB;
-    return (uint32_t)std::min<unsigned long>(mib * ((1ul << 20) / (16ul * otc_dev::CLAIM_UNIT)), 1ul << 30);
-}
-
 /* The split: tt(cl) launches the T-table claim kernel on st, bs(cl, aux) the
- * bitsliced claim kernel on the auxiliary stream, both over the whole buffer;
- * plain(n) is the T-table alone (calls under two units, or no memory for the
- * counter).  *ran: the kernels actually used. */
+ * bitsliced claim kernel on the auxiliary stream, both over the whole buffer
+ * (nunits claim units, the T-table kernel also runs what lies past the last
+ * unit); plain() is the T-table alone (too few units, or no memory for the
+ * counter / no auxiliary stream).  bs_only: impl "bitslice" -- the T-table
+ * kernel's back counter starts full, so the bitsliced kernel (bs_wgs
+ * workgroups) takes every unit and one T-table workgroup runs the rest.
+ * *ran: the kernels actually used. */
 template <class TT, class BS, class PLAIN>
-hipError_t split_claim(uint64_t nblocks, hipStream_t st, int *ran, TT tt, BS bs, PLAIN plain)
+hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsigned bs_wgs, hipStream_t st, int *ran,
+                       TT tt, BS bs, PLAIN plain)
 {
-    const uint64_t nunits = nblocks / otc_dev::CLAIM_UNIT;
     *ran = OTC_IMPL_TTABLE;
-    if (nunits < 2 * otc_dev::TASK_UNITS || nunits > 0x7FFFFFFFull) return plain(nblocks);
+    if (nunits < (bs_only ? 1 : min_units) || nunits > 0x7FFFFFFFull) return plain();
     unsigned long long *ctr = nullptr;
-    /* word 1: the T-table's counter under OTC_SPLIT_TEST_BS_ONLY, a test hook
-     * -- preset to "every unit taken from the back", so the bitsliced kernel
-     * alone takes every unit (its half task at an odd unit count included)
-     * and the T-table kernel does only the remainder past the last unit */
-    const char *bs_only_env = getenv("OTC_SPLIT_TEST_BS_ONLY");
-    const bool bs_only = bs_only_env && *bs_only_env == '1';
+    /* word 0: the shared claim word; word 1 (bs_only): the T-table kernel's
+     * own word, preset to "every unit taken from the back" */
     hipError_t e = otc_dev::alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&ctr, 2 * sizeof *ctr, st);
     if (e != hipSuccess) {
         (void)hipGetLastError();
-        return plain(nblocks);
+        return plain();
     }
     int dev = 0;
     AuxStream a;
-    if ((e = hipGetDevice(&dev)) != hipSuccess || (e = aux_take(dev, a)) != hipSuccess) {
+    if (hipGetDevice(&dev) != hipSuccess || aux_take(dev, a) != hipSuccess) {
+        /* no auxiliary stream: the T-table alone still gives the output */
+        (void)hipGetLastError();
         (void)hipFreeAsync(ctr, st);
-        return e;
+        return plain();
     }
-    const SplitClaim cl{ctr, (uint32_t)nunits, bs_only ? 0u : split_reserve_units()};
-    const SplitClaim cl_tt{bs_only ? ctr + 1 : ctr, (uint32_t)nunits, 0};
+    const SplitClaim cl{ctr, (uint32_t)nunits, bs_wgs};
+    const SplitClaim cl_tt{bs_only ? ctr + 1 : ctr, (uint32_t)nunits, bs_only ? 1u : 0u};
     /* zeroed, then fork: the aux stream starts after everything queued on st */
     if ((e = hipMemsetAsync(ctr, 0, 2 * sizeof *ctr, st)) == hipSuccess &&
         (!bs_only || (e = hipMemsetD32Async((hipDeviceptr_t)((uint32_t *)(ctr + 1) + 1), (int)nunits, 1, st)) == hipSuccess) &&
         (e = hipEventRecord(a.fork, st)) == hipSuccess && (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess &&
         (e = tt(cl_tt)) == hipSuccess) {
         /* the bitsliced half failing (no memory for its key table) leaves the
-         * T-table claim kernel to take every unit: the output is complete, so
-         * the call succeeds as a T-table run.  The join is recorded either way
-         * (a failure after its launch must still be waited for). */
+         * T-table claim kernel to take every unit -- unless it was told to
+         * take none (bs_only): then the T-table alone redoes the call.  The
+         * join is recorded either way (a failure after its launch must still
+         * be waited for). */
         const hipError_t eb = bs(cl, a.s);
         if (eb != hipSuccess) (void)hipGetLastError();
         if ((e = hipEventRecord(a.join, a.s)) == hipSuccess) e = hipStreamWaitEvent(st, a.join, 0);
-        if (e == hipSuccess)
-            *ran = eb == hipSuccess ? OTC_IMPL_SPLIT : OTC_IMPL_TTABLE;
-        else
+        if (e == hipSuccess) {
+            if (eb == hipSuccess) *ran = bs_only ? OTC_IMPL_BITSLICE : OTC_IMPL_SPLIT;
+            else if (bs_only) e = plain();
+        } else {
             (void)hipStreamSynchronize(a.s); /* no join on st: the counter must outlive the bitsliced kernel */
+        }
     }
     const hipError_t f = hipFreeAsync(ctr, st); /* after the join: both kernels are done with it */
     aux_give(a); /* reusable as soon as the work is enqueued: stream order */
     return e != hipSuccess ? e : f;
 }
 
-hipError_t ecb_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, hipStream_t st, int *ran)
+/* bitsliced claim workgroups: one per CU beside the T-table (4 T-table waves
+ * + 1 bitsliced wave per SIMD), three per CU alone (<= 168 VGPRs) */
+unsigned bs_wgs_for(bool bs_only) { return (unsigned)otc_dev::device_cus() * (bs_only ? 3u : 1u); }
+
+hipError_t ecb_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, bool bs_only, hipStream_t st,
+                     int *ran)
 {
+    const uint64_t nunits = nblocks / otc_dev::CLAIM_UNIT;
     if (K.dir == OTC_DIR_ENCRYPT)
         return split_claim(
-            nblocks, st, ran, [&](SplitClaim cl) { return otc_impl::tt_ecb_encrypt_claim(in, out, nblocks, K, cl, st); },
+            nunits, 2, bs_only, bs_wgs_for(bs_only), st, ran,
+            [&](SplitClaim cl) { return otc_impl::tt_ecb_encrypt_claim(in, out, nblocks, K, cl, st); },
             [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_ECB, in, out, nblocks, K, nullptr, cl, s); },
-            [&](uint64_t n) { return otc_impl::tt_ecb_encrypt(in, out, n, K, st); });
+            [&]() { return otc_impl::tt_ecb_encrypt(in, out, nblocks, K, st); });
     return split_claim(
-        nblocks, st, ran, [&](SplitClaim cl) { return otc_impl::tt_ecb_decrypt_claim(in, out, nblocks, K, cl, st); },
+        nunits, 2, bs_only, bs_wgs_for(bs_only), st, ran,
+        [&](SplitClaim cl) { return otc_impl::tt_ecb_decrypt_claim(in, out, nblocks, K, cl, st); },
         [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_ECB_DEC, in, out, nblocks, K, nullptr, cl, s); },
-        [&](uint64_t n) { return otc_impl::tt_ecb_decrypt(in, out, n, K, st); });
+        [&]() { return otc_impl::tt_ecb_decrypt(in, out, nblocks, K, st); });
 }
 
 hipError_t cbc_dec_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, const uint8_t iv[16],
-                         hipStream_t st, int *ran)
+                         bool bs_only, hipStream_t st, int *ran)
 {
     uint32_t ivw[4];
     memcpy(ivw, iv, 16); /* the bitsliced kernel's IV: LE words of the bytes */
     const Ctr128 ivc = ctr_from_bytes(iv);
     return split_claim(
-        nblocks, st, ran, [&](SplitClaim cl) { return otc_impl::tt_cbc_decrypt_claim(in, out, nblocks, K, ivc, cl, st); },
+        nblocks / otc_dev::CLAIM_UNIT, 2, bs_only, bs_wgs_for(bs_only), st, ran,
+        [&](SplitClaim cl) { return otc_impl::tt_cbc_decrypt_claim(in, out, nblocks, K, ivc, cl, st); },
         [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_CBC_DEC, in, out, nblocks, K, ivw, cl, s); },
-        [&](uint64_t n) { return otc_impl::tt_cbc_decrypt(in, out, n, K, ivc, st); });
+        [&]() { return otc_impl::tt_cbc_decrypt(in, out, nblocks, K, ivc, st); });
 }
 
 hipError_t cfb_dec_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, const uint32_t ivw[4],
-                         hipStream_t st, int *ran)
+                         bool bs_only, hipStream_t st, int *ran)
 {
     return split_claim(
-        nblocks, st, ran, [&](SplitClaim cl) { return otc_impl::tt_cfb_decrypt_claim(in, out, nblocks, K, ivw, cl, st); },
+        nblocks / otc_dev::CLAIM_UNIT, 2, bs_only, bs_wgs_for(bs_only), st, ran,
+        [&](SplitClaim cl) { return otc_impl::tt_cfb_decrypt_claim(in, out, nblocks, K, ivw, cl, st); },
         [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_CFB_DEC, in, out, nblocks, K, ivw, cl, s); },
-        [&](uint64_t n) { return otc_impl::tt_cfb_decrypt(in, out, n, K, ivw, st); });
+        [&]() { return otc_impl::tt_cfb_decrypt(in, out, nblocks, K, ivw, st); });
 }
 
 /* Segment decryption (CBC / CFB128 over independent segments of 2^shift
@@ -386,23 +387,20 @@ int seg_shift_of(size_t seg_blocks)
 int pick_seg_impl(int impl, int bits, size_t nbytes, size_t seg_blocks)
 {
     if (seg_shift_of(seg_blocks) < 0) return OTC_IMPL_TTABLE;
-    /* the bitsliced segment kernels run only as the split's half */
-    if (impl == OTC_IMPL_BITSLICE) return OTC_IMPL_SPLIT;
-    const int p = pick_ecb_impl(impl, bits, nbytes);
-    return p == OTC_IMPL_BITSLICE ? OTC_IMPL_SPLIT : p;
+    return pick_ecb_impl(impl, bits, nbytes);
 }
 
 hipError_t seg_dec_split(bool cfb, const void *in, void *out, size_t seg_blocks, size_t nseg, const otc_aes_key &K,
-                         Ctr128 iv0, hipStream_t st, int *ran)
+                         Ctr128 iv0, bool bs_only, hipStream_t st, int *ran)
 {
     const uint64_t nblocks = (uint64_t)seg_blocks * nseg;
     const uint32_t sh = (uint32_t)seg_shift_of(seg_blocks);
-    auto plain = [&](uint64_t) {
+    auto plain = [&]() {
         return cfb ? otc_impl::tt_cfb_decrypt_seg(in, out, seg_blocks, nseg, K, iv0, st)
                    : otc_impl::tt_cbc_decrypt_seg(in, out, seg_blocks, nseg, K, iv0, st);
     };
     return split_claim(
-        nblocks, st, ran,
+        nblocks / otc_dev::CLAIM_UNIT, 2, bs_only, bs_wgs_for(bs_only), st, ran,
         [&](SplitClaim cl) {
             return cfb ? otc_impl::tt_cfb_decrypt_seg_claim(in, out, nblocks, K, iv0, sh, cl, st)
                        : otc_impl::tt_cbc_decrypt_seg_claim(in, out, nblocks, K, iv0, sh, cl, st);
@@ -411,6 +409,41 @@ hipError_t seg_dec_split(bool cfb, const void *in, void *out, size_t seg_blocks,
             return otc_impl::bs_claim_seg(cfb ? BS_CFB_DEC_SEG : BS_CBC_DEC_SEG, in, out, nblocks, K, iv0, sh, cl, s);
         },
         plain);
+}
+
+/* Segment ENCRYPTION (CBC / CFB128, one serial chain per segment): the
+ * T-table segment kernel beside the row-sliced bs8 kernel (aes_bs8.hip),
+ * claiming 64-segment units -- the T-table one per wave from the back, bs8
+ * eight per wave from the front.  bs8 needs segments of < 8 MiB (32-bit lane
+ * offsets); at least 16 units (1024 segments) to split. */
+constexpr uint64_t SEG_UNIT = 64;
+bool segenc_bs8_ok(size_t seg_bytes) { return seg_bytes >= 16 && seg_bytes * SEG_UNIT * 8 <= 0xFFFFFFFFull; }
+
+/* auto: the split from segenc_split_min() bytes (docs/PERF.md round 5) */
+size_t segenc_split_min() { return (size_t)896 << 20; }
+
+int pick_segenc_impl(int impl, size_t nbytes, size_t seg_bytes)
+{
+    if (!segenc_bs8_ok(seg_bytes)) return OTC_IMPL_TTABLE;
+    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_SPLIT) return impl;
+    const int env = env_impl();
+    if (env != OTC_IMPL_AUTO) return env;
+    return nbytes >= segenc_split_min() ? OTC_IMPL_SPLIT : OTC_IMPL_TTABLE;
+}
+
+hipError_t seg_enc_split(bool cfb, const void *in, void *out, size_t seg_blocks, size_t nseg, const otc_aes_key &K,
+                         Ctr128 iv0, bool bs_only, hipStream_t st, int *ran)
+{
+    return split_claim(
+        nseg / SEG_UNIT, 16, bs_only, (unsigned)otc_dev::device_cus() * (bs_only ? 4u : 1u), st, ran,
+        [&](SplitClaim cl) { return otc_impl::tt_seg_encrypt_claim(cfb, in, out, seg_blocks, nseg, K, iv0, cl, st); },
+        [&](SplitClaim cl, hipStream_t s) {
+            return otc_impl::bs8_seg_encrypt_claim(cfb, in, out, seg_blocks, K, iv0, cl, s);
+        },
+        [&]() {
+            return cfb ? otc_impl::tt_cfb_encrypt_seg(in, out, seg_blocks, nseg, K, iv0, st)
+                       : otc_impl::tt_cbc_encrypt_seg(in, out, seg_blocks, nseg, K, iv0, st);
+        });
 }
 
 /* the kernel family the calling thread's last AES call ran (otc_last_impl) */
@@ -461,13 +494,17 @@ extern "C" int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, in
     return OTC_OK;
 }
 
-/* mode: 1 CTR, 0 ECB encryption, 2 decryption (ECB / CBC), 3 CFB decryption */
+/* mode: 1 CTR, 0 ECB encryption, 2 decryption (ECB / CBC), 3 CFB decryption, 4 segment decryption
+ * (power-of-two segments), 5 segment encryption (segments < 8 MiB) */
 extern "C" int otc_pick_impl(int impl, int bits, int mode, uint64_t nbytes)
 {
     if (check_impl(impl)) return -1;
     if (mode == 0 || mode == 3) return pick_ecb_impl(impl, bits, (size_t)nbytes);
     if (mode == 2) return pick_dec_impl(impl, bits, (size_t)nbytes);
-    return pick_impl(impl, bits, (size_t)nbytes);
+    if (mode == 4) return pick_seg_impl(impl, bits, (size_t)nbytes, 1);
+    if (mode == 5) return pick_segenc_impl(impl, (size_t)nbytes, 16);
+    if (mode == 1) return pick_impl(impl, bits, (size_t)nbytes);
+    return -1;
 }
 
 /* the auxiliary streams of the split (otc_release_resources) */
@@ -503,15 +540,15 @@ extern "C" int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_a
     hipError_t e;
     if (k->dir == OTC_DIR_ENCRYPT) {
         g_last_impl = pick_ecb_impl(impl, k->bits, nbytes);
-        if (g_last_impl == OTC_IMPL_SPLIT) e = ecb_split(in, out, nbytes / 16, *k, st, &g_last_impl);
-        else if (g_last_impl == OTC_IMPL_BITSLICE) e = otc_impl::bs_ecb_encrypt(in, out, nbytes / 16, *k, st);
-        else e = otc_impl::tt_ecb_encrypt(in, out, nbytes / 16, *k, st);
     } else {
         g_last_impl = pick_dec_impl(impl, k->bits, nbytes);
-        if (g_last_impl == OTC_IMPL_SPLIT) e = ecb_split(in, out, nbytes / 16, *k, st, &g_last_impl);
-        else if (g_last_impl == OTC_IMPL_BITSLICE) e = otc_impl::bs_ecb_decrypt(in, out, nbytes / 16, *k, st);
-        else e = otc_impl::tt_ecb_decrypt(in, out, nbytes / 16, *k, st);
     }
+    if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE)
+        e = ecb_split(in, out, nbytes / 16, *k, g_last_impl == OTC_IMPL_BITSLICE, st, &g_last_impl);
+    else if (k->dir == OTC_DIR_ENCRYPT)
+        e = otc_impl::tt_ecb_encrypt(in, out, nbytes / 16, *k, st);
+    else
+        e = otc_impl::tt_ecb_decrypt(in, out, nbytes / 16, *k, st);
     if (e != hipSuccess) return hip_fail(e, "aes_ecb launch");
     return OTC_OK;
 }
@@ -674,14 +711,8 @@ extern "C" int otc_aes_cbc_decrypt_impl(const void *in, void *out, size_t nbytes
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     g_last_impl = pick_dec_impl(impl, k->bits, nbytes);
-    if (g_last_impl == OTC_IMPL_SPLIT) {
-        e = cbc_dec_split(in, out, nbytes / 16, *k, iv, st, &g_last_impl);
-    } else if (g_last_impl == OTC_IMPL_BITSLICE) {
-        uint32_t w[4];
-        for (int j = 0; j < 4; ++j)
-            w[j] = (uint32_t)iv[4 * j] | (uint32_t)iv[4 * j + 1] << 8 | (uint32_t)iv[4 * j + 2] << 16 |
-                   (uint32_t)iv[4 * j + 3] << 24;
-        e = otc_impl::bs_cbc_decrypt(in, out, nbytes / 16, *k, w, false, st);
+    if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE) {
+        e = cbc_dec_split(in, out, nbytes / 16, *k, iv, g_last_impl == OTC_IMPL_BITSLICE, st, &g_last_impl);
     } else {
         e = otc_impl::tt_cbc_decrypt(in, out, nbytes / 16, *k, ctr_from_bytes(iv), st);
     }
@@ -695,8 +726,8 @@ extern "C" int otc_aes_cbc_decrypt(const void *in, void *out, size_t nbytes, con
     return otc_aes_cbc_decrypt_impl(in, out, nbytes, k, iv, OTC_IMPL_AUTO, stream);
 }
 
-extern "C" int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
-                                            const otc_aes_key *k, const uint8_t iv0[16], void *stream)
+extern "C" int otc_aes_cbc_encrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                                 const otc_aes_key *k, const uint8_t iv0[16], int impl, void *stream)
 {
     Range rg("otc_aes_cbc_encrypt_segments");
     int r = check_key(k, OTC_DIR_ENCRYPT);
@@ -705,11 +736,24 @@ extern "C" int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t se
     if (!iv0) return set_err(OTC_ERR_ARG, "null iv");
     if (nseg && seg_bytes > SIZE_MAX / nseg) return set_err(OTC_ERR_ARG, "size overflow");
     if ((r = check_bufs(in, out, seg_bytes * nseg, true, "aes_cbc_encrypt_segments"))) return r;
+    if ((r = check_impl(impl))) return r;
     if (nseg == 0 || seg_bytes == 0) return OTC_OK;
-    hipError_t e = otc_impl::tt_cbc_encrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
-                                                (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    g_last_impl = pick_segenc_impl(impl, seg_bytes * nseg, seg_bytes);
+    if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE)
+        e = seg_enc_split(false, in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
+                          g_last_impl == OTC_IMPL_BITSLICE, st, &g_last_impl);
+    else
+        e = otc_impl::tt_cbc_encrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0), st);
     if (e != hipSuccess) return hip_fail(e, "cbc_encrypt_segments launch");
     return OTC_OK;
+}
+
+extern "C" int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                            const otc_aes_key *k, const uint8_t iv0[16], void *stream)
+{
+    return otc_aes_cbc_encrypt_segments_impl(in, out, seg_bytes, nseg, k, iv0, OTC_IMPL_AUTO, stream);
 }
 
 extern "C" int otc_aes_cbc_decrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
@@ -728,8 +772,9 @@ extern "C" int otc_aes_cbc_decrypt_segments_impl(const void *in, void *out, size
     if (nseg == 0) return OTC_OK;
     hipError_t e;
     g_last_impl = pick_seg_impl(impl, k->bits, seg_bytes * nseg, sb);
-    if (g_last_impl == OTC_IMPL_SPLIT)
-        e = seg_dec_split(false, in, out, sb, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream, &g_last_impl);
+    if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE)
+        e = seg_dec_split(false, in, out, sb, nseg, *k, ctr_from_bytes(iv0), g_last_impl == OTC_IMPL_BITSLICE,
+                          (hipStream_t)stream, &g_last_impl);
     else
         e = otc_impl::tt_cbc_decrypt_seg(in, out, sb, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "cbc_decrypt_segments launch");
@@ -763,14 +808,20 @@ static int cfb_seg_common(const void *in, void *out, size_t seg_bytes, size_t ns
     hipError_t e;
     if (decrypt) {
         g_last_impl = pick_seg_impl(impl, k->bits, seg_bytes * nseg, seg_bytes / 16);
-        if (g_last_impl == OTC_IMPL_SPLIT)
-            e = seg_dec_split(true, in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream,
-                              &g_last_impl);
+        if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE)
+            e = seg_dec_split(true, in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
+                              g_last_impl == OTC_IMPL_BITSLICE, (hipStream_t)stream, &g_last_impl);
         else
             e = otc_impl::tt_cfb_decrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
                                              (hipStream_t)stream);
     } else {
-        e = otc_impl::tt_cfb_encrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream);
+        g_last_impl = pick_segenc_impl(impl, seg_bytes * nseg, seg_bytes);
+        if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE)
+            e = seg_enc_split(true, in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
+                              g_last_impl == OTC_IMPL_BITSLICE, (hipStream_t)stream, &g_last_impl);
+        else
+            e = otc_impl::tt_cfb_encrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
+                                             (hipStream_t)stream);
     }
     if (e != hipSuccess) return hip_fail(e, what);
     return OTC_OK;
@@ -779,8 +830,15 @@ static int cfb_seg_common(const void *in, void *out, size_t seg_bytes, size_t ns
 extern "C" int otc_aes_cfb128_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                                const otc_aes_key *k, const uint8_t iv0[16], void *stream)
 {
+    return otc_aes_cfb128_encrypt_segments_impl(in, out, seg_bytes, nseg, k, iv0, OTC_IMPL_AUTO, stream);
+}
+
+extern "C" int otc_aes_cfb128_encrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                                    const otc_aes_key *k, const uint8_t iv0[16], int impl,
+                                                    void *stream)
+{
     Range rg("otc_aes_cfb128_encrypt_segments");
-    return cfb_seg_common(in, out, seg_bytes, nseg, k, iv0, stream, false, "cfb128_encrypt_segments");
+    return cfb_seg_common(in, out, seg_bytes, nseg, k, iv0, stream, false, "cfb128_encrypt_segments", impl);
 }
 
 extern "C" int otc_aes_cfb128_decrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
@@ -813,10 +871,8 @@ extern "C" int otc_aes_cfb128_decrypt_impl(const void *in, void *out, size_t nby
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     g_last_impl = pick_ecb_impl(impl, k->bits, nbytes);
-    if (g_last_impl == OTC_IMPL_SPLIT)
-        e = cfb_dec_split(in, out, nbytes / 16, *k, ivw, st, &g_last_impl);
-    else if (g_last_impl == OTC_IMPL_BITSLICE)
-        e = otc_impl::bs_cfb_decrypt(in, out, nbytes / 16, *k, ivw, false, st);
+    if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE)
+        e = cfb_dec_split(in, out, nbytes / 16, *k, ivw, g_last_impl == OTC_IMPL_BITSLICE, st, &g_last_impl);
     else
         e = otc_impl::tt_cfb_decrypt(in, out, nbytes / 16, *k, ivw, st);
     if (e != hipSuccess) return hip_fail(e, "cfb_decrypt launch");

@@ -115,34 +115,24 @@ enum : int { BS_CTR = 0, BS_ECB = 1, BS_ECB_DEC = 2, BS_CBC_DEC = 3, BS_CFB_DEC 
               BS_CBC_DEC_SEG = 5, BS_CFB_DEC_SEG = 6 };
 
 /* Work claiming of a co-resident split (engine.cpp split_claim): the T-table
- * and the bitsliced kernel take OTC_CLAIM_UNIT-block units of ONE buffer from
- * a shared 64-bit counter -- the bitsliced kernel from the front (count in
- * the low 32 bits), the T-table kernel from the back (high 32 bits) -- so
- * both run until the buffer is done and finish together, whatever rate each
- * gets on the box.  Every claim is one atomic add on the whole word, valid
- * iff front + back units claimed before it < nunits, so the two ends never
- * overlap and a failed claim (nothing left) hides nothing.  A T-table claim
- * adds one unit; a bitsliced claim adds a 2048-block task (TASK_UNITS units:
- * the front count stays task-aligned) and gets the whole task, or its first
- * half when one unit was left.  With a reserve, a bitsliced wave first reads
- * the counter and stops if no more than a task plus `reserve` units are left.
- * Shipped: 2048-block units (TASK_UNITS = 1) and no reserve.  1024-block
- * T-table units, with or without a reserve of 32-160 MiB, measured 1-11%
- * slower (profiles/r4/claim_unit/; docs/PERF.md round 4, "claim unit"); the
- * knobs stay for the A/B.  A wave claims with one lane (a vector-memory
- * atomic) and broadcasts. */
-#ifndef OTC_CLAIM_UNIT
-#define OTC_CLAIM_UNIT 2048u
-#endif
-constexpr uint32_t CLAIM_UNIT = OTC_CLAIM_UNIT;
-constexpr uint32_t TASK_UNITS = 2048u / OTC_CLAIM_UNIT;
-static_assert(TASK_UNITS * CLAIM_UNIT == 2048u && TASK_UNITS <= 2, "a bitsliced task is one or two units");
-/* a front claim that got only the first half of its task (bit of the result) */
-constexpr int64_t CLAIM_HALF = 1ll << 40;
+ * and the bitsliced kernel take units of ONE buffer from a shared 64-bit
+ * counter -- the bitsliced kernel from the front (count in the low 32 bits),
+ * the T-table kernel from the back (high 32 bits) -- so both run until the
+ * buffer is done and finish together, whatever rate each gets on the box.
+ * Every claim is one atomic add on the whole word, valid iff front + back
+ * units claimed before it < nunits, so the two ends never overlap and a
+ * failed claim (nothing left) hides nothing.  A T-table claim adds one unit;
+ * a front claim adds n units and gets [f, f + min(n, nunits - used)).
+ * Units: 2048 blocks for the whole-buffer modes (one bitsliced task; 1024-
+ * block units and a reserve left to the T-table measured 1-11% slower and
+ * were removed, profiles/r4/claim_unit/); 64 segments for the chained
+ * segment encryption (one T-table wave; a bs8 task is 8 of them, aes_bs8.hip).
+ * A wave claims with one lane (a vector-memory atomic) and broadcasts. */
+constexpr uint32_t CLAIM_UNIT = 2048u;
 struct SplitClaim {
     unsigned long long *ctr; /* zeroed (stream-ordered) before the launches */
-    uint32_t nunits;         /* full CLAIM_UNIT-block units */
-    uint32_t reserve;        /* units the bitsliced side leaves to the T-table */
+    uint32_t nunits;         /* full units */
+    uint32_t wgs;            /* host side: workgroups of the kernel given this claim (0: one per CU) */
 };
 
 /* lane id from the exec-mask count: nothing to keep live across a loop
@@ -150,31 +140,41 @@ struct SplitClaim {
  * loop body, hipcc keeps it -- and spills it) */
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
-/* back: a unit index; front: a 2048-block task index, | CLAIM_HALF when
- * only its first CLAIM_UNIT blocks are claimed; -1 when nothing is left for
- * this side (wave-uniform) */
-__device__ __forceinline__ int64_t claim_unit(const SplitClaim &c, bool back)
+/* one atomic add of `inc` on the claim word; returns the old value (wave-uniform) */
+__device__ __forceinline__ uint64_t claim_add(const SplitClaim &c, unsigned long long inc)
 {
     unsigned long long old = 0;
-    if (!back && c.reserve) {
-        if (lane_id() == 0) old = __hip_atomic_load(c.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t used = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)old) +
-                              __builtin_amdgcn_readfirstlane((uint32_t)(old >> 32));
-        if (used + TASK_UNITS + c.reserve > c.nunits) return -1; /* soft: no add, so nothing hidden */
-    }
     if (lane_id() == 0) {
         /* built per claim: hoisted out of a caller's loop, the operand pair
          * would stay live (and spill) across the whole loop body */
-        unsigned long long inc = back ? (1ull << 32) : (unsigned long long)TASK_UNITS;
         asm volatile("" : "+v"(inc));
         old = __hip_atomic_fetch_add(c.ctr, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const uint32_t f = __builtin_amdgcn_readfirstlane((uint32_t)old);
     const uint32_t b = __builtin_amdgcn_readfirstlane((uint32_t)(old >> 32));
+    return (uint64_t)b << 32 | f;
+}
+
+/* back: a unit index; front: the next unit index from the front; -1 when
+ * nothing is left for this side (wave-uniform) */
+__device__ __forceinline__ int64_t claim_unit(const SplitClaim &c, bool back)
+{
+    const uint64_t old = claim_add(c, back ? (1ull << 32) : 1ull);
+    const uint32_t f = (uint32_t)old, b = (uint32_t)(old >> 32);
+    if ((uint64_t)f + b >= c.nunits) return -1;
+    return back ? (int64_t)(c.nunits - 1u - b) : (int64_t)f;
+}
+
+/* front claim of up to n units: the first unit, and *got = how many (1..n);
+ * -1 when nothing is left */
+__device__ __forceinline__ int64_t claim_front(const SplitClaim &c, uint32_t n, uint32_t *got)
+{
+    const uint64_t old = claim_add(c, n);
+    const uint32_t f = (uint32_t)old, b = (uint32_t)(old >> 32);
     const uint64_t used = (uint64_t)f + b;
     if (used >= c.nunits) return -1;
-    if (back) return (int64_t)(c.nunits - 1u - b);
-    return (int64_t)(f / TASK_UNITS) | (used + TASK_UNITS > c.nunits ? CLAIM_HALF : 0);
+    *got = (uint32_t)(c.nunits - used < n ? c.nunits - used : n);
+    return (int64_t)f;
 }
 
 /* Allocation fault injection, a test hook (otc_fault_inject_alloc): true

@@ -59,20 +59,29 @@ int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 
 /* ---- implementation selection ------------------------------------------- */
 #define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for CTR calls >= 2 GiB (AES-256:
-                               >= 1 GiB), the split below for ECB / CBC / CFB decrypt >= 896 MiB, T-table otherwise
-                               (OTC_IMPL=ttable|bitslice|split env overrides for the whole process) */
+                               >= 1 GiB), the split below for ECB / CBC / CFB decrypt and the segment modes
+                               >= 896 MiB, T-table otherwise (OTC_IMPL=ttable|bitslice|split env overrides for
+                               the whole process) */
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
-#define OTC_IMPL_BITSLICE 2 /* 32-block-per-lane bitsliced VALU kernel */
-#define OTC_IMPL_SPLIT 3    /* ECB, CBC-decrypt and CFB-decrypt: both kernels CONCURRENTLY on disjoint ranges (the bitsliced
-                               one on an auxiliary stream), co-resident on every CU -- LDS and VALU busy at
-                               once; "auto" for these calls >= 896 MiB.  CTR: as auto */
+#define OTC_IMPL_BITSLICE 2 /* bitsliced VALU kernel alone: 32 blocks per lane (CTR, ECB, the decryptions; their
+                               claim kernels take every 2048-block unit and one T-table workgroup the blocks past
+                               the last), 8 chains per lane for segment encryption (bs8) */
+#define OTC_IMPL_SPLIT 3    /* ECB, the CBC / CFB decryptions and the segment modes: the T-table and the bitsliced
+                               kernel CONCURRENTLY over one buffer (the bitsliced one on an auxiliary stream),
+                               co-resident on every CU -- LDS and VALU busy at once -- claiming units from one
+                               counter; "auto" for these calls >= 896 MiB.  CTR: as auto */
 
 /* The kernel family `impl` resolves to for a call of nbytes with a bits-bit
  * key (mode 1: CTR, 0: ECB encryption, 2: ECB / CBC decryption, 3: CFB128
- * decryption); -1 for an invalid impl. */
+ * decryption, 4: CBC / CFB128 decryption of power-of-two segments, 5: CBC /
+ * CFB128 encryption of segments < 8 MiB); -1 for an invalid impl or mode. */
 int otc_pick_impl(int impl, int bits, int mode, uint64_t nbytes);
-/* OTC_IMPL_TTABLE / OTC_IMPL_BITSLICE: what the calling thread's last
- * otc_aes_ctr / otc_aes_ecb call ran (OTC_IMPL_AUTO before any call). */
+/* What the calling thread's last AES call ran: OTC_IMPL_TTABLE,
+ * OTC_IMPL_BITSLICE or OTC_IMPL_SPLIT (OTC_IMPL_AUTO before any call).  Set
+ * by otc_aes_ctr / _rfc3686 / _ctr_stream, otc_aes_ecb, the CBC / CFB128
+ * decryptions and every segment call; a split or bitsliced request that fell
+ * back to the T-table (too few units, no memory for the claim counter) reports
+ * OTC_IMPL_TTABLE. */
 int otc_last_impl(void);
 
 /* ---- device ops (device pointers; async on `stream`) ---------------------
@@ -126,6 +135,13 @@ int otc_aes_cbc_decrypt_impl(const void *in, void *out, size_t nbytes, const otc
  * A single segment (nseg == 1) is exact single-stream CBC, serial. */
 int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                  const otc_aes_key *k, const uint8_t iv0[16], void *stream);
+/* _impl: with a kernel choice.  OTC_IMPL_SPLIT: the T-table segment kernel
+ * beside the row-sliced bs8 kernel (8 chains per lane), both claiming
+ * 64-segment units; OTC_IMPL_BITSLICE: bs8 alone (the T-table runs the
+ * segments past the last unit); "auto" splits from 896 MiB.  Segments of
+ * >= 8 MiB and calls under 1024 segments: the T-table. */
+int otc_aes_cbc_encrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                      const otc_aes_key *k, const uint8_t iv0[16], int impl, void *stream);
 /* Same, decryption side (fully parallel).  _impl: with a kernel choice --
  * "auto" runs the T-table + bitsliced split for >= 896 MiB of power-of-two
  * segments (OTC_IMPL_BITSLICE means the split here: the bitsliced segment
@@ -141,6 +157,8 @@ int otc_aes_cbc_decrypt_segments_impl(const void *in, void *out, size_t seg_byte
  * directions.  Encrypt may run in place; decrypt may not. */
 int otc_aes_cfb128_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                     const otc_aes_key *k, const uint8_t iv0[16], void *stream);
+int otc_aes_cfb128_encrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
+                                         const otc_aes_key *k, const uint8_t iv0[16], int impl, void *stream);
 int otc_aes_cfb128_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                     const otc_aes_key *k, const uint8_t iv0[16], void *stream);
 int otc_aes_cfb128_decrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
@@ -352,6 +370,8 @@ int otc_multi_ctr_resident(int ngpus, void *const *dev_bufs, size_t shard_bytes,
 
 /* Library self description / tests */
 int otc_bitslice_selftest(int verbose);
+/* the row-sliced chain kernel's arithmetic (otc_bs8.h) against the C oracle */
+int otc_bs8_selftest(int verbose);
 const char *otc_build_info(void);
 
 #ifdef __cplusplus

@@ -133,6 +133,7 @@ def _declare_cpu(lib):
         "AES_CTR_encrypt": (None, [c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int]),
         "AES_CTR_encrypt_at": (None, [c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int, ctypes.c_ulonglong]),
         "otc_bitslice_selftest": (c_int, [c_int]),
+        "otc_bs8_selftest": (c_int, [c_int]),
         "AES_CBC_encrypt": (None, [c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int]),
         "AES_CFB128_encrypt": (None, [c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int]),
         "aes_monte_carlo": (c_int, [c_int, c_int, c_u8p]),
@@ -175,6 +176,8 @@ def _declare_gpu(lib):
         "otc_stream_destroy": (None, [c_vp]),
         "otc_stream_join": (c_int, [c_vp, c_vp]),
         "otc_aes_cbc_encrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
+        "otc_aes_cbc_encrypt_segments_impl": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_int, c_vp]),
+        "otc_aes_cfb128_encrypt_segments_impl": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_int, c_vp]),
         "otc_aes_cbc_decrypt_segments": (c_int, [c_vp, c_vp, c_sz, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cfb128_decrypt": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_vp]),
         "otc_aes_cfb128_decrypt_impl": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_int, c_vp]),

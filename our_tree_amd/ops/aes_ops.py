@@ -31,7 +31,7 @@ def _impl(impl) -> int:
 _IMPL_NAMES = {v: k for k, v in IMPLS.items()}
 
 
-_PICK_MODES = {"ctr": 1, "ecb": 0, "dec": 2, "ecb-dec": 2, "cbc-dec": 2, "cfb-dec": 3}
+_PICK_MODES = {"ctr": 1, "ecb": 0, "dec": 2, "ecb-dec": 2, "cbc-dec": 2, "cfb-dec": 3, "seg-dec": 4, "seg-enc": 5}
 
 
 def pick_impl(impl="auto", bits: int = 128, mode: str = "ctr", nbytes: int = 0) -> str:
@@ -495,31 +495,25 @@ def cbc_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None, impl="auto") -
     return out
 
 
-def cbc_encrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None) -> torch.Tensor:
+def cbc_encrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None,
+                         impl="auto") -> torch.Tensor:
     """CBC encryption of independent contiguous segments; segment s uses
-    IV = iv0 + s (128-bit BE), one serial chain per GPU lane.  A single
-    segment is exact serial CBC on ONE lane -- use ``models.AES.cbc_encrypt``
-    (routes exact single-stream encryption to the host AES-NI chain) unless
-    the buffer is small."""
-    _check_dev(x, "x")
-    out = _out_like(x, out)
-    n = _nbytes(x)
-    if segment_bytes <= 0 or n % segment_bytes:
-        raise ValueError("byte size must be a multiple of segment_bytes")
-    k = expand_key(key)
-    with torch.cuda.device(x.device):
-        rc = _run(x, out, lambda ip, op: _lib().otc_aes_cbc_encrypt_segments(ip, op, segment_bytes, n // segment_bytes,
-            ctypes.byref(k), _b16(iv0, "iv0"), _stream(x)))
-    _native.check(rc, "otc_aes_cbc_encrypt_segments")
-    return out
+    IV = iv0 + s (128-bit BE), one serial chain per segment.  ``impl``:
+    "ttable" (one chain per lane), "bitslice" (the row-sliced bs8 kernel, 8
+    chains per lane), "split" (both at once over the buffer, claiming
+    64-segment units) or "auto" (split from 896 MiB of segments < 8 MiB).  A
+    single segment is exact serial CBC on ONE lane -- use
+    ``models.AES.cbc_encrypt`` (routes exact single-stream encryption to the
+    host AES-NI chain) unless the buffer is small.  May run in place."""
+    return _seg_call("otc_aes_cbc_encrypt_segments_impl", x, key, iv0, segment_bytes, out, True, impl)
 
 
 def cbc_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None,
                          impl="auto") -> torch.Tensor:
     """Inverse of ``cbc_encrypt_segments``: fully parallel.  ``impl``:
-    "ttable", or "split" / "bitslice" (the T-table + bitsliced split: the
-    bitsliced segment kernel runs only beside the T-table), "auto" = split
-    from 896 MiB of power-of-two segments."""
+    "ttable", "bitslice" (the bitsliced claim kernel alone), "split" (both at
+    once), "auto" = split from 896 MiB of power-of-two segments (other
+    segment sizes: the T-table)."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     n = _nbytes(x)
@@ -548,7 +542,8 @@ def cfb128_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None, impl="auto"
     return out
 
 
-def _seg_call(fn_name: str, x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out, inplace_ok: bool):
+def _seg_call(fn_name: str, x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out, inplace_ok: bool,
+              impl="auto"):
     _check_dev(x, "x")
     out = _out_like(x, out)
     n = _nbytes(x)
@@ -557,15 +552,16 @@ def _seg_call(fn_name: str, x: torch.Tensor, key: bytes, iv0: bytes, segment_byt
     k = expand_key(key)
     with torch.cuda.device(x.device):
         rc = _run(x, out, lambda ip, op: getattr(_lib(), fn_name)(ip, op, segment_bytes, n // segment_bytes,
-                  ctypes.byref(k), _b16(iv0, "iv0"), _stream(x)), inplace_ok=inplace_ok)
+                  ctypes.byref(k), _b16(iv0, "iv0"), _impl(impl), _stream(x)), inplace_ok=inplace_ok)
     _native.check(rc, fn_name)
     return out
 
 
-def cfb128_encrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None) -> torch.Tensor:
+def cfb128_encrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None,
+                            impl="auto") -> torch.Tensor:
     """CFB128 encryption of independent segments (IV_s = iv0 + s), one
-    serial chain per lane (the CBC sector kernel with the CFB chain step)."""
-    return _seg_call("otc_aes_cfb128_encrypt_segments", x, key, iv0, segment_bytes, out, True)
+    serial chain per segment (``impl`` as ``cbc_encrypt_segments``)."""
+    return _seg_call("otc_aes_cfb128_encrypt_segments_impl", x, key, iv0, segment_bytes, out, True, impl)
 
 
 def cfb128_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None,

@@ -1,76 +1,79 @@
-"""The work-claiming protocol of the co-resident split (csrc/hip/otc_device.h
-claim_unit, engine.cpp split_claim), replayed on the host: any interleaving
-of front (bitsliced, a whole task of TASK units) and back (T-table, one unit)
-claims on the one 64-bit counter hands out every unit exactly once, with the
-bitsliced tasks aligned and clear of the reserve, including the claims that
-arrive after the buffer is exhausted (they still add to the counter)."""
+"""The co-resident split's work-claim protocol (csrc/hip/otc_device.h
+claim_unit / claim_front), modelled on the CPU: one 64-bit word, front
+(bitsliced) count in the low half, back (T-table) count in the high half,
+every claim one atomic add.  Any interleaving of claims must hand out every
+unit exactly once -- front claims of n units (1 for the 2048-block split, 8
+for the bs8 segment-encryption kernel, which gets a partial task at the
+meeting point) and back claims of one -- and a failed claim takes nothing."""
 import random
 
 import pytest
 
 
-TASKS = (1, 2)  # units per bitsliced task, 2048 / OTC_CLAIM_UNIT: shipped 1, the A/B build 2
-
-
-def claim(counter, nunits, back, reserve=0, TASK=1):
-    """the soft reserve check (a plain read, no add), then one atomic add on
-    the word + the validity rule; returns (counter, claimed units)"""
+def claim(counter, nunits, back, n=1):
+    """one atomic add; returns (new counter, list of units claimed)"""
     f, b = counter & 0xFFFFFFFF, counter >> 32
-    if not back and reserve and f + b + TASK + reserve > nunits:
-        return counter, None  # stop without adding
-    old = counter
-    counter = (counter + ((1 << 32) if back else TASK)) & ((1 << 64) - 1)
-    f, b = old & 0xFFFFFFFF, old >> 32
-    if f + b >= nunits:
-        return counter, None
+    counter += (1 << 32) if back else n
+    used = f + b
+    if used >= nunits:
+        return counter, []
     if back:
         return counter, [nunits - 1 - b]
-    assert f % TASK == 0
-    half = f + b + TASK > nunits  # CLAIM_HALF: only the task's first unit
-    return counter, [f] if half else list(range(f, f + TASK))
+    got = min(n, nunits - used)
+    return counter, list(range(f, f + got))
 
 
-@pytest.mark.parametrize("task", TASKS)
-@pytest.mark.parametrize("seed", range(60))
-def test_every_unit_once(seed, task):
-    rnd = random.Random(seed)
-    nunits = rnd.choice([1, 4, 5, 7, 64, 1000, 4097])
-    reserve = rnd.choice([0, 0, 1, 3, 100])
-    front_waves, back_waves = rnd.randint(1, 40), rnd.randint(1, 200)
-    waves = [("f", i) for i in range(front_waves)] + [("b", i) for i in range(back_waves)]
-    live = set(waves)
-    counter, got = 0, []
-    while live:
-        w = rnd.choice(sorted(live))  # any wave may claim next: the atomics' order
-        counter, us = claim(counter, nunits, w[0] == "b", reserve, task)
-        if us is None:
-            live.discard(w)  # a wave stops at its first failed claim
-        else:
-            got += [(u, w[0]) for u in us]
-    units = sorted(u for u, _ in got)
-    assert units == list(range(nunits))  # all, none twice
-    # the bitsliced side holds a prefix, the T-table side the matching suffix
-    front = sorted(u for u, s in got if s == "f")
-    assert front == list(range(len(front)))
+@pytest.mark.parametrize("n", [1, 8])
+def test_every_unit_exactly_once(n):
+    rnd = random.Random(1234 + n)
+    for _ in range(300):
+        nunits = rnd.randint(1, 300)
+        counter, seen, front = 0, [], []
+        waves = ["b"] * rnd.randint(1, 20) + ["f"] * rnd.randint(0, 20)
+        live = list(waves)
+        while live:
+            w = rnd.randrange(len(live))  # any wave may claim next: the atomics' order
+            counter, us = claim(counter, nunits, live[w] == "b", n)
+            if not us:
+                live.pop(w)  # a wave whose claim failed exits its loop
+            elif live[w] == "f":
+                front += us
+            seen += us
+        assert sorted(seen) == list(range(nunits)), (nunits, waves)  # all, none twice
+        # the bitsliced side holds a prefix, the T-table side the matching suffix
+        assert sorted(front) == list(range(len(front)))
 
 
-@pytest.mark.parametrize("task", TASKS)
-def test_reserve_is_soft_but_kept_without_races(task):
-    """With claims in sequence (no read-to-add race), the bitsliced side
-    stops with more than `reserve` units left to the T-table."""
-    nunits, reserve = 1000, 37
-    counter, front = 0, 0
+def test_front_partial_task_at_the_meeting_point():
+    """A bs8 front claim with fewer than 8 units left gets exactly the rest
+    (its chains past the claim load chain 0 and store nothing), and later
+    claims of either side fail."""
+    counter = 0
+    counter, us = claim(counter, 19, False, 8)
+    assert us == list(range(8))
+    counter, us = claim(counter, 19, True)
+    assert us == [18]
+    counter, us = claim(counter, 19, False, 8)
+    assert us == list(range(8, 16))
+    counter, us = claim(counter, 19, False, 8)
+    assert us == [16, 17]
+    for back in (True, False):
+        counter, us = claim(counter, 19, back, 8)
+        assert us == []
+
+
+def test_bitsliced_only_mode():
+    """impl "bitslice": the T-table kernel's own word starts at
+    back = nunits, so every one of its claims fails and the front side alone
+    takes every unit."""
+    nunits = 37
+    tt_word = nunits << 32
+    tt_word, us = claim(tt_word, nunits, True)
+    assert us == []
+    counter, seen = 0, []
     while True:
-        counter, us = claim(counter, nunits, False, reserve, task)
-        if us is None:
+        counter, us = claim(counter, nunits, False, 8)
+        if not us:
             break
-        front += len(us)
-    assert nunits - front >= reserve and front % task == 0
-
-
-def test_counter_halves_cannot_carry():
-    """Counts stay far below 2^32 (units <= 2^31 - 1, plus one failed claim
-    per wave), so the front half never carries into the back half."""
-    nunits = (1 << 31) - 1
-    waves = 1 << 14
-    assert nunits + waves < (1 << 32)
+        seen += us
+    assert seen == list(range(nunits))

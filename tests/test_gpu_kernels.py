@@ -480,20 +480,17 @@ def test_ecb_split_matches_ttable(gpu, bits):
 
 
 @pytest.mark.parametrize("k", [4, 5, 7, 64 * 5 + 1])
-def test_split_bitsliced_alone(gpu, k, monkeypatch):
-    """With OTC_SPLIT_TEST_BS_ONLY the T-table claim kernel claims nothing (it
-    only runs the remainder past the last unit), so the bitsliced claim
-    kernel takes every unit of the buffer.  Every split mode (ECB in place,
-    ECB / CBC / CFB decryption, segment decryption) still equals the T-table;
-    so does a run with a reserve left to the T-table (OTC_SPLIT_RESERVE_MIB).
-    In a 1024-block-unit build (scripts/r4_unit_ab.sh) an odd k makes the
-    bitsliced kernel's last claim a half task: slots 16-31 redo slots 0-15
-    instead of touching the blocks past the unit."""
+def test_split_bitsliced_alone(gpu, k):
+    """impl="bitslice" for the whole-buffer modes is the bitsliced claim
+    kernel alone: the T-table claim kernel's counter starts full, so one
+    T-table workgroup runs only the remainder past the last unit and the
+    bitsliced kernel (three workgroups per CU) takes every unit.  Every split
+    mode (ECB in place, ECB / CBC / CFB decryption, segment decryption) still
+    equals the T-table."""
     key, iv = os.urandom(32), os.urandom(16)
-    nunits = k
-    n = (k * 1024 + 300) * 16
+    n = (k * 2048 + 300) * 16
     x = torch.empty(n, dtype=torch.uint8, device=gpu)
-    ops.fill_random_(x, seed=nunits)
+    ops.fill_random_(x, seed=k)
     calls = {
         "ecb": lambda x, impl: ops.ecb_encrypt(x, key, impl=impl),
         "ecb-dec": lambda x, impl: ops.ecb_decrypt(x, key, impl=impl),
@@ -502,22 +499,55 @@ def test_split_bitsliced_alone(gpu, k, monkeypatch):
         "cbc-dec-seg": lambda x, impl: ops.cbc_decrypt_segments(x[:n - n % 4096], key, iv, 4096, impl=impl),
         "cfb-dec-seg": lambda x, impl: ops.cfb128_decrypt_segments(x[:n - n % 4096], key, iv, 4096, impl=impl),
     }
-    for env in ({"OTC_SPLIT_TEST_BS_ONLY": "1"}, {"OTC_SPLIT_RESERVE_MIB": "1"}):
-        for name, f in calls.items():
-            t = f(x, "ttable")
-            for k, v in env.items():
-                monkeypatch.setenv(k, v)
-            y = f(x, "split")
-            assert ops.last_impl() == "split", (name, env)
-            if name == "ecb":
-                w = x.clone()
-                ops.ecb_encrypt(w, key, out=w, impl="split")
-            for k in env:
-                monkeypatch.delenv(k)
+    for name, f in calls.items():
+        t = f(x, "ttable")
+        y = f(x, "bitslice")
+        assert ops.last_impl() == "bitslice", name
+        torch.cuda.synchronize()
+        assert torch.equal(y, t), (name, k)
+        if name == "ecb":
+            w = x.clone()
+            ops.ecb_encrypt(w, key, out=w, impl="bitslice")
             torch.cuda.synchronize()
-            assert torch.equal(y, t), (name, nunits, env)
-            if name == "ecb":
-                assert torch.equal(w, t), (nunits, env, "in place")
+            assert torch.equal(w, t), (k, "in place")
+
+
+@pytest.mark.parametrize("bits", KEYBITS)
+def test_segment_encrypt_split_matches_oracle(gpu, bits):
+    """CBC / CFB128 ENCRYPTION of independent segments through the row-sliced
+    bs8 kernel (8 chains per lane, aes_bs8.hip) -- alone ("bitslice") and
+    beside the T-table claim kernel ("split", 64-segment units from one
+    counter) -- equals the T-table kernel and the CPU oracle: 1-block,
+    512-byte, non-power-of-two and 4 KiB segments, a unit count that leaves a
+    partial last bs8 task, segments past the last unit (T-table workgroup 0),
+    an IV_s carry across the low 64 bits, in place and out of place."""
+    key = os.urandom(bits // 8)
+    iv0 = os.urandom(8) + (2**64 - 700).to_bytes(8, "big")
+    for seg, nseg in ((16, 64 * 19 + 37), (512, 64 * 19 + 37), (528, 64 * 17 + 5), (4096, 64 * 40 + 63),
+                      (4096, 64 * 8 * 12)):
+        n = seg * nseg
+        x = torch.empty(n, dtype=torch.uint8, device=gpu)
+        ops.fill_random_(x, seed=seg ^ bits ^ nseg)
+        hx = host(x)
+        for name in ("cbc", "cfb"):
+            f = ops.cbc_encrypt_segments if name == "cbc" else ops.cfb128_encrypt_segments
+            ref = cpu_ref.cbc_segments if name == "cbc" else cpu_ref.cfb128_segments
+            t = f(x, key, iv0, seg, impl="ttable")
+            assert ops.last_impl() == "ttable"
+            for impl in ("bitslice", "split"):
+                y = f(x, key, iv0, seg, impl=impl)
+                assert ops.last_impl() == impl, (name, seg, nseg, impl)
+                w = x.clone()
+                f(w, key, iv0, seg, out=w, impl=impl)
+                torch.cuda.synchronize()
+                assert torch.equal(y, t), (name, bits, seg, nseg, impl)
+                assert torch.equal(w, t), (name, bits, seg, nseg, impl, "in place")
+            hy = host(t)
+            for s0 in (0, nseg // 2, nseg - 4):
+                lo, hi = s0 * seg, (s0 + 4) * seg
+                assert hy[lo:hi] == ref(key, sh.ctr_add(iv0, s0), hx[lo:hi], seg), (name, bits, seg, s0)
+    assert ops.pick_impl("auto", 256, "seg-enc", 896 << 20) == "split"
+    assert ops.pick_impl("auto", 256, "seg-enc", (896 << 20) - 16) == "ttable"
 
 
 def test_ecb_split_stream_order(gpu):

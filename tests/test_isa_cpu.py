@@ -33,9 +33,12 @@ def counts():
 
 
 def test_every_bulk_kernel_found(counts):
-    for mode in ("CTR", "ECB", "ECB-dec", "CBC-dec", "CFB-dec"):
+    """CTR has a bulk launch; ECB and the decryptions run only as claim
+    kernels (beside the T-table, or alone for impl "bitslice")."""
+    for mode in ("CTR", "ECB-claim", "ECB-dec-claim", "CBC-dec-claim", "CFB-dec-claim"):
         for bits in ("AES-128", "AES-192", "AES-256"):
             assert (mode, bits) in counts, (mode, bits, sorted(counts))
+    assert not any(k[0] in ("ECB", "ECB-dec", "CBC-dec", "CFB-dec") for k in counts), sorted(counts)
 
 
 def test_bulk_kernels_spill_free(counts):
@@ -107,3 +110,37 @@ def test_split_pairs_share_a_simd():
             assert 4 * alloc(t) + alloc(b) <= 512, (mode, nr, t, b)
             seen += 1
     assert seen == 18
+
+
+def _vgprs(obj):
+    import tempfile
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_count
+
+    with tempfile.TemporaryDirectory() as tmp:
+        return isa_count.metadata(isa_count.code_object(obj, tmp))
+
+
+def test_bs8_segment_pair_shares_a_simd():
+    """The chained segment-encryption split: the row-sliced bs8 kernel
+    (csrc/hip/aes_bs8.hip, <= 128 VGPRs, no scratch) fits one wave per SIMD
+    beside the 4 waves of the T-table segment claim kernel, for CBC and CFB at
+    every key size."""
+    tt_obj = os.path.join(ROOT, "build", "obj", "hip", "aes_tt.o")
+    bs8_obj = os.path.join(ROOT, "build", "obj", "hip", "aes_bs8.o")
+    if not os.path.exists(tt_obj) or not os.path.exists(bs8_obj) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):
+        pytest.skip("no built objects (make) or no ROCm LLVM tools")
+    tt, b8 = _vgprs(tt_obj), _vgprs(bs8_obj)
+    alloc = lambda n: -(-n // 8) * 8
+    seen = 0
+    for nr in (10, 12, 14):
+        for cfb in ("0", "1"):
+            tn = [k for k in tt if "k_aes_seg_enc_tt_claim" in k and f"ILi{nr}E" in k and f"ELb{cfb}E" in k]
+            bn = [k for k in b8 if "k_aes_bs8_seg_claim" in k and f"ILi{nr}ELb{cfb}E" in k]
+            assert tn and bn, (nr, cfb, sorted(b8))
+            t, b = max(tt[k][0] for k in tn), max(b8[k][0] for k in bn)
+            assert b <= 128 and all(b8[k][1] == 0 for k in bn), (nr, cfb, b)
+            assert 4 * alloc(t) + alloc(b) <= 512, (nr, cfb, t, b)
+            seen += 1
+    assert seen == 6
