@@ -35,7 +35,7 @@ endif
 LIBDIR := our_tree_amd/lib
 OBJ    := build/obj
 
-CPU_SRC := csrc/cpu/aes.c csrc/cpu/arc4.c csrc/cpu/rc4.c csrc/cpu/aesni.c csrc/cpu/numa.c
+CPU_SRC := csrc/cpu/aes.c csrc/cpu/arc4.c csrc/cpu/rc4.c csrc/cpu/aesni.c csrc/cpu/numa.c csrc/cpu/rccl_plan.c
 CPU_OBJ := $(patsubst csrc/cpu/%.c,$(OBJ)/cpu/%.o,$(CPU_SRC)) $(OBJ)/cpu/bs_selftest.o
 HIP_SRC := csrc/hip/aes_tt.hip csrc/hip/aes_bs.hip csrc/hip/aes_bs8.hip csrc/hip/stream_ops.hip
 HIP_OBJ := $(patsubst csrc/hip/%.hip,$(OBJ)/hip/%.o,$(HIP_SRC)) $(OBJ)/hip/engine.o $(OBJ)/hip/pipeline.o

@@ -462,8 +462,10 @@ def main():
         extra["rccl_ranks"] = sc["ranks"]
         extra["rccl_ranks_verified"] = sc["ranks_verified"]
         extra["rccl_backend"] = sc["backend"]
+        extra["rccl_transport"] = sc["transport"]  # "xgmi" only over RCCL; gloo rehearsals: "host"
         extra["rccl_xgmi_bytes_verified"] = sc["xgmi_bytes_verified"]
         extra["rccl_xgmi_bytes_timed"] = sc["xgmi_bytes_timed"]
+        extra["rccl_host_bytes_verified"] = sc["host_bytes_verified"]
         extra["rccl_scatter_bytes"] = sc["total_bytes"]
         extra["rccl_scatter_verified"] = sc["verified"]
         if not sc["verified"]:

@@ -81,7 +81,9 @@ def main():
                           "value": round(res["gbps"], 3), "unit": "GB/s", "verified_sample": res["verified"],
                           "ranks": res["ranks"], "ranks_verified": res["ranks_verified"],
                           "backend": res["backend"], "collectives": res["collectives"],
+                          "transport": res["transport"],
                           "xgmi_bytes_verified": res["xgmi_bytes_verified"],
+                          "host_bytes_verified": res["host_bytes_verified"],
                           "xgmi_bytes_timed": res["xgmi_bytes_timed"],
                           "data": "synthetic random (root GPU fill)"}), flush=True)
     if torch.distributed.is_initialized():

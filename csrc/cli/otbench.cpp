@@ -8,6 +8,8 @@
  *           [--bits 128] [--bytes 1G] [--iters 20] [--warmup 3]
  *           [--impl auto|ttable|bitslice|split] [--inplace] [--verify] [--clock]
  *           [--mark]                        "OTB_MARK start|end" on stderr around the timed loop
+ *           [--split-stats]                 one extra call after the loop: units each side of a
+ *                                           split took ("split_units": [bitsliced, T-table, all])
  *           [--corrupt-at OFF]              test hook: flip output byte OFF after the
  *                                           verified op (verification must then fail)
  *           [--e2e --chunk 256M]            host-resident, pinned pipeline
@@ -65,7 +67,7 @@ struct Cfg {
     size_t bytes = 1ull << 30;
     int iters = 20, warmup = 3;
     int impl = OTC_IMPL_AUTO;
-    bool inplace = false, verify = false, e2e = false, clock = false, mark = false;
+    bool inplace = false, verify = false, e2e = false, clock = false, mark = false, split_stats = false;
     long long corrupt_at = -1;
     size_t chunk = 256ull << 20;
     int gpus = 1, strategy = 0;
@@ -373,6 +375,7 @@ int main(int argc, char **argv)
         else if (a == "--verify") c.verify = true;
         else if (a == "--clock") c.clock = true;
         else if (a == "--mark") c.mark = true;
+        else if (a == "--split-stats") c.split_stats = true;
         else if (a == "--corrupt-at") c.corrupt_at = atoll(nx());
         else if (a == "--e2e") c.e2e = true;
         else if (a == "--chunk") c.chunk = parse_size(nx());
@@ -552,17 +555,30 @@ int main(int argc, char **argv)
         return 1;
     }
     if (c.mark) mark("end");
+    char split_units[96] = "";
     const double gbps = c.bytes / (ms * 1e6);
+    if (c.split_stats) { /* one more call, after the timed loop: which side took how many units */
+        uint64_t f = 0, b = 0, n = 0;
+        otc_split_stats(1);
+        const int rs = run_op(&a) || otc_split_last_units(&f, &b, &n);
+        otc_split_stats(0);
+        if (rs) {
+            fprintf(stderr, "split stats: %s\n", otc_last_error());
+            return 1;
+        }
+        snprintf(split_units, sizeof split_units, "\"split_units\": [%" PRIu64 ", %" PRIu64 ", %" PRIu64 "], ", f, b, n);
+    }
     const double cpb = (ms * 1e-3) * clk_hz * cus / (double)c.bytes;
     double held = 0.0;
     if (c.clock && otc_measure_clock(run_op, &a, &held)) {
         fprintf(stderr, "clock: %s\n", otc_last_error());
         return 1;
     }
-    char clk[224] = "";
+    char clk[320] = "";
     if (c.clock)
         snprintf(clk, sizeof clk, "\"held_clock_ghz\": %.3f, \"cycles_per_byte_per_cu_held\": %.3f, ", held,
                  (ms * 1e-3) * held * 1e9 * cus / (double)c.bytes);
+    strncat(clk, split_units, sizeof clk - strlen(clk) - 1);
     if (c.mode.size() > 6 && c.mode.compare(c.mode.size() - 6, 6, "-split") == 0)
         snprintf(clk + strlen(clk), sizeof clk - strlen(clk), "\"share\": %.3f, ", c.share);
     const int ran = otc_last_impl(); /* what the last timed call ran (this thread) */

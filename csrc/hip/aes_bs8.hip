@@ -25,6 +25,8 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "otc_bs8.h"
 #include "otc_device.h"
 
@@ -75,6 +77,13 @@ struct Bs8Terms {
     }
 };
 
+/* f(integral_constant<int, T>) for each T, in order */
+template <int... T, class F>
+__device__ __forceinline__ void for_each_c(std::integer_sequence<int, T...>, F f)
+{
+    (f(std::integral_constant<int, T>{}), ...);
+}
+
 using gptr = __attribute__((address_space(1))) uint8_t *;
 using gcptr = const __attribute__((address_space(1))) uint8_t *;
 
@@ -83,6 +92,11 @@ using gcptr = const __attribute__((address_space(1))) uint8_t *;
  *   base + j * 16 + k * chain_bytes + l * seg_bytes
  * (uniform 64-bit base + 32-bit offsets: global loads / stores with an SGPR
  * base and one VGPR offset). */
+#ifndef OTC_BS8_BURST
+#define OTC_BS8_BURST 1 /* plaintext blocks per chain per load burst (A/B knob) */
+#endif
+constexpr int BURST = OTC_BS8_BURST;
+
 template <int NR, bool CFB, bool FULL>
 __device__ __forceinline__ void bs8_task(const Bs8Params &P, uint64_t u0, uint32_t n)
 {
@@ -118,68 +132,96 @@ __device__ __forceinline__ void bs8_task(const Bs8Params &P, uint64_t u0, uint32
     pin_n(s, 32);
 
     const uint64_t sb = P.seg_blocks;
-    uint4 pt[8];
-    auto load = [&](uint64_t j) {
+    /* plaintext in bursts of BURST blocks per chain (32-64 contiguous bytes
+     * instead of 16 per cache line visit), loaded right after the last add of
+     * the previous burst: the rounds of one step cover the latency */
+    uint4 pt[BURST][8];
+    auto load = [&](uint64_t j0) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            pt[k] = *(const uint4 *)(ib + j * 16 + kk(k) * cb + lo);
-    };
-    auto store = [&](uint64_t j) {
+        for (int t = 0; t < BURST; ++t) {
+            const uint64_t j = j0 + t < sb ? j0 + t : sb - 1; /* a short last burst re-reads a valid block */
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if (FULL || (uint32_t)k < n)
-                *(uint4 *)(ob + j * 16 + k * cb + lo) =
-                    make_uint4(s[k] ^ kl0, s[8 + k] ^ kl1, s[16 + k] ^ kl2, s[24 + k] ^ kl3);
-    };
-    auto add_pt = [&]() {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            s[k] ^= pt[k].x;
-            s[8 + k] ^= pt[k].y;
-            s[16 + k] ^= pt[k].z;
-            s[24 + k] ^= pt[k].w;
+            for (int k = 0; k < 8; ++k) pt[t][k] = *(const uint4 *)(ib + j * 16 + kk(k) * cb + lo);
         }
     };
-    /* one loop shape for both modes: planes -> words, store / add the
-     * plaintext, words -> planes, prefetch, rounds.  CBC adds p_j to
-     * F_{j-1} before the rounds of step j; CFB adds p_j to F_j after them, so
-     * its rounds run one step ahead (the first before the loop, none after
-     * the last block) */
+    /* CBC stores c_{j-1} = F_{j-1} ^ k_NR after adding p_j (s = F_{j-1} ^ p_j,
+     * so c_{j-1} = s ^ p_j ^ k_NR, one v_bitop3 per word): the stores then
+     * follow the plaintext wait instead of preceding it -- in the other order
+     * hipcc waits for the stores too (vmcnt(0) per step, the loop's merged
+     * counts).  CFB stores y_j ^ k_NR. */
+    auto store = [&](uint64_t j, int t) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (FULL || (uint32_t)k < n) {
+                uint4 v = make_uint4(s[k] ^ kl0, s[8 + k] ^ kl1, s[16 + k] ^ kl2, s[24 + k] ^ kl3);
+                if (!CFB) {
+                    v.x ^= pt[t][k].x;
+                    v.y ^= pt[t][k].y;
+                    v.z ^= pt[t][k].z;
+                    v.w ^= pt[t][k].w;
+                }
+                *(uint4 *)(ob + j * 16 + k * cb + lo) = v;
+            }
+    };
+    auto add_pt = [&](int t) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            s[k] ^= pt[t][k].x;
+            s[8 + k] ^= pt[t][k].y;
+            s[16 + k] ^= pt[t][k].z;
+            s[24 + k] ^= pt[t][k].w;
+        }
+    };
+    /* one loop shape for both modes: planes -> words, add the plaintext,
+     * store, words -> planes, (prefetch), rounds.  CBC adds p_j to F_{j-1}
+     * before the rounds of step j; CFB adds p_j to F_j after them, so its
+     * rounds run one step ahead (the first before the loop, none after the
+     * last block) */
+    load(0);
     if (CFB) {
         otc_bs8::rounds<NR>(s, kt);
         pin_n(s, 32);
         sched_fence();
     }
-    load(0);
-    for (uint64_t j = 0; j < sb; ++j) {
-        transpose32(s);
-        if (CFB) {
-            add_pt();
-            store(j);
-        } else {
-            if (j > 0) store(j - 1);
-            add_pt();
+    /* step t of a burst, t a compile-time constant (pt[t] in registers; a
+     * "#pragma unroll" loop over t was left rolled at AES-256 -- pt to scratch) */
+    auto step = [&](uint64_t j0, auto tc) {
+        constexpr int t = decltype(tc)::value;
+        const uint64_t j = j0 + t;
+        if (BURST == 1 || j < sb) {
+            transpose32(s);
+            add_pt(t);
+            if (CFB) store(j, t);
+            else if (j > 0) store(j - 1, t);
+            if (!CFB || j + 1 < sb) {
+                transpose32(s);
+                pin_n(s, 32);
+                sched_fence();
+                if (t == BURST - 1 && j + 1 < sb) load(j + 1);
+                sched_fence();
+                otc_bs8::rounds<NR>(s, kt);
+                pin_n(s, 32);
+                sched_fence();
+            }
         }
-        if (CFB && j + 1 == sb) break;
-        transpose32(s);
-        pin_n(s, 32);
-        sched_fence();
-        if (j + 1 < sb) load(j + 1); /* lands while the rounds run */
-        sched_fence();
-        otc_bs8::rounds<NR>(s, kt);
-        pin_n(s, 32);
-        sched_fence();
-    }
+    };
+    for (uint64_t j0 = 0; j0 < sb; j0 += BURST)
+        for_each_c(std::make_integer_sequence<int, BURST>{}, [&](auto tc) { step(j0, tc); });
     if (!CFB) {
         transpose32(s);
-        store(sb - 1);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (FULL || (uint32_t)k < n)
+                *(uint4 *)(ob + (sb - 1) * 16 + k * cb + lo) =
+                    make_uint4(s[k] ^ kl0, s[8 + k] ^ kl1, s[16 + k] ^ kl2, s[24 + k] ^ kl3);
     }
 }
 
-/* one workgroup per CU beside the T-table claim kernel (one wave per SIMD),
- * up to four alone: <= 128 VGPRs */
+/* one workgroup per CU beside the T-table claim kernel: one wave per SIMD
+ * beside its four (<= 72 VGPRs each at 4-block bursts), so up to 224 VGPRs
+ * (tests/test_isa_cpu.py::test_bs8_segment_pair_shares_a_simd) */
 template <int NR, bool CFB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_aes_bs8_seg_claim(Bs8Params P)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_aes_bs8_seg_claim(Bs8Params P)
 {
     for (;;) {
         uint32_t n = 0;

@@ -272,6 +272,24 @@ int pick_ecb_impl(int impl, int bits, size_t nbytes)
 
 int pick_dec_impl(int impl, int bits, size_t nbytes) { return pick_ecb_impl(impl, bits, nbytes); }
 
+/* Split accounting (otc_split_stats): off by default -- one relaxed load
+ * per split call.  On, each split call copies its claim word back and waits
+ * for it (a profiling mode), so the caller can read how many units each side
+ * took. */
+std::atomic<int> g_split_stats{0};
+__global__ void k_claim_snapshot(unsigned long long *ctr, unsigned long long *host)
+{
+    const unsigned long long v = __hip_atomic_fetch_add(ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+thread_local uint64_t g_split_word = 0, g_split_nunits = 0, g_split_ttwaves = 0;
+
+#ifndef OTC_SPLIT_TT_WGS
+#define OTC_SPLIT_TT_WGS 0u /* T-table claim workgroups in a split (0: one per CU; A/B knob) */
+#endif
+#ifndef OTC_SPLIT_BS_FIRST
+#define OTC_SPLIT_BS_FIRST 0 /* launch the bitsliced half first (A/B knob) */
+#endif
 /* The split: tt(cl) launches the T-table claim kernel on st, bs(cl, aux) the
  * bitsliced claim kernel on the auxiliary stream, both over the whole buffer
  * (nunits claim units, the T-table kernel also runs what lies past the last
@@ -288,7 +306,7 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
     if (nunits < (bs_only ? 1 : min_units) || nunits > 0x7FFFFFFFull) return plain();
     unsigned long long *ctr = nullptr;
     /* word 0: the shared claim word; word 1 (bs_only): the T-table kernel's
-     * own word, preset to "every unit taken from the back" */
+     * own word, preset to "every unit taken" */
     hipError_t e = otc_dev::alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&ctr, 2 * sizeof *ctr, st);
     if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -303,23 +321,50 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
         return plain();
     }
     const SplitClaim cl{ctr, (uint32_t)nunits, bs_wgs};
-    const SplitClaim cl_tt{bs_only ? ctr + 1 : ctr, (uint32_t)nunits, bs_only ? 1u : 0u};
-    /* zeroed, then fork: the aux stream starts after everything queued on st */
-    if ((e = hipMemsetAsync(ctr, 0, 2 * sizeof *ctr, st)) == hipSuccess &&
-        (!bs_only || (e = hipMemsetD32Async((hipDeviceptr_t)((uint32_t *)(ctr + 1) + 1), (int)nunits, 1, st)) == hipSuccess) &&
+    const SplitClaim cl_tt{bs_only ? ctr + 1 : ctr, (uint32_t)nunits, bs_only ? 1u : OTC_SPLIT_TT_WGS};
+    /* zeroed (bs_only: the T-table's word all ones -- front + back far past
+     * nunits, so its claims fail; hipMemsetD32Async at a 4-byte offset cost
+     * ~40 ms per call), then fork: the aux stream starts after everything
+     * queued on st */
+    if ((e = hipMemsetAsync(ctr, 0, sizeof *ctr, st)) == hipSuccess &&
+        (e = hipMemsetAsync(ctr + 1, bs_only ? 0xFF : 0, sizeof *ctr, st)) == hipSuccess &&
         (e = hipEventRecord(a.fork, st)) == hipSuccess && (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess &&
-        (e = tt(cl_tt)) == hipSuccess) {
+        (OTC_SPLIT_BS_FIRST || (e = tt(cl_tt)) == hipSuccess)) {
         /* the bitsliced half failing (no memory for its key table) leaves the
          * T-table claim kernel to take every unit -- unless it was told to
          * take none (bs_only): then the T-table alone redoes the call.  The
          * join is recorded either way (a failure after its launch must still
          * be waited for). */
         const hipError_t eb = bs(cl, a.s);
+        if (OTC_SPLIT_BS_FIRST) e = tt(cl_tt);
         if (eb != hipSuccess) (void)hipGetLastError();
         if ((e = hipEventRecord(a.join, a.s)) == hipSuccess) e = hipStreamWaitEvent(st, a.join, 0);
         if (e == hipSuccess) {
             if (eb == hipSuccess) *ran = bs_only ? OTC_IMPL_BITSLICE : OTC_IMPL_SPLIT;
             else if (bs_only) e = plain();
+            if (e == hipSuccess && g_split_stats.load(std::memory_order_relaxed)) {
+                /* the counter's last value sits where the agent-scope atomics
+                 * left it: read it with one (an ordinary copy can see a stale
+                 * line) into pinned host memory */
+                thread_local unsigned long long *snap = nullptr;
+                if (!snap && hipHostMalloc((void **)&snap, sizeof *snap, hipHostMallocDefault) != hipSuccess) {
+                    (void)hipGetLastError();
+                    snap = nullptr;
+                }
+                if (snap) {
+                    hipLaunchKernelGGL(k_claim_snapshot, dim3(1), dim3(1), 0, st, ctr, snap);
+                    if ((e = hipGetLastError()) == hipSuccess) e = hipStreamSynchronize(st);
+                }
+                if (snap && e == hipSuccess) {
+                    const uint64_t w = *(volatile unsigned long long *)snap;
+                    g_split_word = bs_only ? (uint64_t)nunits : w; /* bs_only: the T-table has its own word */
+                    g_split_nunits = nunits;
+                    /* every T-table claim kernel runs 1024-thread workgroups,
+                     * one per CU; each of their waves ends on one failed
+                     * claim */
+                    g_split_ttwaves = bs_only ? 0 : 16ull * (uint64_t)otc_dev::device_cus();
+                }
+            }
         } else {
             (void)hipStreamSynchronize(a.s); /* no join on st: the counter must outlive the bitsliced kernel */
         }
@@ -417,6 +462,9 @@ hipError_t seg_dec_split(bool cfb, const void *in, void *out, size_t seg_blocks,
  * eight per wave from the front.  bs8 needs segments of < 8 MiB (32-bit lane
  * offsets); at least 16 units (1024 segments) to split. */
 constexpr uint64_t SEG_UNIT = 64;
+#ifndef OTC_BS8_SPLIT_WGS
+#define OTC_BS8_SPLIT_WGS 1u /* bs8 workgroups per CU beside the T-table (A/B knob) */
+#endif
 bool segenc_bs8_ok(size_t seg_bytes) { return seg_bytes >= 16 && seg_bytes * SEG_UNIT * 8 <= 0xFFFFFFFFull; }
 
 /* auto: the split from segenc_split_min() bytes (docs/PERF.md round 5) */
@@ -435,7 +483,7 @@ hipError_t seg_enc_split(bool cfb, const void *in, void *out, size_t seg_blocks,
                          Ctr128 iv0, bool bs_only, hipStream_t st, int *ran)
 {
     return split_claim(
-        nseg / SEG_UNIT, 16, bs_only, (unsigned)otc_dev::device_cus() * (bs_only ? 4u : 1u), st, ran,
+        nseg / SEG_UNIT, 16, bs_only, (unsigned)otc_dev::device_cus() * (bs_only ? 4u : OTC_BS8_SPLIT_WGS), st, ran,
         [&](SplitClaim cl) { return otc_impl::tt_seg_encrypt_claim(cfb, in, out, seg_blocks, nseg, K, iv0, cl, st); },
         [&](SplitClaim cl, hipStream_t s) {
             return otc_impl::bs8_seg_encrypt_claim(cfb, in, out, seg_blocks, K, iv0, cl, s);
@@ -525,6 +573,24 @@ void otc_rt::aux_release_all()
 }
 
 extern "C" int otc_last_impl(void) { return g_last_impl; }
+
+extern "C" void otc_split_stats(int on) { g_split_stats.store(on ? 1 : 0, std::memory_order_relaxed); }
+
+extern "C" int otc_split_last_units(uint64_t *front, uint64_t *back, uint64_t *nunits)
+{
+    if (!front || !back || !nunits) return set_err(OTC_ERR_ARG, "null argument");
+    /* every T-table wave ends on one failed back claim (+1 each), so the
+     * back count less those is what the T-table took; the front took the rest */
+    const uint64_t b = g_split_word >> 32, n = g_split_nunits;
+    *back = b > g_split_ttwaves ? std::min(n, b - g_split_ttwaves) : 0;
+    *front = n - *back;
+    *nunits = n;
+    if (getenv("OTC_DEBUG_SPLIT_RAW"))
+        fprintf(stderr, "split raw word: front %llu back %llu, T-table waves %llu, units %llu\n",
+                (unsigned long long)(g_split_word & 0xFFFFFFFFull), (unsigned long long)(g_split_word >> 32),
+                (unsigned long long)g_split_ttwaves, (unsigned long long)n);
+    return OTC_OK;
+}
 
 /* ---- device ops --------------------------------------------------------- */
 extern "C" int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_aes_key *k, int impl,

@@ -490,20 +490,23 @@ static int rccl_job_run(RcclJob &J, int mode, const uint8_t *hin, uint8_t *hout,
 {
     const int ngpus = J.n;
     const size_t S = J.S, round = S * (size_t)ngpus;
-    const size_t nrounds = (nbytes + round - 1) / round;
+    /* the round plan: csrc/cpu/rccl_plan.c (pure, tested on the CPU at N = 2..8) */
+    const uint64_t nrounds = otc_rccl_nrounds(nbytes, ngpus, S);
     std::vector<uint8_t> halos;
     if (mode == OTC_MODE_CBC_DEC) {
         std::vector<size_t> starts(nrounds * (size_t)ngpus);
-        for (size_t i = 0; i < starts.size(); ++i) starts[i] = std::min(i * S, nbytes);
+        for (size_t i = 0; i < starts.size(); ++i) starts[i] = otc_rccl_halo_start(nbytes, S, i);
         halos = capture_halos(hin, starts);
     }
     for (size_t r = 0; r < nrounds; ++r) {
         const int b = (int)(r & 1);
-        const size_t off = r * round, n = std::min(round, nbytes - off);
+        otc_rccl_piece pc;
+        if (int e = otc_rccl_plan_piece(nbytes, ngpus, S, r, 0, &pc)) return e;
+        const size_t off = pc.round_off, n = pc.round_bytes;
         HIPCHK(hipSetDevice(0));
         /* on sc[0]: after round r-2's scatter (which read root_in[b]), before
          * this round's */
-        if (n < round) HIPCHK(hipMemsetAsync(J.root_in[b], 0, round, J.sc[0]));
+        if (pc.pad_bytes) HIPCHK(hipMemsetAsync(J.root_in[b], 0, round, J.sc[0]));
         HIPCHK(hipMemcpyAsync(J.root_in[b], hin + off, n, hipMemcpyHostToDevice, J.sc[0]));
         /* piece_in[b][g] is free once round r-2's cipher has read it */
         if (r >= 2)
@@ -521,11 +524,11 @@ static int rccl_job_run(RcclJob &J, int mode, const uint8_t *hin, uint8_t *hout,
             HIPCHK(hipStreamWaitEvent(J.kst[g], J.ev_sc[b][g], 0));
             /* piece_out[b][g] is free once round r-2's gather has read it */
             if (r >= 2) HIPCHK(hipStreamWaitEvent(J.kst[g], J.ev_ga[b][g], 0));
-            const size_t goff = off + (size_t)g * S;
-            if (goff < nbytes) {
-                const size_t gn = std::min(S, nbytes - goff);
-                const uint8_t *hp = (mode == OTC_MODE_CBC_DEC && goff > 0) ? &halos[16 * (r * ngpus + g)] : nullptr;
-                if (int rr = run_chunk(mode, J.pin[b][g], J.pout[b][g], gn, k, ivc, goff / 16, hp, impl, J.kst[g])) {
+            if (int e = otc_rccl_plan_piece(nbytes, ngpus, S, r, g, &pc)) return e;
+            if (pc.bytes) {
+                const uint8_t *hp = (mode == OTC_MODE_CBC_DEC && pc.halo >= 0) ? &halos[16 * (size_t)pc.halo] : nullptr;
+                if (int rr = run_chunk(mode, J.pin[b][g], J.pout[b][g], pc.bytes, k, ivc, pc.blk0, hp, impl,
+                                       J.kst[g])) {
                     J.failed = true;
                     return rr;
                 }

@@ -83,6 +83,14 @@ int otc_pick_impl(int impl, int bits, int mode, uint64_t nbytes);
  * back to the T-table (too few units, no memory for the claim counter) reports
  * OTC_IMPL_TTABLE. */
 int otc_last_impl(void);
+/* Split accounting, a profiling mode (off by default): with
+ * otc_split_stats(1) every split call on this thread waits for its kernels
+ * and records its claim counter; otc_split_last_units then gives the units
+ * the bitsliced side (front) and the T-table side (back) took in the last
+ * such call, of nunits (2048-block units, or 64-segment units for segment
+ * encryption).  Under impl "bitslice" front == nunits. */
+void otc_split_stats(int on);
+int otc_split_last_units(uint64_t *front, uint64_t *back, uint64_t *nunits);
 
 /* ---- device ops (device pointers; async on `stream`) ---------------------
  * All functions accept any byte length; the trailing partial block of CTR is
@@ -349,6 +357,28 @@ typedef struct {
 int otc_multi_run(int ngpus, int strategy, int mode, const void *host_in, void *host_out,
                   size_t nbytes, const otc_aes_key *k, const uint8_t iv_or_ctr[16], int impl,
                   size_t chunk_bytes, otc_multi_stats *stats);
+
+/* The round plan of strategy 1, a pure function (csrc/cpu/rccl_plan.c, also
+ * in the CPU-only library, so the N > 1 plan is tested without GPUs): the
+ * stream goes in rounds of ngpus pieces of `piece` bytes each (the equal
+ * counts ncclScatter / ncclGather need); the last round is zero-padded.
+ * Piece (r, g) covers stream bytes [off, off + bytes) -- bytes 0 for a piece
+ * wholly past the end --, starts at CTR block blk0 = off / 16, and for CBC
+ * decryption takes its predecessor block from halo slot `halo` (the 16
+ * stream bytes before halo_start(halo)), or the IV when halo < 0. */
+typedef struct {
+    uint64_t round_off;   /* stream offset of round r */
+    uint64_t round_bytes; /* stream bytes in round r (< ngpus * piece: the last round) */
+    uint64_t pad_bytes;   /* zero padding of round r's root buffer */
+    uint64_t off, bytes;  /* piece (r, g) */
+    uint64_t blk0;        /* its first block (CTR counter offset) */
+    int64_t halo;         /* CBC decryption: halo slot, -1 = the IV */
+} otc_rccl_piece;
+uint64_t otc_rccl_nrounds(uint64_t nbytes, int ngpus, uint64_t piece);
+/* 0, or OTC_ERR_ARG for ngpus < 1, piece == 0 or a (r, g) out of the plan */
+int otc_rccl_plan_piece(uint64_t nbytes, int ngpus, uint64_t piece, uint64_t r, int g, otc_rccl_piece *out);
+/* stream offset whose preceding 16 bytes fill halo slot i (clamped to nbytes) */
+uint64_t otc_rccl_halo_start(uint64_t nbytes, uint64_t piece, uint64_t i);
 
 /* Free the RCCL communicators / buffers that strategy 1 caches between calls
  * and the per-shard engines of strategy 0 (rebuilt on demand). */

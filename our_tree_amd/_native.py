@@ -92,6 +92,19 @@ class StreamStats(ctypes.Structure):
     ]
 
 
+class RcclPiece(ctypes.Structure):
+    """otc_rccl_piece (otc.h): one GPU's piece of one round of the RCCL job"""
+    _fields_ = [
+        ("round_off", ctypes.c_uint64),
+        ("round_bytes", ctypes.c_uint64),
+        ("pad_bytes", ctypes.c_uint64),
+        ("off", ctypes.c_uint64),
+        ("bytes", ctypes.c_uint64),
+        ("blk0", ctypes.c_uint64),
+        ("halo", ctypes.c_int64),
+    ]
+
+
 class MultiStats(ctypes.Structure):
     _fields_ = [
         ("total_ms", ctypes.c_double),
@@ -134,6 +147,9 @@ def _declare_cpu(lib):
         "AES_CTR_encrypt_at": (None, [c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int, ctypes.c_ulonglong]),
         "otc_bitslice_selftest": (c_int, [c_int]),
         "otc_bs8_selftest": (c_int, [c_int]),
+        "otc_rccl_nrounds": (c_u64, [c_u64, c_int, c_u64]),
+        "otc_rccl_plan_piece": (c_int, [c_u64, c_int, c_u64, c_u64, c_int, P(RcclPiece)]),
+        "otc_rccl_halo_start": (c_u64, [c_u64, c_u64, c_u64]),
         "AES_CBC_encrypt": (None, [c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int]),
         "AES_CFB128_encrypt": (None, [c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int]),
         "aes_monte_carlo": (c_int, [c_int, c_int, c_u8p]),

@@ -218,8 +218,15 @@ def cbc_scatter_job(rounds: int, chunk: int, key: bytes, iv0: bytes, sector: int
     total = rounds * chunk * world
     # bytes that demonstrably crossed between GPUs: every verified non-root
     # piece out (scatter) and back (gather), in the two checked rounds
-    xgmi_verified = sum(2 * piece_bytes * (2 if rounds > 0 else 1)
-                        for g, ok in enumerate(per_rank) if ok and g != pipe.root)
+    peer_verified = sum(2 * piece_bytes * (2 if rounds > 0 else 1)
+                        for g, ok in enumerate(per_rank) if ok and g != pipe.root) if pipe.comm else 0
+    # what the timed collectives were asked to move between ranks (their last
+    # round is among the verified ones above)
+    peer_timed = 2 * rounds * (world - 1) * piece_bytes if pipe.comm else 0
+    backend = dist.get_backend() if pdist._pg_on() else "none"
+    # only RCCL ("nccl") moves GPU-to-GPU bytes over xGMI; gloo (the CPU
+    # rehearsals) moves them through host memory / TCP
+    xgmi = backend == "nccl"
     return {
         "seconds": el,
         "total_bytes": total,
@@ -228,11 +235,14 @@ def cbc_scatter_job(rounds: int, chunk: int, key: bytes, iv0: bytes, sector: int
         "ranks": world,
         "ranks_verified": nver,
         "per_rank_ok": per_rank,
-        "backend": dist.get_backend() if pdist._pg_on() else "none",
+        "backend": backend,
         "collectives": bool(pipe.comm),
         "overlap": pipe.overlap,
-        "xgmi_bytes_verified": xgmi_verified if pipe.comm else 0,
-        # what the timed collectives were asked to move between GPUs (their
-        # last round is among the verified ones above)
-        "xgmi_bytes_timed": 2 * rounds * (world - 1) * piece_bytes if pipe.comm else 0,
+        "transport": "xgmi" if xgmi else ("host" if pipe.comm else "none"),
+        "peer_bytes_verified": peer_verified,
+        "peer_bytes_timed": peer_timed,
+        "xgmi_bytes_verified": peer_verified if xgmi else 0,
+        "xgmi_bytes_timed": peer_timed if xgmi else 0,
+        "host_bytes_verified": 0 if xgmi else peer_verified,
+        "host_bytes_timed": 0 if xgmi else peer_timed,
     }

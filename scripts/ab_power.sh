@@ -20,6 +20,6 @@ d = json.loads(open(sys.argv[1]).read().splitlines()[-1])
 p = d["power"]
 print(f'{d["label"]:8s} {d["mode"]:8s} {d["bits"]} {d["bytes"] >> 30:3d}G {d["gbps"]:8.1f} GB/s v={d["verified"]} '
       f'{p.get("avg_socket_w")} W {d.get("joules_per_gb")} J/GB PPT {p.get("ppt_residency")} '
-      f'gfx {p.get("gfxclk_mhz_mean")} MHz', flush=True)
+      f'gfx {p.get("gfxclk_mhz_mean")} MHz' + (f' units {d["split_units"]}' if "split_units" in d else ''), flush=True)
 PY
 done; done; done

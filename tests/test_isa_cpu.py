@@ -124,9 +124,9 @@ def _vgprs(obj):
 
 def test_bs8_segment_pair_shares_a_simd():
     """The chained segment-encryption split: the row-sliced bs8 kernel
-    (csrc/hip/aes_bs8.hip, <= 128 VGPRs, no scratch) fits one wave per SIMD
-    beside the 4 waves of the T-table segment claim kernel, for CBC and CFB at
-    every key size."""
+    (csrc/hip/aes_bs8.hip, no scratch) fits one wave per SIMD beside the 4
+    waves of the T-table segment claim kernel (single-buffered 8-block
+    bursts, <= 72 allocated), for CBC and CFB at every key size."""
     tt_obj = os.path.join(ROOT, "build", "obj", "hip", "aes_tt.o")
     bs8_obj = os.path.join(ROOT, "build", "obj", "hip", "aes_bs8.o")
     if not os.path.exists(tt_obj) or not os.path.exists(bs8_obj) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):
@@ -140,7 +140,7 @@ def test_bs8_segment_pair_shares_a_simd():
             bn = [k for k in b8 if "k_aes_bs8_seg_claim" in k and f"ILi{nr}ELb{cfb}E" in k]
             assert tn and bn, (nr, cfb, sorted(b8))
             t, b = max(tt[k][0] for k in tn), max(b8[k][0] for k in bn)
-            assert b <= 128 and all(b8[k][1] == 0 for k in bn), (nr, cfb, b)
+            assert all(b8[k][1] == 0 for k in bn), (nr, cfb, b)
             assert 4 * alloc(t) + alloc(b) <= 512, (nr, cfb, t, b)
             seen += 1
     assert seen == 6

@@ -60,9 +60,12 @@ def test_every_rank_verified(world, decrypt):
         assert v["verified"], v
         assert v["ranks_verified"] == world and v["per_rank_ok"] == [True] * world
         assert v["collectives"] and v["backend"] == "gloo"
-        # observed: every non-root piece out and back, in the warmup and last round
-        assert v["xgmi_bytes_verified"] == 2 * 2 * (world - 1) * piece
-        assert v["xgmi_bytes_timed"] == 2 * 3 * (world - 1) * piece
+        # observed: every non-root piece out and back, in the warmup and last
+        # round -- over gloo, i.e. host memory, never labelled xGMI
+        assert v["transport"] == "host"
+        assert v["peer_bytes_verified"] == v["host_bytes_verified"] == 2 * 2 * (world - 1) * piece
+        assert v["peer_bytes_timed"] == v["host_bytes_timed"] == 2 * 3 * (world - 1) * piece
+        assert v["xgmi_bytes_verified"] == 0 and v["xgmi_bytes_timed"] == 0
 
 
 @pytest.mark.parametrize("world,where", [(4, "recv"), (8, "recv"), (4, "out")])
@@ -72,7 +75,7 @@ def test_corrupted_piece_on_rank3_fails(world, where):
         assert not v["verified"], v
         assert v["per_rank_ok"][3] is False
         assert v["ranks_verified"] == world - 1
-        assert v["xgmi_bytes_verified"] == 2 * 2 * (world - 2) * 4096
+        assert v["peer_bytes_verified"] == 2 * 2 * (world - 2) * 4096 and v["xgmi_bytes_verified"] == 0
 
 
 def test_host_checksum_matches_definition():
