@@ -8,6 +8,7 @@
  *           [--bits 128] [--bytes 1G] [--iters 20] [--warmup 3]
  *           [--impl auto|ttable|bitslice|split] [--inplace] [--verify] [--clock]
  *           [--mark]                        "OTB_MARK start|end" on stderr around the timed loop
+ *           [--strace]                      diagnostic builds (OTC_SPLIT_TRACE): wave start times of a split
  *           [--split-stats]                 one extra call after the loop: units each side of a
  *                                           split took ("split_units": [bitsliced, T-table, all])
  *           [--corrupt-at OFF]              test hook: flip output byte OFF after the
@@ -34,6 +35,7 @@
  * has an oracle; "verified" is true only when every sample matched, false when
  * one did not (exit 3), and null when --verify was not given.
  */
+#include <algorithm>
 #include <chrono>
 #include <cinttypes>
 #include <cstdio>
@@ -67,7 +69,7 @@ struct Cfg {
     size_t bytes = 1ull << 30;
     int iters = 20, warmup = 3;
     int impl = OTC_IMPL_AUTO;
-    bool inplace = false, verify = false, e2e = false, clock = false, mark = false, split_stats = false;
+    bool inplace = false, verify = false, e2e = false, clock = false, mark = false, split_stats = false, strace = false;
     long long corrupt_at = -1;
     size_t chunk = 256ull << 20;
     int gpus = 1, strategy = 0;
@@ -376,6 +378,7 @@ int main(int argc, char **argv)
         else if (a == "--clock") c.clock = true;
         else if (a == "--mark") c.mark = true;
         else if (a == "--split-stats") c.split_stats = true;
+        else if (a == "--strace") c.strace = true;
         else if (a == "--corrupt-at") c.corrupt_at = atoll(nx());
         else if (a == "--e2e") c.e2e = true;
         else if (a == "--chunk") c.chunk = parse_size(nx());
@@ -556,6 +559,29 @@ int main(int argc, char **argv)
     }
     if (c.mark) mark("end");
     char split_units[96] = "";
+    if (c.strace) { /* diagnostic builds: when each kernel's waves started, one more call */
+        std::vector<unsigned long long> rec(2 * 16384);
+        for (int w = 0; w < 3; ++w) (void)otc_split_trace(w, rec.data(), 16384); /* reset */
+        if (run_op(&a) || otc_device_sync()) return 1;
+        unsigned long long t0 = ~0ull;
+        std::vector<std::vector<unsigned long long>> st(3);
+        for (int w = 0; w < 3; ++w) {
+            const int n = otc_split_trace(w, rec.data(), 16384);
+            for (int i = 0; i < n; ++i) {
+                st[w].push_back(rec[2 * i]);
+                if (w == 0) t0 = std::min(t0, rec[2 * i]);
+            }
+        }
+        for (int w = 0; w < 3; ++w) {
+            auto &v = st[w];
+            if (v.empty()) continue;
+            std::sort(v.begin(), v.end());
+            auto us = [&](unsigned long long t) { return t0 == ~0ull ? 0.0 : ((double)t - (double)t0) / 100.0; };
+            fprintf(stderr, "strace %s: %zu waves, start (us after the first T-table wave) min %.1f median %.1f p90 %.1f max %.1f\n",
+                    w == 0 ? "ttable" : w == 1 ? "bitslice" : "bs8", v.size(), us(v.front()), us(v[v.size() / 2]),
+                    us(v[v.size() * 9 / 10]), us(v.back()));
+        }
+    }
     const double gbps = c.bytes / (ms * 1e6);
     if (c.split_stats) { /* one more call, after the timed loop: which side took how many units */
         uint64_t f = 0, b = 0, n = 0;

@@ -64,6 +64,7 @@ int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir)
 /* the host double runs the oracle: it reports the T-table family */
 int otc_last_impl(void) { return OTC_IMPL_TTABLE; }
 void otc_split_stats(int) {}
+int otc_split_trace(int, unsigned long long *, int) { return -1; }
 int otc_split_last_units(uint64_t *f, uint64_t *b, uint64_t *n)
 {
     *f = *b = *n = 0;

@@ -549,6 +549,7 @@ template <int NR, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_aes_bs_claim(BsParams P,
                                                                                                otc_aes_key K)
 {
+    strace(3);
     for (;;) {
         const int64_t u = claim_unit(P.cl, false);
         if (u < 0) break;
@@ -666,6 +667,8 @@ hipError_t launch(const BsParams &P, const otc_aes_key &K, hipStream_t st)
 } // namespace
 
 namespace otc_impl {
+
+OTC_STRACE_READER(strace_read_bs)
 
 hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
 

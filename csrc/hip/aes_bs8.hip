@@ -219,10 +219,13 @@ __device__ __forceinline__ void bs8_task(const Bs8Params &P, uint64_t u0, uint32
 
 /* one workgroup per CU beside the T-table claim kernel: one wave per SIMD
  * beside its four (<= 72 VGPRs each at 4-block bursts), so up to 224 VGPRs
- * (tests/test_isa_cpu.py::test_bs8_segment_pair_shares_a_simd) */
+ * (tests/test_isa_cpu.py::test_bs8_segment_pair_shares_a_simd).  Only a
+ * minimum occupancy: a maximum (waves_per_eu(2, 2)) makes hipcc pad the
+ * descriptor to 169 VGPRs (176 allocated) to enforce it. */
 template <int NR, bool CFB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_aes_bs8_seg_claim(Bs8Params P)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_aes_bs8_seg_claim(Bs8Params P)
 {
+    strace(3);
     for (;;) {
         uint32_t n = 0;
         const int64_t u = claim_front(P.cl, TASK_UNITS, &n);
@@ -237,6 +240,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 } // namespace
 
 namespace otc_impl {
+
+OTC_STRACE_READER(strace_read_bs8)
 
 /* The bitsliced half of the segment-encryption split: units of 64 segments
  * from the front of `cl`, cl.wgs workgroups (default one per CU).  seg_blocks

@@ -32,6 +32,7 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 
@@ -289,13 +290,35 @@ struct DecParams {
  * Encryption-direction kernel: ECB-enc, CFB128-dec (CTR has its own
  * counter-caching kernel below)
  * ------------------------------------------------------------------------- */
+/* The T tables in LDS.  The claim kernels (CLAIM / DYN) take them as dynamic
+ * LDS, sized at launch (launch_dyn below): with a static 128 / 160 KiB array
+ * hipcc knows the workgroup fills the CU and pads the kernel descriptor's
+ * register count up to the occupancy the LDS allows (4 waves per SIMD: 97
+ * VGPRs -> 104 allocated, whatever the kernel uses), and then no bitsliced
+ * wave (160-176 registers) fits beside the 4 T-table waves, so the "split"
+ * ran its halves one after the other (split wave-start trace,
+ * profiles/r5/coresidency/).  Dynamic LDS leaves the descriptor at the
+ * registers actually used (tests/test_isa_cpu.py checks the granule). */
+
+template <bool DYN, uint32_t WORDS>
+__device__ __forceinline__ uint32_t *tt_lds()
+{
+    if constexpr (DYN) {
+        extern __shared__ __attribute__((aligned(16))) uint32_t tt_dyn_lds[];
+        return tt_dyn_lds;
+    } else {
+        __shared__ __attribute__((aligned(16))) uint32_t tt_static_lds[WORDS];
+        return tt_static_lds;
+    }
+}
+
 /* CLAIM: the T-table half of a co-resident split (otc_device.h SplitClaim):
  * workgroup 0 first runs the blocks past the last full 2048-block unit, then
  * every wave takes units from the back of the buffer until none are left. */
 template <int NR, int MODE, int B, int THREADS, bool CLAIM>
 __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_key &K)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
+    uint32_t *tbl = tt_lds<CLAIM, 2 * 256 * 64>();
     fill_tbl4<THREADS>(tbl, g_tab.te0);
     __syncthreads();
 
@@ -351,6 +374,7 @@ __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_ke
     };
 
     if constexpr (CLAIM) {
+        strace(1);
         const uint64_t done = (uint64_t)P.cl.nunits * CLAIM_UNIT; /* the rest: workgroup 0, first */
         if (blockIdx.x == 0)
             for (uint64_t base = done; base < P.nfull; base += PER) chunk(base + (uint64_t)wave * 64u * B + lane, false);
@@ -506,7 +530,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_
 template <int NR, int MODE, int B, int THREADS, bool CLAIM>
 __device__ __forceinline__ void dec_tt_body(const DecParams &P, const otc_aes_key &K)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64 + 256 * 32]; /* 160 KiB */
+    uint32_t *tbl = tt_lds<CLAIM, 2 * 256 * 64 + 256 * 32>(); /* 160 KiB */
     fill_dtbl4<THREADS>(tbl, g_tab.td0, g_tab.is4);
     __syncthreads();
 
@@ -562,6 +586,7 @@ __device__ __forceinline__ void dec_tt_body(const DecParams &P, const otc_aes_ke
     };
 
     if constexpr (CLAIM) { /* as k_aes_enc_tt */
+        strace(1);
         const uint64_t done = (uint64_t)P.cl.nunits * CLAIM_UNIT;
         if (blockIdx.x == 0)
             for (uint64_t base = done; base < P.nfull; base += PER) chunk(base + (uint64_t)wave * 64u * B + lane, false);
@@ -757,18 +782,19 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg_g(CbcSegParams P, o
 }
 
 /* The T-table half of the chained segment encryption split (engine.cpp
- * seg_enc_split): a claim unit is 64 segments, one per lane of a wave, taken
+ * seg_enc_run): a claim unit is 64 segments, one per lane of a wave, taken
  * from the back; workgroup 0 first runs the segments past the last full unit.
  * The bitsliced half (aes_bs8.hip) takes 8 units at a time from the front. */
 constexpr uint32_t SEG_UNIT = 64;
 template <int NR, int G, bool CFB>
 __global__ __launch_bounds__(1024) void k_aes_seg_enc_tt_claim(CbcSegParams P, otc_aes_key K)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
+    uint32_t *tbl = tt_lds<true, 2 * 256 * 64>();
     fill_tbl4<1024>(tbl, g_tab.te0);
     __syncthreads();
     uint32_t lk[4];
     tbl4_lane_consts(threadIdx.x & 63u, lk);
+    strace(1);
     const uint64_t done = (uint64_t)P.cl.nunits * SEG_UNIT;
     if (blockIdx.x == 0 && done + (threadIdx.x & ~63u) < P.nseg) { /* the remainder (< 64 segments): wave 0 */
         const uint64_t seg = done + threadIdx.x;
@@ -1049,6 +1075,26 @@ static_assert(64 * 4 == OTC_BATCH_TILE_BLOCKS, "largest tile must match otc.h");
  * ------------------------------------------------------------------------- */
 inline int num_cus() { return otc_dev::device_cus(); }
 
+/* launch a claim kernel with `lds` bytes of dynamic LDS for its tables
+ * (tt_lds); the opt-in above 64 KiB is made once per kernel and device */
+template <auto KERN, typename... A>
+hipError_t launch_dyn(dim3 g, dim3 b, uint32_t lds, hipStream_t st, A... args)
+{
+    static std::atomic<uint64_t> opted{0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = 1ull << (dev & 63);
+    if (!(opted.load(std::memory_order_acquire) & bit)) {
+        e = hipFuncSetAttribute((const void *)KERN, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        opted.fetch_or(bit, std::memory_order_acq_rel);
+    }
+    hipLaunchKernelGGL(KERN, g, b, lds, st, args...);
+    return hipGetLastError();
+}
+constexpr uint32_t ENC_LDS = 2 * 256 * 64 * 4, DEC_LDS = (2 * 256 * 64 + 256 * 32) * 4;
+
 int grid_for(uint64_t work_items, uint64_t per_wg, int wg_per_cu)
 {
     uint64_t need = (work_items + per_wg - 1) / per_wg;
@@ -1151,25 +1197,18 @@ template <int MODE>
 hipError_t launch_enc_claim(const EncParams &P, const otc_aes_key &K, hipStream_t st)
 {
     const dim3 g(P.cl.wgs ? P.cl.wgs : (unsigned)num_cus()), b(ENC_THREADS);
+    auto go = [&](auto nr) {
+        constexpr int NR = decltype(nr)::value;
+        if constexpr (MODE == E_ECB) return launch_dyn<k_aes_ecb_tt_claim<NR>>(g, b, ENC_LDS, st, P, K);
+        else if constexpr (MODE == E_CFB_DEC) return launch_dyn<k_aes_cfb_tt_claim<NR>>(g, b, ENC_LDS, st, P, K);
+        else return launch_dyn<k_aes_cfbseg_tt_claim<NR>>(g, b, ENC_LDS, st, P, K);
+    };
     switch (K.nr) {
-    case 10:
-        if constexpr (MODE == E_ECB) hipLaunchKernelGGL((k_aes_ecb_tt_claim<10>), g, b, 0, st, P, K);
-        else if constexpr (MODE == E_CFB_DEC) hipLaunchKernelGGL((k_aes_cfb_tt_claim<10>), g, b, 0, st, P, K);
-        else hipLaunchKernelGGL((k_aes_cfbseg_tt_claim<10>), g, b, 0, st, P, K);
-        break;
-    case 12:
-        if constexpr (MODE == E_ECB) hipLaunchKernelGGL((k_aes_ecb_tt_claim<12>), g, b, 0, st, P, K);
-        else if constexpr (MODE == E_CFB_DEC) hipLaunchKernelGGL((k_aes_cfb_tt_claim<12>), g, b, 0, st, P, K);
-        else hipLaunchKernelGGL((k_aes_cfbseg_tt_claim<12>), g, b, 0, st, P, K);
-        break;
-    case 14:
-        if constexpr (MODE == E_ECB) hipLaunchKernelGGL((k_aes_ecb_tt_claim<14>), g, b, 0, st, P, K);
-        else if constexpr (MODE == E_CFB_DEC) hipLaunchKernelGGL((k_aes_cfb_tt_claim<14>), g, b, 0, st, P, K);
-        else hipLaunchKernelGGL((k_aes_cfbseg_tt_claim<14>), g, b, 0, st, P, K);
-        break;
+    case 10: return go(std::integral_constant<int, 10>{});
+    case 12: return go(std::integral_constant<int, 12>{});
+    case 14: return go(std::integral_constant<int, 14>{});
     default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 template <int MODE>
@@ -1177,12 +1216,11 @@ hipError_t launch_dec_claim(const DecParams &P, const otc_aes_key &K, hipStream_
 {
     const dim3 g(P.cl.wgs ? P.cl.wgs : (unsigned)num_cus()), b(DEC_THREADS);
     switch (K.nr) {
-    case 10: hipLaunchKernelGGL((k_aes_dec_tt_claim<10, MODE>), g, b, 0, st, P, K); break;
-    case 12: hipLaunchKernelGGL((k_aes_dec_tt_claim<12, MODE>), g, b, 0, st, P, K); break;
-    case 14: hipLaunchKernelGGL((k_aes_dec_tt_claim<14, MODE>), g, b, 0, st, P, K); break;
+    case 10: return launch_dyn<k_aes_dec_tt_claim<10, MODE>>(g, b, DEC_LDS, st, P, K);
+    case 12: return launch_dyn<k_aes_dec_tt_claim<12, MODE>>(g, b, DEC_LDS, st, P, K);
+    case 14: return launch_dyn<k_aes_dec_tt_claim<14, MODE>>(g, b, DEC_LDS, st, P, K);
     default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 template <int NR, bool CFB>
@@ -1226,6 +1264,8 @@ hipError_t launch_ctr_batch_nr(const BatchParams &P, int tile_blocks, hipStream_
 
 /* ---- internal entry points used by engine.cpp ---------------------------- */
 namespace otc_impl {
+
+OTC_STRACE_READER(strace_read_tt)
 
 hipError_t tt_ctr_batch(const otc_ctr_msg *msgs, const otc_aes_key *keys, const uint32_t *tile_msg,
                         const uint64_t *tile_first, uint64_t ntiles, int tile_blocks, int nr, hipStream_t st)
@@ -1496,17 +1536,17 @@ hipError_t tt_seg_encrypt_claim(bool cfb, const void *in, void *out, uint64_t se
     P.cl = cl;
     const dim3 g(cl.wgs ? cl.wgs : (unsigned)num_cus()), b(1024);
     constexpr int G = OTC_SEG_CLAIM_G;
-#define OTC_SEG_CLAIM_LAUNCH(NR)                                                                   \
-    if (cfb) hipLaunchKernelGGL((k_aes_seg_enc_tt_claim<NR, G, true>), g, b, 0, st, P, K);        \
-    else hipLaunchKernelGGL((k_aes_seg_enc_tt_claim<NR, G, false>), g, b, 0, st, P, K)
+    auto go = [&](auto nr) {
+        constexpr int NR = decltype(nr)::value;
+        return cfb ? launch_dyn<k_aes_seg_enc_tt_claim<NR, G, true>>(g, b, ENC_LDS, st, P, K)
+                   : launch_dyn<k_aes_seg_enc_tt_claim<NR, G, false>>(g, b, ENC_LDS, st, P, K);
+    };
     switch (K.nr) {
-    case 10: OTC_SEG_CLAIM_LAUNCH(10); break;
-    case 12: OTC_SEG_CLAIM_LAUNCH(12); break;
-    case 14: OTC_SEG_CLAIM_LAUNCH(14); break;
+    case 10: return go(std::integral_constant<int, 10>{});
+    case 12: return go(std::integral_constant<int, 12>{});
+    case 14: return go(std::integral_constant<int, 14>{});
     default: return hipErrorInvalidValue;
     }
-#undef OTC_SEG_CLAIM_LAUNCH
-    return hipGetLastError();
 }
 
 hipError_t tt_cfb_decrypt_seg(const void *in, void *out, uint64_t seg_blocks, uint64_t nseg,

@@ -59,6 +59,9 @@ hipError_t tt_seg_encrypt_claim(bool, const void *, void *, uint64_t, uint64_t, 
                                 hipStream_t);
 hipError_t bs8_seg_encrypt_claim(bool, const void *, void *, uint64_t, const otc_aes_key &, Ctr128, SplitClaim,
                                  hipStream_t);
+int strace_read_tt(unsigned long long *, int);
+int strace_read_bs(unsigned long long *, int);
+int strace_read_bs8(unsigned long long *, int);
 hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
 hipError_t tt_ctr_shift(const void *, void *, size_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t xor_small(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
@@ -155,7 +158,7 @@ namespace {
  * (the bitsliced grid needs ~768 workgroups to fill the chip, plus two table
  * kernels per call) take the T-table.  ECB, CBC / CFB decryption: the
  * co-resident split (split_claim below) from split_min() bytes, the T-table
- * below that.
+ * below that.  Segment encryption: T-table kernels only (seg_enc_run).
  * ctr_bytes = 0 for non-CTR calls.  OTC_IMPL=ttable|bitslice|split overrides
  * "auto" for the whole process. */
 int env_impl()
@@ -255,12 +258,15 @@ void aux_give(const AuxStream &a)
     g_aux_free.push_back(a);
 }
 
-/* the smallest call that splits: 896 MiB.  Below it the T-table alone wins:
- * a claim unit is ~130 us of one T-table wave's work, so a short call ends
- * with idle waves (profiles/r4/claim_split/small_sizes.jsonl,
- * mid_sizes.jsonl: 512 MiB loses 2-6%, 896 MiB ties ECB and wins decryption
- * 4-7%, 1000 MiB -- the reference's own size -- wins 3-11%) */
-size_t split_min(int) { return (size_t)896 << 20; }
+/* the smallest call that splits: 2 GiB.  Measured with the kernels truly
+ * co-resident (round 5, profiles/r5/split_thresholds/): AES-256 1 GiB loses
+ * 3-6% to the grid T-table (ECB 930 vs 991, CBC-dec 916 vs 971), 2 GiB wins
+ * 2-14%, 4 GiB 0-9%, 16 GiB 10-14%.  Below 2 GiB the persistent kernels'
+ * granularity (4096 T-table waves x 32 KiB units = 128 MiB per round, plus
+ * 32 MiB of LDS table fills per launch) costs more than the bitsliced waves
+ * add.  (Round 4's 896 MiB was measured while the halves ran one after the
+ * other: docs/PERF.md round 5.) */
+size_t split_min(int) { return (size_t)2 << 30; }
 
 int pick_ecb_impl(int impl, int bits, size_t nbytes)
 {
@@ -284,12 +290,6 @@ __global__ void k_claim_snapshot(unsigned long long *ctr, unsigned long long *ho
 }
 thread_local uint64_t g_split_word = 0, g_split_nunits = 0, g_split_ttwaves = 0;
 
-#ifndef OTC_SPLIT_TT_WGS
-#define OTC_SPLIT_TT_WGS 0u /* T-table claim workgroups in a split (0: one per CU; A/B knob) */
-#endif
-#ifndef OTC_SPLIT_BS_FIRST
-#define OTC_SPLIT_BS_FIRST 0 /* launch the bitsliced half first (A/B knob) */
-#endif
 /* The split: tt(cl) launches the T-table claim kernel on st, bs(cl, aux) the
  * bitsliced claim kernel on the auxiliary stream, both over the whole buffer
  * (nunits claim units, the T-table kernel also runs what lies past the last
@@ -321,7 +321,7 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
         return plain();
     }
     const SplitClaim cl{ctr, (uint32_t)nunits, bs_wgs};
-    const SplitClaim cl_tt{bs_only ? ctr + 1 : ctr, (uint32_t)nunits, bs_only ? 1u : OTC_SPLIT_TT_WGS};
+    const SplitClaim cl_tt{bs_only ? ctr + 1 : ctr, (uint32_t)nunits, bs_only ? 1u : 0u};
     /* zeroed (bs_only: the T-table's word all ones -- front + back far past
      * nunits, so its claims fail; hipMemsetD32Async at a 4-byte offset cost
      * ~40 ms per call), then fork: the aux stream starts after everything
@@ -329,18 +329,17 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
     if ((e = hipMemsetAsync(ctr, 0, sizeof *ctr, st)) == hipSuccess &&
         (e = hipMemsetAsync(ctr + 1, bs_only ? 0xFF : 0, sizeof *ctr, st)) == hipSuccess &&
         (e = hipEventRecord(a.fork, st)) == hipSuccess && (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess &&
-        (OTC_SPLIT_BS_FIRST || (e = tt(cl_tt)) == hipSuccess)) {
+        (e = tt(cl_tt)) == hipSuccess) {
         /* the bitsliced half failing (no memory for its key table) leaves the
          * T-table claim kernel to take every unit -- unless it was told to
          * take none (bs_only): then the T-table alone redoes the call.  The
          * join is recorded either way (a failure after its launch must still
          * be waited for). */
-        const hipError_t eb = bs(cl, a.s);
-        if (OTC_SPLIT_BS_FIRST) e = tt(cl_tt);
+        const hipError_t eb = bs_wgs ? bs(cl, a.s) : hipSuccess; /* 0: the T-table claim kernel alone */
         if (eb != hipSuccess) (void)hipGetLastError();
         if ((e = hipEventRecord(a.join, a.s)) == hipSuccess) e = hipStreamWaitEvent(st, a.join, 0);
         if (e == hipSuccess) {
-            if (eb == hipSuccess) *ran = bs_only ? OTC_IMPL_BITSLICE : OTC_IMPL_SPLIT;
+            if (eb == hipSuccess && bs_wgs) *ran = bs_only ? OTC_IMPL_BITSLICE : OTC_IMPL_SPLIT;
             else if (bs_only) e = plain();
             if (e == hipSuccess && g_split_stats.load(std::memory_order_relaxed)) {
                 /* the counter's last value sits where the agent-scope atomics
@@ -456,46 +455,63 @@ hipError_t seg_dec_split(bool cfb, const void *in, void *out, size_t seg_blocks,
         plain);
 }
 
-/* Segment ENCRYPTION (CBC / CFB128, one serial chain per segment): the
- * T-table segment kernel beside the row-sliced bs8 kernel (aes_bs8.hip),
- * claiming 64-segment units -- the T-table one per wave from the back, bs8
- * eight per wave from the front.  bs8 needs segments of < 8 MiB (32-bit lane
- * offsets); at least 16 units (1024 segments) to split. */
+/* the kernel family the calling thread's last AES call ran (otc_last_impl) */
+thread_local int g_last_impl = OTC_IMPL_AUTO;
+
+/* Segment ENCRYPTION (CBC / CFB128, one serial chain per segment).  Three
+ * forms: the grid T-table kernel; the persistent T-table claim kernel alone
+ * (64-segment units from one counter, no bitsliced half); and the
+ * co-resident split with the row-sliced bs8 kernel (aes_bs8.hip) taking
+ * 8-unit tasks from the front.  The split is explicit only (impl "split" /
+ * "bitslice"): measured with the kernels truly co-resident it LOSES at every
+ * size -- a bs8 wave beside four T-table waves runs a 512-chain task at
+ * ~0.06 GB/s, slows the latency-bound T-table chains by up to 30%, and its
+ * 8-unit tasks outlast the whole call at 4 KiB segments (CBC-enc-seg-256 4
+ * GiB: 738 vs 988 GB/s; 512 B: 983 vs 1027; profiles/r5/seg_split/).  auto
+ * runs the T-table: the persistent kernel for segments <= 1 KiB in calls >=
+ * 4 GiB (+1-7% over the grid kernel), the grid kernel otherwise (at 4 KiB
+ * segments the two tie within box noise, and below 4 GiB the grid kernel
+ * wins).  bs8 needs segments of < 8 MiB (32-bit lane offsets); at least 16
+ * units (1024 segments) to claim. */
 constexpr uint64_t SEG_UNIT = 64;
-#ifndef OTC_BS8_SPLIT_WGS
-#define OTC_BS8_SPLIT_WGS 1u /* bs8 workgroups per CU beside the T-table (A/B knob) */
-#endif
 bool segenc_bs8_ok(size_t seg_bytes) { return seg_bytes >= 16 && seg_bytes * SEG_UNIT * 8 <= 0xFFFFFFFFull; }
 
-/* auto: the split from segenc_split_min() bytes (docs/PERF.md round 5) */
-size_t segenc_split_min() { return (size_t)896 << 20; }
-
-int pick_segenc_impl(int impl, size_t nbytes, size_t seg_bytes)
+int pick_segenc_impl(int impl, size_t, size_t seg_bytes)
 {
     if (!segenc_bs8_ok(seg_bytes)) return OTC_IMPL_TTABLE;
     if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_SPLIT) return impl;
     const int env = env_impl();
-    if (env != OTC_IMPL_AUTO) return env;
-    return nbytes >= segenc_split_min() ? OTC_IMPL_SPLIT : OTC_IMPL_TTABLE;
+    return env != OTC_IMPL_AUTO ? env : OTC_IMPL_TTABLE;
 }
 
-hipError_t seg_enc_split(bool cfb, const void *in, void *out, size_t seg_blocks, size_t nseg, const otc_aes_key &K,
-                         Ctr128 iv0, bool bs_only, hipStream_t st, int *ran)
+bool segenc_persistent(size_t nbytes, size_t seg_bytes, size_t nseg)
 {
+    return seg_bytes <= 1024 && nbytes >= ((size_t)4 << 30) && nseg / SEG_UNIT >= 16 && nseg / SEG_UNIT <= 0x7FFFFFFFull;
+}
+
+hipError_t seg_enc_run(bool cfb, const void *in, void *out, size_t seg_bytes, size_t nseg, const otc_aes_key &K,
+                       Ctr128 iv0, int impl, hipStream_t st)
+{
+    const size_t seg_blocks = seg_bytes / 16;
+    const int pick = pick_segenc_impl(impl, seg_bytes * nseg, seg_bytes);
+    g_last_impl = pick;
+    auto grid = [&]() {
+        return cfb ? otc_impl::tt_cfb_encrypt_seg(in, out, seg_blocks, nseg, K, iv0, st)
+                   : otc_impl::tt_cbc_encrypt_seg(in, out, seg_blocks, nseg, K, iv0, st);
+    };
+    const bool persistent = pick == OTC_IMPL_TTABLE && segenc_persistent(seg_bytes * nseg, seg_bytes, nseg);
+    if (pick == OTC_IMPL_TTABLE && !persistent) return grid();
+    const bool bs_only = pick == OTC_IMPL_BITSLICE;
+    const unsigned bs_wgs = persistent ? 0u : (unsigned)otc_dev::device_cus() * (bs_only ? 4u : 1u);
     return split_claim(
-        nseg / SEG_UNIT, 16, bs_only, (unsigned)otc_dev::device_cus() * (bs_only ? 4u : OTC_BS8_SPLIT_WGS), st, ran,
+        nseg / SEG_UNIT, 16, bs_only, bs_wgs, st, &g_last_impl,
         [&](SplitClaim cl) { return otc_impl::tt_seg_encrypt_claim(cfb, in, out, seg_blocks, nseg, K, iv0, cl, st); },
         [&](SplitClaim cl, hipStream_t s) {
             return otc_impl::bs8_seg_encrypt_claim(cfb, in, out, seg_blocks, K, iv0, cl, s);
         },
-        [&]() {
-            return cfb ? otc_impl::tt_cfb_encrypt_seg(in, out, seg_blocks, nseg, K, iv0, st)
-                       : otc_impl::tt_cbc_encrypt_seg(in, out, seg_blocks, nseg, K, iv0, st);
-        });
+        grid);
 }
 
-/* the kernel family the calling thread's last AES call ran (otc_last_impl) */
-thread_local int g_last_impl = OTC_IMPL_AUTO;
 
 /* Device buffers of the cipher ops: non-null, 16-byte aligned (every kernel
  * moves 16 B per lane with global_load/store_dwordx4), and either the same
@@ -574,6 +590,15 @@ void otc_rt::aux_release_all()
 
 extern "C" int otc_last_impl(void) { return g_last_impl; }
 
+/* which: 0 the T-table kernels' records, 1 the bitsliced (32-block) claim
+ * kernels', 2 bs8's; -1 in a build without OTC_SPLIT_TRACE */
+extern "C" int otc_split_trace(int which, unsigned long long *buf, int max)
+{
+    if (!buf || max < 0) return set_err(OTC_ERR_ARG, "bad trace buffer");
+    return which == 0 ? otc_impl::strace_read_tt(buf, max) : which == 1 ? otc_impl::strace_read_bs(buf, max)
+                                                                         : otc_impl::strace_read_bs8(buf, max);
+}
+
 extern "C" void otc_split_stats(int on) { g_split_stats.store(on ? 1 : 0, std::memory_order_relaxed); }
 
 extern "C" int otc_split_last_units(uint64_t *front, uint64_t *back, uint64_t *nunits)
@@ -585,10 +610,6 @@ extern "C" int otc_split_last_units(uint64_t *front, uint64_t *back, uint64_t *n
     *back = b > g_split_ttwaves ? std::min(n, b - g_split_ttwaves) : 0;
     *front = n - *back;
     *nunits = n;
-    if (getenv("OTC_DEBUG_SPLIT_RAW"))
-        fprintf(stderr, "split raw word: front %llu back %llu, T-table waves %llu, units %llu\n",
-                (unsigned long long)(g_split_word & 0xFFFFFFFFull), (unsigned long long)(g_split_word >> 32),
-                (unsigned long long)g_split_ttwaves, (unsigned long long)n);
     return OTC_OK;
 }
 
@@ -806,12 +827,7 @@ extern "C" int otc_aes_cbc_encrypt_segments_impl(const void *in, void *out, size
     if (nseg == 0 || seg_bytes == 0) return OTC_OK;
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
-    g_last_impl = pick_segenc_impl(impl, seg_bytes * nseg, seg_bytes);
-    if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE)
-        e = seg_enc_split(false, in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
-                          g_last_impl == OTC_IMPL_BITSLICE, st, &g_last_impl);
-    else
-        e = otc_impl::tt_cbc_encrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0), st);
+    e = seg_enc_run(false, in, out, seg_bytes, nseg, *k, ctr_from_bytes(iv0), impl, st);
     if (e != hipSuccess) return hip_fail(e, "cbc_encrypt_segments launch");
     return OTC_OK;
 }
@@ -881,13 +897,7 @@ static int cfb_seg_common(const void *in, void *out, size_t seg_bytes, size_t ns
             e = otc_impl::tt_cfb_decrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
                                              (hipStream_t)stream);
     } else {
-        g_last_impl = pick_segenc_impl(impl, seg_bytes * nseg, seg_bytes);
-        if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE)
-            e = seg_enc_split(true, in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
-                              g_last_impl == OTC_IMPL_BITSLICE, (hipStream_t)stream, &g_last_impl);
-        else
-            e = otc_impl::tt_cfb_encrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
-                                             (hipStream_t)stream);
+        e = seg_enc_run(true, in, out, seg_bytes, nseg, *k, ctr_from_bytes(iv0), impl, (hipStream_t)stream);
     }
     if (e != hipSuccess) return hip_fail(e, what);
     return OTC_OK;

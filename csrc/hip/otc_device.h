@@ -177,6 +177,48 @@ __device__ __forceinline__ int64_t claim_front(const SplitClaim &c, uint32_t n, 
     return (int64_t)f;
 }
 
+/* Wave-start trace of the splits (a diagnostic build: make variant
+ * VFLAGS=-DOTC_SPLIT_TRACE=1): lane 0 of a wave appends {s_memrealtime,
+ * tag << 32 | HW_ID} to a per-code-object buffer; otc_split_trace reads it
+ * back.  Off (no code) in the shipped build. */
+#ifndef OTC_SPLIT_TRACE
+#define OTC_SPLIT_TRACE 0
+#endif
+constexpr unsigned STRACE_MAX = 16384;
+#if OTC_SPLIT_TRACE
+static __device__ unsigned long long g_strace[2 * STRACE_MAX];
+static __device__ unsigned int g_strace_n;
+__device__ __forceinline__ void strace(uint32_t tag)
+{
+    if (lane_id() == 0) {
+        const unsigned i = atomicAdd(&g_strace_n, 1u);
+        if (i < STRACE_MAX) {
+            uint32_t hw;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            g_strace[2 * i] = __builtin_amdgcn_s_memrealtime();
+            g_strace[2 * i + 1] = (unsigned long long)tag << 32 | hw;
+        }
+    }
+}
+/* host: copy out this code object's records (and reset the count) */
+#define OTC_STRACE_READER(NAME)                                                                   \
+    int NAME(unsigned long long *buf, int max)                                                    \
+    {                                                                                             \
+        unsigned n = 0;                                                                           \
+        if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_strace_n), sizeof n) != hipSuccess) return -1;   \
+        if (n > STRACE_MAX) n = STRACE_MAX;                                                       \
+        if ((int)n > max) n = (unsigned)max;                                                      \
+        if (n && hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_strace), 16ull * n) != hipSuccess) return -1; \
+        const unsigned z = 0;                                                                     \
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_strace_n), &z, sizeof z);                            \
+        return (int)n;                                                                            \
+    }
+#else
+__device__ __forceinline__ void strace(uint32_t) {}
+#define OTC_STRACE_READER(NAME)                                                                   \
+    int NAME(unsigned long long *, int) { return -1; }
+#endif
+
 /* Allocation fault injection, a test hook (otc_fault_inject_alloc): true
  * when the runtime allocation about to be made should fail.  One atomic
  * countdown; off (no cost beyond a relaxed load) unless armed. */

@@ -91,6 +91,11 @@ int otc_last_impl(void);
  * encryption).  Under impl "bitslice" front == nunits. */
 void otc_split_stats(int on);
 int otc_split_last_units(uint64_t *front, uint64_t *back, uint64_t *nunits);
+/* Diagnostic builds only (-DOTC_SPLIT_TRACE=1): copy out and reset the
+ * wave-start records of the split's kernels (which: 0 T-table, 1 bitsliced,
+ * 2 bs8), pairs {s_memrealtime, tag << 32 | HW_ID}; returns the count, or -1
+ * in the shipped build. */
+int otc_split_trace(int which, unsigned long long *buf, int max);
 
 /* ---- device ops (device pointers; async on `stream`) ---------------------
  * All functions accept any byte length; the trailing partial block of CTR is

@@ -100,8 +100,9 @@ def test_multi_gpu_api_matrix(gpu, rccl_world1, monkeypatch):
     got = {}
     for mode in ("ctr", "cbc-dec"):
         for name, ngpus, strategy in (("direct1", 1, "direct"), ("direct3", 3, "direct"), ("rccl1", 1, "rccl")):
-            y = np.zeros(n, np.uint8)
-            pstream.multi_gpu_run(mode, x, y, key, iv, ngpus=ngpus, strategy=strategy, chunk_bytes=256 << 10)
+            xp, y = pstream.pinned_empty(n), pstream.pinned_empty(n)  # pinned: the RCCL job's root copies overlap
+            xp[:] = x
+            pstream.multi_gpu_run(mode, xp, y, key, iv, ngpus=ngpus, strategy=strategy, chunk_bytes=256 << 10)
             got[(mode, "otc_multi_run/" + name)] = y.tobytes()
     t = torch.from_numpy(x.copy()).to(gpu)
     r = t.clone()

@@ -42,13 +42,21 @@ def test_engine_matches_oracle(gpu, pinned, mode):
     assert y.tobytes() == ref
 
 
+def pinned_copy(a):
+    p = pstream.pinned_empty(a.nbytes)
+    p[:] = a
+    return p
+
+
 @pytest.mark.parametrize("strategy", ["direct", "rccl"])
 @pytest.mark.parametrize("mode", ["ctr", "cbc-dec"])
 def test_multi_gpu_planner(gpu, strategy, mode):
+    """Pinned host buffers, as config 4/5 run them (the pageable form only
+    warns: test_multi_rccl_pageable_warns)."""
     ngpus = torch.cuda.device_count()
     n = (2 << 20) + 48
     key, iv = os.urandom(16), os.urandom(16)
-    x, y = rnd_np(n, 2), np.zeros(n, np.uint8)
+    x, y = pinned_copy(rnd_np(n, 2)), pstream.pinned_empty(n)
     st = pstream.multi_gpu_run(mode, x, y, key, iv, ngpus=ngpus, strategy=strategy, chunk_bytes=256 << 10)
     ref = cpu_ref.ctr(key, iv, x.tobytes()) if mode == "ctr" else cpu_ref.cbc(key, iv, x.tobytes(), decrypt=True)
     assert y.tobytes() == ref
@@ -204,9 +212,44 @@ def test_multi_rccl_cbc_dec_in_place_many_rounds(gpu):
     n = (5 << 20) + 16 * 3
     key, iv = os.urandom(16), os.urandom(16)
     data = rnd_np(n, 9)
-    x = data.copy()
+    x = pinned_copy(data)
     pstream.multi_gpu_run("cbc-dec", x, x, key, iv, ngpus=ngpus, strategy="rccl", chunk_bytes=512 << 10)
     assert x.tobytes() == cpu_ref.cbc(key, iv, data.tobytes(), decrypt=True)
+
+
+def test_multi_rccl_pageable_warns(gpu):
+    """The one intended pageable case: the job still equals the oracle, and
+    says that its root copies will block."""
+    n = (1 << 20) + 16
+    key, iv = os.urandom(16), os.urandom(16)
+    x, y = rnd_np(n, 10), np.zeros(n, np.uint8)
+    with pytest.warns(RuntimeWarning, match="pageable"):
+        pstream.multi_gpu_run("ctr", x, y, key, iv, ngpus=1, strategy="rccl", chunk_bytes=256 << 10)
+    assert y.tobytes() == cpu_ref.ctr(key, iv, x.tobytes())
+
+
+def test_engine_overlaps_h2d_cipher_d2h(gpu):
+    """A 512 MiB pinned job through the 3-stream engine: H2D of chunk k+1,
+    the cipher of chunk k and D2H of chunk k-1 run at once, so the wall time
+    is well under the sum of the three phases' event times (SURVEY 2.4 P7;
+    the reference's copies were synchronous and pageable,
+    /root/reference/aes-gpu/Source/AES.cu:236,252)."""
+    n = 512 << 20
+    key, ctr = os.urandom(16), os.urandom(16)
+    x = pstream.pinned_empty(n)
+    x[: 1 << 20] = rnd_np(1 << 20, 12)
+    x[1 << 20:] = 0x5A
+    y = pstream.pinned_empty(n)
+    with pstream.StreamEngine(0, chunk_bytes=32 << 20, depth=3) as eng:
+        eng.run("ctr", x, y, key, ctr)  # warm: streams, ring, clocks
+        st = eng.run("ctr", x, y, key, ctr)
+    phases = st["kernel_ms"] + st["h2d_ms"] + st["d2h_ms"]
+    assert st["chunks"] == 16
+    assert st["total_ms"] < 0.75 * phases, st
+    assert st["host_stage_ms"] == 0  # pinned: no staging copies
+    assert y[: 1 << 20].tobytes() == cpu_ref.ctr(key, ctr, x[: 1 << 20].tobytes())
+    tail = n - (1 << 16)
+    assert y[tail:].tobytes() == cpu_ref.ctr(key, ctr, x[tail:].tobytes(), block_offset=tail // 16)
 
 
 def test_multi_ctr_resident(gpu):

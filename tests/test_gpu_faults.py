@@ -55,13 +55,15 @@ def test_engine_create_and_run_under_alloc_faults(inject):
 
 def test_multi_rccl_job_under_alloc_faults(inject):
     key, iv = os.urandom(32), os.urandom(16)
-    x = _rnd((2 << 20) + 48, 2)
+    x = pstream.pinned_empty((2 << 20) + 48)
+    x[:] = _rnd(x.nbytes, 2)
     ref = cpu_ref.cbc(key, iv, x.tobytes(), decrypt=True)
     failed = 0
+    y = pstream.pinned_empty(x.nbytes)  # before arming: the injected faults are the job's own
     for k in range(8):
+        y[:] = 0
         inject(k)
         try:
-            y = np.zeros_like(x)
             pstream.multi_gpu_run("cbc-dec", x, y, key, iv, ngpus=1, strategy="rccl", chunk_bytes=256 << 10)
             assert y.tobytes() == ref
         except RuntimeError as e:
@@ -71,7 +73,7 @@ def test_multi_rccl_job_under_alloc_faults(inject):
             inject(-1)
         _native.require_gpu_lib().otc_release_resources()  # next attempt builds the job afresh
     assert failed >= 4  # 2 x (pin, pout) + 2 x (root_in, root_out)
-    y = np.zeros_like(x)
+    y = pstream.pinned_empty(x.nbytes)
     pstream.multi_gpu_run("cbc-dec", x, y, key, iv, ngpus=1, strategy="rccl", chunk_bytes=256 << 10)
     assert y.tobytes() == ref
 

@@ -435,14 +435,16 @@ def test_bitslice_launch_structures(gpu, bits):
 def test_auto_routing_rule(gpu):
     """impl="auto" by size (docs/PERF.md, profiles/r3/auto_impl,
     profiles/r4/ecb_split): bitsliced CTR from 2 GiB (AES-128/192) or 1 GiB
-    (AES-256), the co-resident split for ECB encryption from 896 MiB, T-table
-    for everything else; the boundaries are exact.  "split" is an
+    (AES-256), the co-resident split for ECB encryption from 2 GiB (round 5,
+    measured with the halves truly co-resident), T-table for everything else;
+    the boundaries are exact.  "split" is an
     ECB-encryption form: for CTR it routes as auto."""
     G = 1 << 30
     cases = [(128, "ctr", 64 * G, "bitslice"), (128, "ctr", 2 * G - 16, "ttable"), (128, "ctr", 2 * G, "bitslice"),
              (256, "ctr", 1 * G, "bitslice"), (256, "ctr", 1 * G - 16, "ttable"), (256, "ctr", 4 * G, "bitslice"),
              (192, "ctr", 2 * G, "bitslice"), (192, "ctr", 2 * G - 16, "ttable"), (192, "ctr", 1 * G, "ttable"),
-             (256, "ecb", 64 * G, "split"), (128, "ecb", 896 << 20, "split"), (192, "ecb", (896 << 20) - 16, "ttable"),
+             (256, "ecb", 64 * G, "split"), (128, "ecb", 2 * G, "split"), (192, "ecb", 2 * G - 16, "ttable"),
+             (256, "ecb", 1 * G, "ttable"),
              (128, "ctr", 16, "ttable")]
     for bits, mode, n, want in cases:
         assert ops.pick_impl("auto", bits, mode, n) == want, (bits, mode, n)
@@ -546,8 +548,41 @@ def test_segment_encrypt_split_matches_oracle(gpu, bits):
             for s0 in (0, nseg // 2, nseg - 4):
                 lo, hi = s0 * seg, (s0 + 4) * seg
                 assert hy[lo:hi] == ref(key, sh.ctr_add(iv0, s0), hx[lo:hi], seg), (name, bits, seg, s0)
-    assert ops.pick_impl("auto", 256, "seg-enc", 896 << 20) == "split"
-    assert ops.pick_impl("auto", 256, "seg-enc", (896 << 20) - 16) == "ttable"
+    # auto never picks the bs8 split: it loses at every size (engine.cpp seg_enc_run)
+    for n in (896 << 20, 4 << 30, 64 << 30):
+        assert ops.pick_impl("auto", 256, "seg-enc", n) == "ttable"
+
+
+@pytest.mark.parametrize("seg", [512, 1024])
+def test_segment_encrypt_persistent_ttable(gpu, seg):
+    """Segment encryption of >= 4 GiB in segments of <= 1 KiB runs the
+    persistent T-table claim kernel alone (64-segment units from one counter,
+    the segments past the last unit in workgroup 0): byte-identical to the
+    bs8 kernel alone and, on sampled segments, to the CPU oracle, CBC and
+    CFB, in place."""
+    key = os.urandom(32)
+    iv0 = os.urandom(8) + (2**64 - 3).to_bytes(8, "big")
+    nseg = ((4 << 30) + 64 * 7 * seg + 5 * seg) // seg  # a partial last unit
+    n = nseg * seg
+    x = torch.empty(n, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(x, seed=seg)
+    for name in ("cbc", "cfb"):
+        f = ops.cbc_encrypt_segments if name == "cbc" else ops.cfb128_encrypt_segments
+        ref = cpu_ref.cbc_segments if name == "cbc" else cpu_ref.cfb128_segments
+        y = f(x, key, iv0, seg)
+        assert ops.last_impl() == "ttable"
+        b = f(x, key, iv0, seg, impl="bitslice")
+        torch.cuda.synchronize()
+        assert torch.equal(y, b), (name, seg)
+        del b
+        for s0 in (0, nseg // 3, nseg - 70, nseg - 4):
+            lo, hi = s0 * seg, (s0 + 4) * seg
+            assert host(y[lo:hi]) == ref(key, sh.ctr_add(iv0, s0), host(x[lo:hi]), seg), (name, seg, s0)
+        f(x, key, iv0, seg, out=x)
+        torch.cuda.synchronize()
+        assert torch.equal(x, y), (name, seg, "in place")
+        del y
+        ops.fill_random_(x, seed=seg)
 
 
 def test_ecb_split_stream_order(gpu):
@@ -645,8 +680,8 @@ def test_bitsliced_decrypt_matches_ttable(gpu, bits):
         S = min(n, 1 << 14)
         assert host(t[:S]) == cpu_ref.ecb(key, host(x[:S]), decrypt=True)
         assert host(tc[:S]) == cpu_ref.cbc(key, iv, host(x[:S]), decrypt=True)
-    assert ops.pick_impl("auto", bits, "dec", 896 << 20) == "split"
-    assert ops.pick_impl("auto", bits, "dec", (896 << 20) - 16) == "ttable"
+    assert ops.pick_impl("auto", bits, "dec", 2 << 30) == "split"
+    assert ops.pick_impl("auto", bits, "dec", (2 << 30) - 16) == "ttable"
 
 
 @pytest.mark.parametrize("bits", [128, 192, 256])
@@ -674,8 +709,8 @@ def test_bitsliced_cfb_decrypt_matches_ttable(gpu, bits):
         assert host(t[:S]) == cpu_ref.cfb128(key, iv, host(x[:S]), decrypt=True)
         if n > S:  # the tail, with its predecessor block as the IV
             assert host(t[-S:]) == cpu_ref.cfb128(key, host(x[-S - 16:-S]), host(x[-S:]), decrypt=True)
-    assert ops.pick_impl("auto", bits, "cfb-dec", 896 << 20) == "split"
-    assert ops.pick_impl("auto", bits, "cfb-dec", (896 << 20) - 16) == "ttable"
+    assert ops.pick_impl("auto", bits, "cfb-dec", 2 << 30) == "split"
+    assert ops.pick_impl("auto", bits, "cfb-dec", (2 << 30) - 16) == "ttable"
 
 
 @pytest.mark.parametrize("bits", [128, 256])

@@ -78,10 +78,12 @@ def test_ctr_valu_budget(counts):
 def test_split_pairs_share_a_simd():
     """Co-residency of the claimed split, from the code objects: for every
     split mode, 4 waves of the T-table claim kernel plus 1 wave of the
-    bitsliced claim kernel fit in a SIMD's 512 registers at the hardware's
-    8-register allocation granule (docs/PERF.md round 4) -- a T-table change
-    that adds a few registers would silently turn the split into time
-    slicing."""
+    bitsliced claim kernel fit in a SIMD's 512 registers, counted as the
+    kernel descriptors allocate them (8-register granules; hipcc pads a
+    static-LDS kernel's descriptor to its LDS occupancy, which made the
+    round-4 "split" run its halves one after the other, docs/PERF.md round 5)
+    -- a T-table change that adds a few registers would silently turn the
+    split into time slicing."""
     tt_obj = os.path.join(ROOT, "build", "obj", "hip", "aes_tt.o")
     if not os.path.exists(tt_obj) or not os.path.exists(OBJ) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):
         pytest.skip("no built objects (make) or no ROCm LLVM tools")
@@ -92,7 +94,7 @@ def test_split_pairs_share_a_simd():
 
     def vgprs(obj):
         with tempfile.TemporaryDirectory() as tmp:
-            return {k: v[0] for k, v in isa_count.metadata(isa_count.code_object(obj, tmp)).items()}
+            return isa_count.descriptor_vgprs(isa_count.code_object(obj, tmp))
 
     tt, bs = vgprs(tt_obj), vgprs(OBJ)
     alloc = lambda n: -(-n // 8) * 8
@@ -113,20 +115,49 @@ def test_split_pairs_share_a_simd():
 
 
 def _vgprs(obj):
+    """kernel -> (descriptor VGPRs, scratch bytes)"""
     import tempfile
 
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import isa_count
 
     with tempfile.TemporaryDirectory() as tmp:
-        return isa_count.metadata(isa_count.code_object(obj, tmp))
+        co = isa_count.code_object(obj, tmp)
+        meta, desc = isa_count.metadata(co), isa_count.descriptor_vgprs(co)
+    return {k: (v, meta.get(k + ".kd", meta.get(k, (0, -1)))[1]) for k, v in desc.items()}
+
+
+def test_descriptors_match_register_use():
+    """Every claim kernel's descriptor allocates what the kernel uses (the
+    metadata's .vgpr_count rounded to the granule), not an occupancy-padded
+    count: the padding is what kept the round-4 split from co-running."""
+    import tempfile
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_count
+
+    objs = [os.path.join(ROOT, "build", "obj", "hip", f"{o}.o") for o in ("aes_tt", "aes_bs", "aes_bs8")]
+    if not all(os.path.exists(o) for o in objs) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):
+        pytest.skip("no built objects (make) or no ROCm LLVM tools")
+    seen = 0
+    for obj in objs:
+        with tempfile.TemporaryDirectory() as tmp:
+            co = isa_count.code_object(obj, tmp)
+            meta, desc = isa_count.metadata(co), isa_count.descriptor_vgprs(co)
+        for k, v in desc.items():
+            if "claim" in k:
+                used = meta.get(k + ".kd", meta.get(k))[0]
+                assert v == -(-used // 8) * 8, (k, v, used)
+                seen += 1
+    assert seen >= 30
 
 
 def test_bs8_segment_pair_shares_a_simd():
     """The chained segment-encryption split: the row-sliced bs8 kernel
     (csrc/hip/aes_bs8.hip, no scratch) fits one wave per SIMD beside the 4
     waves of the T-table segment claim kernel (single-buffered 8-block
-    bursts, <= 72 allocated), for CBC and CFB at every key size."""
+    bursts, <= 72 allocated), for CBC and CFB at every key size, counted
+    from the kernel descriptors."""
     tt_obj = os.path.join(ROOT, "build", "obj", "hip", "aes_tt.o")
     bs8_obj = os.path.join(ROOT, "build", "obj", "hip", "aes_bs8.o")
     if not os.path.exists(tt_obj) or not os.path.exists(bs8_obj) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):

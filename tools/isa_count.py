@@ -48,6 +48,31 @@ def metadata(co):
     return out
 
 
+def descriptor_vgprs(co):
+    """kernel symbol -> VGPRs the hardware allocates per wave, from the kernel
+    descriptor (compute_pgm_rsrc1 bits 5:0 = granules of 8 minus 1 on gfx950
+    wave64).  This, not the metadata's .vgpr_count, decides co-residency: with
+    a static LDS array hipcc pads the descriptor up to the occupancy the LDS
+    allows (csrc/hip/aes_tt.hip tt_lds)."""
+    secs = subprocess.run([f"{LLVM}/llvm-readelf", "-S", "-W", co], check=True, capture_output=True,
+                          text=True).stdout
+    layout = []  # (addr, file offset, size)
+    for m in re.finditer(r"\]\s+\S+\s+\S+\s+([0-9a-f]{8,})\s+([0-9a-f]{6,})\s+([0-9a-f]{6,})", secs):
+        layout.append((int(m.group(1), 16), int(m.group(2), 16), int(m.group(3), 16)))
+    syms = subprocess.run([f"{LLVM}/llvm-readelf", "-s", "-W", co], check=True, capture_output=True,
+                          text=True).stdout
+    data = open(co, "rb").read()
+    out = {}
+    for m in re.finditer(r"^\s*\d+:\s+([0-9a-f]+)\s+64\s+OBJECT\s+\S+\s+\S+\s+\S+\s+(\S+)\.kd$", syms, re.M):
+        addr = int(m.group(1), 16)
+        for a, off, size in layout:
+            if a <= addr < a + size:
+                rsrc1 = int.from_bytes(data[addr - a + off + 48:addr - a + off + 52], "little")
+                out[m.group(2)] = ((rsrc1 & 0x3F) + 1) * 8
+                break
+    return out
+
+
 def main():
     for obj in sys.argv[1:]:
         with tempfile.TemporaryDirectory() as tmp:
