@@ -127,8 +127,8 @@ bin/bc_test: csrc/cli/bc_test.cpp csrc/include/otc_cipher.hpp $(LIBDIR)/libotc.s
 O0FLAGS := -g -Wall -pedantic -O0 -std=gnu99
 O0_OBJ  := $(patsubst csrc/cpu/%.c,$(OBJ)/o0/%.o,$(CPU_SRC)) $(OBJ)/o0/bs_selftest.o
 # --- A/B variant libraries ------------------------------------------------
-# make variant NAME=kt0 VFLAGS="-DOTC_BS_KT_PREFETCH=0"  ->  variants/kt0/libotc.so
-# (its own object dir; load it with OTC_LIB=variants/kt0/libotc.so).  A/B
+# make variant NAME=b4 VFLAGS="-DOTC_TT_CLAIM_B=4"  ->  variants/b4/libotc.so
+# (its own object dir; load it with OTC_LIB=variants/b4/libotc.so).  A/B
 # switches are compile-time: the production library carries no env knobs.
 .PHONY: variant
 variant:

@@ -656,10 +656,8 @@ hipError_t launch(const BsParams &P, const otc_aes_key &K, hipStream_t st)
 {
     switch (K.nr) {
     case 10: return launch_nr<10, MODE>(P, K, st);
-#ifndef OTC_BS_ONLY_NR10
     case 12: return launch_nr<12, MODE>(P, K, st);
     case 14: return launch_nr<14, MODE>(P, K, st);
-#endif
     default: return hipErrorInvalidValue;
     }
 }

@@ -92,10 +92,9 @@ using gcptr = const __attribute__((address_space(1))) uint8_t *;
  *   base + j * 16 + k * chain_bytes + l * seg_bytes
  * (uniform 64-bit base + 32-bit offsets: global loads / stores with an SGPR
  * base and one VGPR offset). */
-#ifndef OTC_BS8_BURST
-#define OTC_BS8_BURST 1 /* plaintext blocks per chain per load burst (A/B knob) */
-#endif
-constexpr int BURST = OTC_BS8_BURST;
+/* plaintext blocks per chain per load burst: 2 and 4 (32-64 contiguous bytes
+ * per cache-line visit) measured no faster (profiles/r5/seg_split/bs8_burst.jsonl) */
+constexpr int BURST = 1;
 
 template <int NR, bool CFB, bool FULL>
 __device__ __forceinline__ void bs8_task(const Bs8Params &P, uint64_t u0, uint32_t n)

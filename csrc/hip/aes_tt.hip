@@ -44,15 +44,10 @@ using namespace otc_dev;
 #ifndef OTC_SEG_G
 #define OTC_SEG_G 8 /* blocks per load burst, grouped segment encryption (A/B knob) */
 #endif
-#ifndef OTC_SEG_TT_NT
-#define OTC_SEG_TT_NT 0 /* non-temporal plaintext / ciphertext in the segment claim kernel (A/B knob) */
-#endif
-#ifndef OTC_SEG_CLAIM_DB
-#define OTC_SEG_CLAIM_DB 0 /* double-buffered bursts in the segment claim kernel (A/B knob: single-buffered 8-block bursts, 60-65 VGPRs, ran 3-5% faster in the split than double-buffered 4-block ones, profiles/r5/seg_split) */
-#endif
-#ifndef OTC_SEG_CLAIM_G
-#define OTC_SEG_CLAIM_G 8 /* the same, in the claim kernel of the segment-encryption split */
-#endif
+/* the segment claim kernel: single-buffered 8-block bursts (60-65 VGPRs; 3-5%
+ * faster than double-buffered 4-block ones, non-temporal loads / stores far
+ * slower: profiles/r5/seg_split/tt_claim_ab.jsonl, tt_sb_ab.jsonl) */
+constexpr int SEG_CLAIM_G = 8;
 #ifndef OTC_TT_CTR_B
 #define OTC_TT_CTR_B 4 /* blocks per lane, bulk CTR kernel (A/B knob: 2 fits a bitsliced wave beside it) */
 #endif
@@ -248,18 +243,6 @@ __device__ __forceinline__ uint4 ld16(const uint8_t *p, uint64_t blk)
 __device__ __forceinline__ void st16(uint8_t *p, uint64_t blk, uint4 v)
 {
     *reinterpret_cast<uint4 *>(p + 16 * blk) = v;
-}
-/* non-temporal forms (the streaming cache policy) */
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 ld16_nt(const uint8_t *p, uint64_t blk)
-{
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p + 16 * blk));
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void st16_nt(uint8_t *p, uint64_t blk, uint4 v)
-{
-    u32x4 w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p + 16 * blk));
 }
 enum : int { E_ECB = 0, E_CFB_DEC = 2, E_CFB_DEC_SEG = 3 };
 enum : int { D_ECB = 0, D_CBC = 1, D_CBC_SEG = 2 };
@@ -713,7 +696,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg(CbcSegParams P, otc
  * group g is encrypted; ciphertext overwrites the plaintext registers and is
  * stored as a burst at the end of the group.  One segment per lane (two, with
  * 4- or 8-block bursts, measured 1-27% slower: profiles/r4/seg_ab/). */
-template <int NR, int G, bool CFB, bool NT = false, bool DB = true>
+template <int NR, int G, bool CFB, bool DB = true>
 __device__ __forceinline__ void seg_chain_g(const CbcSegParams &P, const otc_aes_key &K, const uint32_t *tbl,
                                             const uint32_t (&lk)[4], uint64_t seg, bool live)
 {
@@ -727,13 +710,13 @@ __device__ __forceinline__ void seg_chain_g(const CbcSegParams &P, const otc_aes
     ivv.hi = P.iv0.hi + (ivv.lo < P.iv0.lo ? 1 : 0);
     ctr_words(ivv, 0, false, c[0], c[1], c[2], c[3]);
 #pragma unroll
-    for (int t = 0; t < G; ++t) cur[t] = (live && ng) ? (NT ? ld16_nt : ld16)(P.in, first + t) : make_uint4(0, 0, 0, 0);
+    for (int t = 0; t < G; ++t) cur[t] = (live && ng) ? ld16(P.in, first + t) : make_uint4(0, 0, 0, 0);
     for (uint64_t g = 0; g < ng; ++g) {
         const bool more = g + 1 < ng;
         if constexpr (DB) {
 #pragma unroll
             for (int t = 0; t < G; ++t)
-                nxt[t] = (live && more) ? (NT ? ld16_nt : ld16)(P.in, first + (g + 1) * G + t) : make_uint4(0, 0, 0, 0);
+                nxt[t] = (live && more) ? ld16(P.in, first + (g + 1) * G + t) : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int t = 0; t < G; ++t) {
@@ -745,7 +728,7 @@ __device__ __forceinline__ void seg_chain_g(const CbcSegParams &P, const otc_aes
         }
 #pragma unroll
         for (int t = 0; t < G; ++t) {
-            if (live) (NT ? st16_nt : st16)(P.out, first + g * G + t, cur[t]);
+            if (live) st16(P.out, first + g * G + t, cur[t]);
             if constexpr (DB) cur[t] = nxt[t];
         }
         if constexpr (!DB) {
@@ -753,17 +736,17 @@ __device__ __forceinline__ void seg_chain_g(const CbcSegParams &P, const otc_aes
              * stores; the other waves of the SIMD cover its latency */
 #pragma unroll
             for (int t = 0; t < G; ++t)
-                cur[t] = (live && more) ? (NT ? ld16_nt : ld16)(P.in, first + (g + 1) * G + t) : make_uint4(0, 0, 0, 0);
+                cur[t] = (live && more) ? ld16(P.in, first + (g + 1) * G + t) : make_uint4(0, 0, 0, 0);
         }
     }
     /* remaining sb % G blocks, one at a time */
     for (uint64_t j = ng * G; j < sb; ++j) {
         uint32_t s[1][4];
-        const uint4 p = live ? (NT ? ld16_nt : ld16)(P.in, first + j) : make_uint4(0, 0, 0, 0);
+        const uint4 p = live ? ld16(P.in, first + j) : make_uint4(0, 0, 0, 0);
         chain_in<CFB>(p, c, K, s[0]);
         enc_rounds4_from<1, NR, 1>(tbl, lk, K, s);
         chain_out<CFB>(p, s[0], c);
-        if (live) (NT ? st16_nt : st16)(P.out, first + j, make_uint4(c[0], c[1], c[2], c[3]));
+        if (live) st16(P.out, first + j, make_uint4(c[0], c[1], c[2], c[3]));
     }
 }
 
@@ -798,12 +781,12 @@ __global__ __launch_bounds__(1024) void k_aes_seg_enc_tt_claim(CbcSegParams P, o
     const uint64_t done = (uint64_t)P.cl.nunits * SEG_UNIT;
     if (blockIdx.x == 0 && done + (threadIdx.x & ~63u) < P.nseg) { /* the remainder (< 64 segments): wave 0 */
         const uint64_t seg = done + threadIdx.x;
-        seg_chain_g<NR, G, CFB, OTC_SEG_TT_NT, OTC_SEG_CLAIM_DB>(P, K, tbl, lk, seg, seg < P.nseg);
+        seg_chain_g<NR, G, CFB, false>(P, K, tbl, lk, seg, seg < P.nseg);
     }
     for (;;) {
         const int64_t u = claim_unit(P.cl, true);
         if (u < 0) break;
-        seg_chain_g<NR, G, CFB, OTC_SEG_TT_NT, OTC_SEG_CLAIM_DB>(P, K, tbl, lk, (uint64_t)u * SEG_UNIT + lane_id(), true);
+        seg_chain_g<NR, G, CFB, false>(P, K, tbl, lk, (uint64_t)u * SEG_UNIT + lane_id(), true);
     }
 }
 
@@ -1535,7 +1518,7 @@ hipError_t tt_seg_encrypt_claim(bool cfb, const void *in, void *out, uint64_t se
     P.iv0 = iv0;
     P.cl = cl;
     const dim3 g(cl.wgs ? cl.wgs : (unsigned)num_cus()), b(1024);
-    constexpr int G = OTC_SEG_CLAIM_G;
+    constexpr int G = SEG_CLAIM_G;
     auto go = [&](auto nr) {
         constexpr int NR = decltype(nr)::value;
         return cfb ? launch_dyn<k_aes_seg_enc_tt_claim<NR, G, true>>(g, b, ENC_LDS, st, P, K)

@@ -97,10 +97,8 @@ __device__ __forceinline__ uint32_t rc4_addr(uint32_t x, uint32_t lane4) { retur
  * zero pad), then t = x | x << 6 (bits 0-1 = x0-1, bits 8-13 = x2-7) and one
  * bit-field insert of the lane term into bits 2-7 (mask 0x3F03 in an SGPR).
  * The PRGA issues ~21 instructions per byte with the LDS pipe 25% busy
- * (profiles/r5/rc4/): instruction count, not LDS bandwidth, is its budget. */
-#ifndef OTC_RC4_ADDR3
-#define OTC_RC4_ADDR3 1
-#endif
+ * (profiles/r5/rc4/): +1-3% over the five-VALU form
+ * (profiles/r5/rc4/ab_addr3_vs_addr5.jsonl). */
 __device__ __forceinline__ uint32_t add8(uint32_t a, uint32_t b)
 {
     uint32_t r;
@@ -243,15 +241,15 @@ __device__ __forceinline__ void rc4_prga(uint8_t *S, uint32_t lane4, uint32_t &i
             uint8_t *si_ = q < 15 ? Sk + rc4_ioff(q + 1) : Sn;                                                 \
             uint8_t *sp_ = q < 14 ? Sk + rc4_ioff(q + 2) : (q == 14 ? Sn : Sn + rc4_ioff(1));                            \
             const uint32_t a_ = an;                                                                            \
-            j = OTC_RC4_ADDR3 ? add8(j, a_) : (j + a_) & 0xFFu;                                                \
-            const uint32_t aj_ = OTC_RC4_ADDR3 ? rc4_addr8(j, lane4) : rc4_addr(j, lane4);                    \
+            j = add8(j, a_);                                                                                   \
+            const uint32_t aj_ = rc4_addr8(j, lane4);                                                          \
             const uint32_t b_ = S[aj_];                                                                        \
             const uint32_t pn_ = *sp_;                                                                         \
             const uint32_t inx_ = q < 14 ? ib + (uint32_t)(q + 2) : nb + (uint32_t)(q - 14);                   \
             an = (j == inx_) ? a_ : pn_;                                                                       \
             *si_ = (uint8_t)b_;                                                                                \
             S[aj_] = (uint8_t)a_;                                                                              \
-            const uint32_t o_ = S[OTC_RC4_ADDR3 ? rc4_addr8(add8(a_, b_), lane4) : rc4_addr(a_ + b_, lane4)];   \
+            const uint32_t o_ = S[rc4_addr8(add8(a_, b_), lane4)];                                            \
             w[q >> 2] |= o_ << (8 * (q & 3));                                                                  \
         }                                                                                                      \
     }

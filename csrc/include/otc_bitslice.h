@@ -25,19 +25,6 @@
 #define OTC_HD inline
 #endif
 
-#ifndef OTC_BS_FENCE_SBOX
-#define OTC_BS_FENCE_SBOX 0
-#endif
-#ifndef OTC_BS_FENCE_MC
-#define OTC_BS_FENCE_MC 0
-#endif
-/* 1: the key terms of the NEXT S-box of a round are loaded (scalar loads)
- * before the current S-box runs, so their latency hides under its ~83 VALU
- * ops instead of stalling every S-box (s_load; s_waitcnt lgkmcnt(0) in front
- * of each one otherwise). */
-#ifndef OTC_BS_KT_PREFETCH
-#define OTC_BS_KT_PREFETCH 1
-#endif
 
 
 namespace otc_bs {
@@ -228,7 +215,6 @@ OTC_HD void mix_column(const W *in, W *out)
         o[5] = xx3<VEC>(dr[4], an[5], d2[5]);
         o[6] = xx3<VEC>(dr[5], an[6], d2[6]);
         o[7] = xx3<VEC>(dr[6], an[7], d2[7]);
-        if (OTC_BS_FENCE_MC) sched_fence();
     }
 }
 
@@ -255,7 +241,6 @@ OTC_HD void mix_column_t(const W *in, W *out)
             const W u = fb ? xx3<VEC>(ar[i - 1], an[i - 1], d7) : xx3<VEC>(ar[i - 1], an[i - 1], t[i]);
             o[i] = fb ? xx3<VEC>(u, t[i], ar[i]) : (u ^ ar[i]);
         }
-        if (OTC_BS_FENCE_MC) sched_fence();
     }
 }
 
@@ -336,7 +321,6 @@ OTC_HD void sbox_byte(W *s, int b, KF &kf)
         sbox_k<false>(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], kf(R, p), kf(R, p + 1), kf(R, p + 2),
                       kf(R, p + 3), kf(R, p + 4), kf(R, p + 5), kf(R, p + 6), kf(R, p + 7));
     if (vec) pin8(x); /* uniform (SALU) bytes must not be forced into VGPRs */
-    if (OTC_BS_FENCE_SBOX) sched_fence();
 }
 
 /* One AES round on the planes.  Streaming order per OUTPUT column c:
@@ -364,7 +348,6 @@ OTC_HD void encrypt_round(W *s, KF &kf)
                 mix_column<false>(col, ns + 32 * c);
             else
                 mix_column<true>(col, ns + 32 * c);
-            if (OTC_BS_FENCE_MC) sched_fence();
         }
 #pragma unroll
         for (int q = 0; q < 128; ++q) s[q] = ns[q];
@@ -399,8 +382,11 @@ OTC_HD void round_step_kt(W *s, KT kt)
      * c = i / 4, r = i % 4 (ShiftRows brings it into column c); decryption:
      * r + 4((c - r) & 3) (InvShiftRows) */
     constexpr int SG = DEC ? -1 : 1;
+    /* the key terms of the NEXT S-box are loaded (scalar loads) before the
+     * current one runs, so their latency hides under its ~83 VALU ops instead
+     * of an s_waitcnt lgkmcnt(0) in front of every S-box */
     W tn[OTC_SBOX_KEY_TERMS];
-    if (OTC_BS_KT_PREFETCH) kt(0, tn);
+    kt(0, tn);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         W col[32];
@@ -409,16 +395,12 @@ OTC_HD void round_step_kt(W *s, KT kt)
             const int b = r + 4 * ((c + SG * r) & 3);
             W *x = s + 8 * b;
             W t[OTC_SBOX_KEY_TERMS];
-            if (OTC_BS_KT_PREFETCH) {
 #pragma unroll
-                for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = tn[j];
-                kt_ready(t);
-                const int i = 4 * c + r + 1;
-                if (i < 16) kt((i & 3) + 4 * (((i >> 2) + SG * (i & 3)) & 3), tn);
-                sched_fence(); /* the loads issue here, not next to their use */
-            } else {
-                kt(b, t);
-            }
+            for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = tn[j];
+            kt_ready(t);
+            const int i = 4 * c + r + 1;
+            if (i < 16) kt((i & 3) + 4 * (((i >> 2) + SG * (i & 3)) & 3), tn);
+            sched_fence(); /* the loads issue here, not next to their use */
             /* FENCE 3: every LUT output pinned in the low-pressure order of
              * tools/sbox_schedule.py; 2: pin + scheduling barrier per S-box;
              * 1: pin only; 0: the scheduler may interleave S-boxes (more ILP,
@@ -454,20 +436,16 @@ template <class KT, bool DEC = false>
 OTC_HD void round_final_kt(W *s, KT kt)
 {
     W tn[OTC_SBOX_KEY_TERMS];
-    if (OTC_BS_KT_PREFETCH) kt(0, tn);
+    kt(0, tn);
 #pragma unroll
     for (int b = 0; b < 16; ++b) {
         W *x = s + 8 * b;
         W t[OTC_SBOX_KEY_TERMS];
-        if (OTC_BS_KT_PREFETCH) {
 #pragma unroll
-            for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = tn[j];
-            kt_ready(t);
-            if (b + 1 < 16) kt(b + 1, tn);
-            sched_fence();
-        } else {
-            kt(b, t);
-        }
+        for (int j = 0; j < OTC_SBOX_KEY_TERMS; ++j) t[j] = tn[j];
+        kt_ready(t);
+        if (b + 1 < 16) kt(b + 1, tn);
+        sched_fence();
         sbox_lut3_c(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7],
                     t[8], t[9], t[10]);
         pin8(x);

@@ -225,6 +225,7 @@ def _declare_gpu(lib):
         "otc_host_register": (c_int, [c_vp, c_sz]),
         "otc_host_unregister": (c_int, [c_vp]),
         "otc_host_alloc_pinned": (c_vp, [c_sz]),
+        "otc_ptr_kind": (c_int, [c_vp]),
         "otc_host_free_pinned": (None, [c_vp]),
         "otc_engine_create": (c_vp, [c_int, c_sz, c_int]),
         "otc_engine_destroy": (None, [c_vp]),

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (evidence script: the knob it varied was removed from the source after the A/B; see docs/PERF.md round 5)
 # bs8 plaintext load bursts (OTC_BS8_BURST 1 / 2 / 4: variants base, b8b2,
 # b8b4), bs8 alone and in the split, CBC-enc-seg AES-256, 4 KiB and 512 B
 # segments, 4 GiB, verified, with power -> gpurun_out/r5_bs8_burst/ab.jsonl

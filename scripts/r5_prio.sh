@@ -1,4 +1,5 @@
 #!/bin/bash
+# (evidence script: the knob it varied was removed from the source after the A/B; see docs/PERF.md round 5)
 # Co-resident split (base) vs the T-table claim kernel alone (nobs) vs the
 # split with the T-table waves at issue priority 3 (prio3): AES-256 4 GiB.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (evidence script: the knob it varied was removed from the source after the A/B; see docs/PERF.md round 5)
 # RC4 PRGA byte-index addressing: 3 VALU (base, OTC_RC4_ADDR3=1) vs 5 (rc4old).
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=gpurun_out/${1:-r5_rc4_ab}; mkdir -p $O

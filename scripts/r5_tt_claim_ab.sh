@@ -1,4 +1,5 @@
 #!/bin/bash
+# (evidence script: the knob it varied was removed from the source after the A/B; see docs/PERF.md round 5)
 # T-table half of the segment-encryption split: 4- vs 8-block bursts
 # (OTC_SEG_CLAIM_G; base = 4, tg8 = 8) and non-temporal plaintext /
 # ciphertext (OTC_SEG_TT_NT; ttnt, tg8nt), CBC-enc-seg AES-256, 4 GiB,

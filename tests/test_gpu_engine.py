@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 import torch
 
+from our_tree_amd import _native
 from our_tree_amd.models import cpu_ref
 from our_tree_amd.parallel import dist as pdist
 from our_tree_amd.parallel import stream as pstream
@@ -226,6 +227,18 @@ def test_multi_rccl_pageable_warns(gpu):
     with pytest.warns(RuntimeWarning, match="pageable"):
         pstream.multi_gpu_run("ctr", x, y, key, iv, ngpus=1, strategy="rccl", chunk_bytes=256 << 10)
     assert y.tobytes() == cpu_ref.ctr(key, iv, x.tobytes())
+
+
+def test_pinned_buffers_are_seen_as_pinned(gpu):
+    """pinned_empty() memory classifies as pinned, numpy memory as pageable,
+    a CUDA tensor as device (otc_ptr_kind through a pointer-typed ctypes
+    signature; undeclared, the address was truncated to 32 bits)."""
+    p, h = pstream.pinned_empty(1 << 20), np.zeros(1 << 20, np.uint8)
+    assert pstream.pageable_buffers(p, h) == [1]
+    lib = _native.require_gpu_lib()
+    d = torch.empty(1 << 20, dtype=torch.uint8, device=gpu)
+    assert lib.otc_ptr_kind(p.ctypes.data) == pstream.PTR_PINNED
+    assert lib.otc_ptr_kind(d.data_ptr()) == pstream.PTR_DEVICE
 
 
 def test_engine_overlaps_h2d_cipher_d2h(gpu):

@@ -3,8 +3,9 @@ detection / fault injection"): ``otc_fault_inject_alloc(n)`` makes the
 (n+1)-th runtime allocation from now fail once -- device chunk buffers,
 NUMA-pinned host windows, RCCL job buffers, the bitsliced kernel's per-call
 tables.  Every entry point must then fail cleanly with an error (or, for the
-bitsliced CTR tables, fall back to the uncached kernel with identical output),
-release what it had built, and work again on the next call."""
+bitsliced CTR tables, fall back to the uncached kernel, and for the claimed
+kernels to the T-table, with identical output), release what it had built,
+and work again on the next call."""
 import os
 
 import numpy as np
@@ -89,17 +90,25 @@ def test_bitslice_ctr_falls_back_without_group_table(inject, gpu, bits):
     assert y.cpu().numpy().tobytes() == cpu_ref.ctr(key, ctr, x.cpu().numpy().tobytes())
 
 
-def test_bitslice_ecb_table_failure_is_an_error(inject, gpu):
+@pytest.mark.parametrize("k", [0, 1])
+def test_bitslice_ecb_alloc_failure_falls_back(inject, gpu, k):
+    """impl="bitslice" ECB is the bitsliced claim kernel alone (split_claim,
+    bs_only).  If its work counter (allocation 0) or key table (allocation 1)
+    cannot be allocated, the T-table runs the call instead -- complete output,
+    and last_impl() says so -- and the next call runs bitsliced again."""
     key = os.urandom(16)
-    x = torch.from_numpy(_rnd(16 * 4096, 4)).to(gpu)
-    inject(0)
-    with pytest.raises(RuntimeError):
-        ops.ecb_encrypt(x, key, impl="bitslice")
-        torch.cuda.synchronize()
+    x = torch.from_numpy(_rnd(16 * 4096 * 3 + 32, 4)).to(gpu)
+    ref = cpu_ref.ecb(key, x.cpu().numpy().tobytes())
+    inject(k)
+    y = ops.ecb_encrypt(x, key, impl="bitslice")
+    torch.cuda.synchronize()
+    assert ops.last_impl() == "ttable"
+    assert y.cpu().numpy().tobytes() == ref
     inject(-1)
     y = ops.ecb_encrypt(x, key, impl="bitslice")
     torch.cuda.synchronize()
-    assert y.cpu().numpy().tobytes() == cpu_ref.ecb(key, x.cpu().numpy().tobytes())
+    assert ops.last_impl() == "bitslice"
+    assert y.cpu().numpy().tobytes() == ref
 
 
 @pytest.mark.parametrize("k,want", [(0, "ttable"), (1, "ttable")])
