@@ -442,13 +442,27 @@ def main():
             emit({"error": "extra verification failed", "failed": bad, **extra})
         sys.exit(1)
 
+    # The extras run after the headline is measured.  An exception in one of
+    # them (a transport error at N > 1, say) is recorded in the line instead
+    # of losing the headline; a verification FAILURE still ends the run.
+    extras_errors = {}
+
+    def guarded(name, fn):
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+            extras_errors[name] = f"{type(e).__name__}: {e}"[:500]
+            return None
+
     if not args.no_stream:
-        extra.update(stream_pass(args, key, counter, rank, world, local, my_block0))
-        if not extra["stream_ctr_verified"]:
+        sp = guarded("stream", lambda: stream_pass(args, key, counter, rank, world, local, my_block0))
+        extra.update(sp or {"stream_ctr_verified": None})
+        if extra["stream_ctr_verified"] is False:
             if rank == 0:
                 emit({"error": "host-streamed CTR verification failed", **extra})
             sys.exit(1)
 
+    sc = None
     if not args.no_scatter:
         from our_tree_amd.parallel import jobs
 
@@ -456,8 +470,9 @@ def main():
         if not cpu:
             torch.cuda.empty_cache()
         chunk = (args.scatter_mib << 20) if not cpu else 4096 * 8
-        sc = jobs.cbc_scatter_job(args.scatter_rounds, chunk, key256, bytes(range(0xA0, 0xB0)), sector=4096,
-                                  device=dev)
+        sc = guarded("rccl_scatter", lambda: jobs.cbc_scatter_job(args.scatter_rounds, chunk, key256,
+                                                                  bytes(range(0xA0, 0xB0)), sector=4096, device=dev))
+    if not args.no_scatter and sc is not None:
         extra["rccl_cbc256_scatter_gbps"] = round(sc["gbps"], 3)
         extra["rccl_ranks"] = sc["ranks"]
         extra["rccl_ranks_verified"] = sc["ranks_verified"]
@@ -477,10 +492,11 @@ def main():
         from our_tree_amd.utils import refmethod
 
         if rank == 0:
-            extra.update(refmethod.ecb256_three_ways(device=local))
+            extra.update(guarded("refmethod", lambda: refmethod.ecb256_three_ways(device=local))
+                         or {"refmethod_verified": None})
         if torch.distributed.is_initialized():
             torch.distributed.barrier()
-        if rank == 0 and not extra["refmethod_verified"]:
+        if rank == 0 and extra["refmethod_verified"] is False:
             emit({"error": "reference-methodology ECB verification failed", **extra})
             sys.exit(1)
 
@@ -523,6 +539,8 @@ def main():
             "verified_sample": all(d["verified"] for d in table),
             **extra,
         }
+        if extras_errors:
+            line["extras_errors"] = extras_errors
         emit(line)
     if meter is not None:
         meter.close()

@@ -72,6 +72,20 @@ __device__ __forceinline__ uint32_t lds_at(const uint32_t *tbl, uint32_t byte_ad
     return *(const uint32_t *)((const char *)tbl + byte_addr);
 }
 
+/* The claim kernels' tables live in dynamic LDS (tt_lds below), which starts
+ * at address 0 -- those kernels declare no static LDS (tests/test_isa_cpu.py
+ * checks their descriptors' fixed group segment size is 0).  hipcc learns the
+ * dynamic base only after instruction selection, so addressing through the
+ * extern array adds it to every lookup (v_add_u32 v, 0, v: +1792 VALU per
+ * AES-256 ECB claim-loop iteration, +36% instructions, ~8-10% slower).  Their
+ * lookups take the integer LDS address instead. */
+struct DynTbl {
+};
+__device__ __forceinline__ uint32_t lds_at(DynTbl, uint32_t byte_addr)
+{
+    return *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t)byte_addr;
+}
+
 /* LDS address of table k's entry for byte k of state word w: byte 1 <- that
  * byte, bytes 0 / 2 <- the per-lane, per-table constant lkk (whose bytes 1
  * and 3 are zero).  For k = 1 the byte is already in place, so the address is
@@ -120,8 +134,8 @@ __device__ __forceinline__ void tbl4_lane_consts(uint32_t lane, uint32_t (&lk)[4
  * in flight per wave); with at most 16 waves per CU (the 128 KiB table allows
  * one workgroup) that starves the LDS pipe.  gfx9 lgkmcnt still caps a wave at
  * 15 outstanding LDS ops. */
-template <int R0, int NR, int B>
-__device__ __forceinline__ void enc_rounds4_from(const uint32_t *tbl, const uint32_t (&lk)[4], const otc_aes_key &K,
+template <int R0, int NR, int B, class TBL>
+__device__ __forceinline__ void enc_rounds4_from(TBL tbl, const uint32_t (&lk)[4], const otc_aes_key &K,
                                                  uint32_t (&s)[B][4])
 {
 #pragma unroll
@@ -193,8 +207,8 @@ __device__ __forceinline__ void fill_dtbl4(uint32_t *lds, const uint32_t *td0, c
     }
 }
 
-template <int NR, int B>
-__device__ __forceinline__ void dec_rounds4(const uint32_t *tbl, const uint32_t (&lk)[4], uint32_t lk_is2,
+template <int NR, int B, class TBL>
+__device__ __forceinline__ void dec_rounds4(TBL tbl, const uint32_t (&lk)[4], uint32_t lk_is2,
                                             const otc_aes_key &K, uint32_t (&s)[B][4])
 {
 #pragma unroll
@@ -294,6 +308,15 @@ __device__ __forceinline__ uint32_t *tt_lds()
         return tt_static_lds;
     }
 }
+/* what the lookups address: the static array, or dynamic LDS by integer */
+template <bool DYN>
+__device__ __forceinline__ auto tt_ref(const uint32_t *p)
+{
+    if constexpr (DYN)
+        return DynTbl{};
+    else
+        return p;
+}
 
 /* CLAIM: the T-table half of a co-resident split (otc_device.h SplitClaim):
  * workgroup 0 first runs the blocks past the last full 2048-block unit, then
@@ -341,7 +364,7 @@ __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_ke
             for (int j = 0; j < 4; ++j) s[b][j] ^= K.rk[j];
         }
 
-        enc_rounds4_from<1, NR, B>(tbl, lk, K, s);
+        enc_rounds4_from<1, NR, B>(tt_ref<CLAIM>(tbl), lk, K, s);
 
 #pragma unroll
         for (int b = 0; b < B; ++b) {
@@ -555,7 +578,7 @@ __device__ __forceinline__ void dec_tt_body(const DecParams &P, const otc_aes_ke
             }
         }
 
-        dec_rounds4<NR, B>(tbl, lk, lk_is2, K, s);
+        dec_rounds4<NR, B>(tt_ref<CLAIM>(tbl), lk, lk_is2, K, s);
 
 #pragma unroll
         for (int b = 0; b < B; ++b) {
@@ -696,8 +719,8 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg(CbcSegParams P, otc
  * group g is encrypted; ciphertext overwrites the plaintext registers and is
  * stored as a burst at the end of the group.  One segment per lane (two, with
  * 4- or 8-block bursts, measured 1-27% slower: profiles/r4/seg_ab/). */
-template <int NR, int G, bool CFB, bool DB = true>
-__device__ __forceinline__ void seg_chain_g(const CbcSegParams &P, const otc_aes_key &K, const uint32_t *tbl,
+template <int NR, int G, bool CFB, bool DB = true, class TBL = const uint32_t *>
+__device__ __forceinline__ void seg_chain_g(const CbcSegParams &P, const otc_aes_key &K, TBL tbl,
                                             const uint32_t (&lk)[4], uint64_t seg, bool live)
 {
     const uint64_t sb = P.seg_blocks;
@@ -781,12 +804,12 @@ __global__ __launch_bounds__(1024) void k_aes_seg_enc_tt_claim(CbcSegParams P, o
     const uint64_t done = (uint64_t)P.cl.nunits * SEG_UNIT;
     if (blockIdx.x == 0 && done + (threadIdx.x & ~63u) < P.nseg) { /* the remainder (< 64 segments): wave 0 */
         const uint64_t seg = done + threadIdx.x;
-        seg_chain_g<NR, G, CFB, false>(P, K, tbl, lk, seg, seg < P.nseg);
+        seg_chain_g<NR, G, CFB, false>(P, K, DynTbl{}, lk, seg, seg < P.nseg);
     }
     for (;;) {
         const int64_t u = claim_unit(P.cl, true);
         if (u < 0) break;
-        seg_chain_g<NR, G, CFB, false>(P, K, tbl, lk, (uint64_t)u * SEG_UNIT + lane_id(), true);
+        seg_chain_g<NR, G, CFB, false>(P, K, DynTbl{}, lk, (uint64_t)u * SEG_UNIT + lane_id(), true);
     }
 }
 

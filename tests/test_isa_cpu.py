@@ -175,3 +175,25 @@ def test_bs8_segment_pair_shares_a_simd():
             assert 4 * alloc(t) + alloc(b) <= 512, (nr, cfb, t, b)
             seen += 1
     assert seen == 6
+
+
+def test_ttable_claim_kernels_have_no_static_lds():
+    """The T-table claim kernels address their dynamic-LDS tables by integer
+    from address 0 (aes_tt.hip DynTbl): that holds only while they declare no
+    static LDS, i.e. their descriptors' fixed group segment is 0 bytes."""
+    import tempfile
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_count
+
+    tt_obj = os.path.join(ROOT, "build", "obj", "hip", "aes_tt.o")
+    if not os.path.exists(tt_obj) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):
+        pytest.skip("no built aes_tt.o (make) or no ROCm LLVM tools")
+    with tempfile.TemporaryDirectory() as tmp:
+        d = isa_count.descriptor_vgprs(isa_count.code_object(tt_obj, tmp), with_lds=True)
+    claims = {k: v for k, v in d.items() if "_claim" in k}
+    assert len(claims) >= 24, sorted(claims)
+    for k, (vg, lds) in claims.items():
+        assert lds == 0, (k, lds)
+    # the grid kernels keep their static tables (128 / 160 KiB)
+    assert any(lds >= 128 << 10 for k, (vg, lds) in d.items() if "_claim" not in k)

@@ -48,12 +48,13 @@ def metadata(co):
     return out
 
 
-def descriptor_vgprs(co):
+def descriptor_vgprs(co, with_lds=False):
     """kernel symbol -> VGPRs the hardware allocates per wave, from the kernel
     descriptor (compute_pgm_rsrc1 bits 5:0 = granules of 8 minus 1 on gfx950
     wave64).  This, not the metadata's .vgpr_count, decides co-residency: with
     a static LDS array hipcc pads the descriptor up to the occupancy the LDS
-    allows (csrc/hip/aes_tt.hip tt_lds)."""
+    allows (csrc/hip/aes_tt.hip tt_lds).  with_lds: (VGPRs, the descriptor's
+    group_segment_fixed_size = static LDS bytes)."""
     secs = subprocess.run([f"{LLVM}/llvm-readelf", "-S", "-W", co], check=True, capture_output=True,
                           text=True).stdout
     layout = []  # (addr, file offset, size)
@@ -68,7 +69,8 @@ def descriptor_vgprs(co):
         for a, off, size in layout:
             if a <= addr < a + size:
                 rsrc1 = int.from_bytes(data[addr - a + off + 48:addr - a + off + 52], "little")
-                out[m.group(2)] = ((rsrc1 & 0x3F) + 1) * 8
+                lds = int.from_bytes(data[addr - a + off:addr - a + off + 4], "little")
+                out[m.group(2)] = (((rsrc1 & 0x3F) + 1) * 8, lds) if with_lds else ((rsrc1 & 0x3F) + 1) * 8
                 break
     return out
 
