@@ -259,13 +259,15 @@ void aux_give(const AuxStream &a)
 }
 
 /* the smallest call that splits: 2 GiB.  Measured with the kernels truly
- * co-resident (round 5, profiles/r5/split_thresholds/): AES-256 1 GiB loses
- * 3-6% to the grid T-table (ECB 930 vs 991, CBC-dec 916 vs 971), 2 GiB wins
- * 2-14%, 4 GiB 0-9%, 16 GiB 10-14%.  Below 2 GiB the persistent kernels'
- * granularity (4096 T-table waves x 32 KiB units = 128 MiB per round, plus
- * 32 MiB of LDS table fills per launch) costs more than the bitsliced waves
- * add.  (Round 4's 896 MiB was measured while the halves ran one after the
- * other: docs/PERF.md round 5.) */
+ * co-resident (round 5, profiles/r5/split_ab/remeasure_int_lds.jsonl,
+ * split_thresholds/thresh2_int_lds.jsonl): against the grid T-table, AES-256
+ * ECB wins 15% at 2 GiB, 24% at 4 and 64 GiB, CBC-dec 10% at 2 GiB and 21% at
+ * 16 GiB, CFB-dec 26% at 16 GiB; at 1 GiB and below it is mixed (ECB 512 MiB
+ * +3%, 1 GiB -13% on one box; CBC-dec 512 MiB -2%, 1 GiB +2%) and at 256 MiB
+ * it loses 2-11%: each of the 4096 T-table waves then gets only one or two
+ * 32 KiB units, and 256 x 128 KiB of LDS table fills plus the fork / join
+ * are a fixed cost.  (Round 4's 896 MiB was measured while the halves ran one
+ * after the other: docs/PERF.md round 5.) */
 size_t split_min(int) { return (size_t)2 << 30; }
 
 int pick_ecb_impl(int impl, int bits, size_t nbytes)
@@ -460,19 +462,21 @@ thread_local int g_last_impl = OTC_IMPL_AUTO;
 
 /* Segment ENCRYPTION (CBC / CFB128, one serial chain per segment).  Three
  * forms: the grid T-table kernel; the persistent T-table claim kernel alone
- * (64-segment units from one counter, no bitsliced half); and the
- * co-resident split with the row-sliced bs8 kernel (aes_bs8.hip) taking
- * 8-unit tasks from the front.  The split is explicit only (impl "split" /
- * "bitslice"): measured with the kernels truly co-resident it LOSES at every
- * size -- a bs8 wave beside four T-table waves runs a 512-chain task at
- * ~0.06 GB/s, slows the latency-bound T-table chains by up to 30%, and its
- * 8-unit tasks outlast the whole call at 4 KiB segments (CBC-enc-seg-256 4
- * GiB: 738 vs 988 GB/s; 512 B: 983 vs 1027; profiles/r5/seg_split/).  auto
- * runs the T-table: the persistent kernel for segments <= 1 KiB in calls >=
- * 4 GiB (+1-7% over the grid kernel), the grid kernel otherwise (at 4 KiB
- * segments the two tie within box noise, and below 4 GiB the grid kernel
- * wins).  bs8 needs segments of < 8 MiB (32-bit lane offsets); at least 16
- * units (1024 segments) to claim. */
+ * (64-segment units from one counter, one workgroup per CU, no bitsliced
+ * half); and the co-resident split with the row-sliced bs8 kernel
+ * (aes_bs8.hip) taking 8-unit tasks from the front.  The bs8 split is
+ * explicit only (impl "split" / "bitslice"): truly co-resident it LOSES at
+ * every size -- a bs8 wave beside four T-table waves runs its 512-chain task
+ * slowly, slows the latency-bound T-table chains, and its 8-unit tasks
+ * outlast a 4 KiB-segment call (AES-256 4 GiB: 775 vs 1040 GB/s for the
+ * claim kernel alone; profiles/r5/split_ab/remeasure_int_lds.jsonl).  auto
+ * runs the T-table: the persistent kernel from 2 GiB (from 1 GiB for
+ * segments <= 1 KiB), where it beats the grid kernel by 4-15% (AES-256 4 KiB
+ * segments: 2 GiB 1027 vs 986, 4 GiB 1040 vs 969, 32 GiB 1142 vs 995; 512 B
+ * at 1 GiB 986 vs 951; AES-128 4 GiB 1383 vs 1267), the grid kernel below
+ * (1 GiB of 4 KiB segments: 916 vs 948; profiles/r5/split_thresholds/).
+ * bs8 needs segments of < 8 MiB (32-bit lane offsets); at least 16 units
+ * (1024 segments) to claim. */
 constexpr uint64_t SEG_UNIT = 64;
 bool segenc_bs8_ok(size_t seg_bytes) { return seg_bytes >= 16 && seg_bytes * SEG_UNIT * 8 <= 0xFFFFFFFFull; }
 
@@ -486,7 +490,8 @@ int pick_segenc_impl(int impl, size_t, size_t seg_bytes)
 
 bool segenc_persistent(size_t nbytes, size_t seg_bytes, size_t nseg)
 {
-    return seg_bytes <= 1024 && nbytes >= ((size_t)4 << 30) && nseg / SEG_UNIT >= 16 && nseg / SEG_UNIT <= 0x7FFFFFFFull;
+    const size_t min_bytes = seg_bytes <= 1024 ? ((size_t)1 << 30) : ((size_t)2 << 30);
+    return nbytes >= min_bytes && nseg / SEG_UNIT >= 16 && nseg / SEG_UNIT <= 0x7FFFFFFFull;
 }
 
 hipError_t seg_enc_run(bool cfb, const void *in, void *out, size_t seg_bytes, size_t nseg, const otc_aes_key &K,
