@@ -316,7 +316,9 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
     }
     int dev = 0;
     AuxStream a;
-    if (hipGetDevice(&dev) != hipSuccess || aux_take(dev, a) != hipSuccess) {
+    /* bs_wgs 0 (and not bs_only): the T-table claim kernel alone, no fork */
+    const bool fork = bs_wgs != 0 || bs_only;
+    if (fork && (hipGetDevice(&dev) != hipSuccess || aux_take(dev, a) != hipSuccess)) {
         /* no auxiliary stream: the T-table alone still gives the output */
         (void)hipGetLastError();
         (void)hipFreeAsync(ctr, st);
@@ -330,16 +332,16 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
      * queued on st */
     if ((e = hipMemsetAsync(ctr, 0, sizeof *ctr, st)) == hipSuccess &&
         (e = hipMemsetAsync(ctr + 1, bs_only ? 0xFF : 0, sizeof *ctr, st)) == hipSuccess &&
-        (e = hipEventRecord(a.fork, st)) == hipSuccess && (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess &&
+        (!fork || ((e = hipEventRecord(a.fork, st)) == hipSuccess && (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess)) &&
         (e = tt(cl_tt)) == hipSuccess) {
         /* the bitsliced half failing (no memory for its key table) leaves the
          * T-table claim kernel to take every unit -- unless it was told to
          * take none (bs_only): then the T-table alone redoes the call.  The
          * join is recorded either way (a failure after its launch must still
          * be waited for). */
-        const hipError_t eb = bs_wgs ? bs(cl, a.s) : hipSuccess; /* 0: the T-table claim kernel alone */
+        const hipError_t eb = bs_wgs ? bs(cl, a.s) : hipSuccess;
         if (eb != hipSuccess) (void)hipGetLastError();
-        if ((e = hipEventRecord(a.join, a.s)) == hipSuccess) e = hipStreamWaitEvent(st, a.join, 0);
+        if (fork && (e = hipEventRecord(a.join, a.s)) == hipSuccess) e = hipStreamWaitEvent(st, a.join, 0);
         if (e == hipSuccess) {
             if (eb == hipSuccess && bs_wgs) *ran = bs_only ? OTC_IMPL_BITSLICE : OTC_IMPL_SPLIT;
             else if (bs_only) e = plain();
@@ -366,12 +368,12 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
                     g_split_ttwaves = bs_only ? 0 : 16ull * (uint64_t)otc_dev::device_cus();
                 }
             }
-        } else {
+        } else if (fork) {
             (void)hipStreamSynchronize(a.s); /* no join on st: the counter must outlive the bitsliced kernel */
         }
     }
     const hipError_t f = hipFreeAsync(ctr, st); /* after the join: both kernels are done with it */
-    aux_give(a); /* reusable as soon as the work is enqueued: stream order */
+    if (fork) aux_give(a); /* reusable as soon as the work is enqueued: stream order */
     return e != hipSuccess ? e : f;
 }
 
