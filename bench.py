@@ -399,16 +399,20 @@ def main():
 
     extra = {}
     if not args.no_other and not cpu:
-        # the other AES-128 CTR kernel on the same shard, same protocol: the
-        # headline's "auto" runs the bitsliced VALU kernel at this size (BASELINE
-        # config 3 names it), the LDS T-table kernel is timed beside it
-        other = "ttable" if resolved == "bitslice" else "bitslice"
-        name = "ttable" if other == "ttable" else "bitsliced"
-        v_ok = pdist.allreduce_max(0.0 if verify_once(key, other) else 1.0) == 0.0
-        o_steps = max(1, min(args.steps, 5))
-        el_o, _, _ = timed(o_steps, key, impl=other)
-        extra[name + "_ctr_gbps_whole_node"] = round(nbytes * world * o_steps / el_o / 1e9, 3)
-        extra[name + "_ctr_verified"] = v_ok
+        # the other AES-128 CTR kernels on the same shard, same protocol: the
+        # headline's "auto" runs the co-resident split at this size (round 5;
+        # the bitsliced VALU kernel alone before), and each single kernel --
+        # the bitsliced one BASELINE config 3 names, the LDS T-table -- is
+        # timed beside it
+        for other in ("bitslice", "ttable"):
+            if other == resolved:
+                continue
+            name = "ttable" if other == "ttable" else "bitsliced"
+            v_ok = pdist.allreduce_max(0.0 if verify_once(key, other) else 1.0) == 0.0
+            o_steps = max(1, min(args.steps, 5))
+            el_o, _, _ = timed(o_steps, key, impl=other)
+            extra[name + "_ctr_gbps_whole_node"] = round(nbytes * world * o_steps / el_o / 1e9, 3)
+            extra[name + "_ctr_verified"] = v_ok
     if not args.no_aes256:
         v_ok = pdist.allreduce_max(0.0 if verify_once(key256) else 1.0) == 0.0
         k256_steps = max(1, min(args.steps, 5))

@@ -258,19 +258,20 @@ __device__ __forceinline__ void st16(uint8_t *p, uint64_t blk, uint4 v)
 {
     *reinterpret_cast<uint4 *>(p + 16 * blk) = v;
 }
-enum : int { E_ECB = 0, E_CFB_DEC = 2, E_CFB_DEC_SEG = 3 };
+enum : int { E_ECB = 0, E_CFB_DEC = 2, E_CFB_DEC_SEG = 3, E_CTR = 4 };
 enum : int { D_ECB = 0, D_CBC = 1, D_CBC_SEG = 2 };
 
 struct EncParams {
     const uint8_t *in;
     uint8_t *out;
     uint64_t nfull;   /* full 16-byte blocks */
-    Ctr128 ctr;       /* CFB_DEC_SEG: IV of segment 0 (IV_s = ctr + s) */
+    Ctr128 ctr;       /* CFB_DEC_SEG: IV of segment 0 (IV_s = ctr + s); CTR: the counter of block 0 */
     uint32_t iv[4];   /* CFB: IV as LE words */
     uint64_t seg_blocks; /* CFB_DEC_SEG: blocks per segment */
     uint32_t seg_shift;  /* CFB_DEC_SEG: log2(seg_blocks), or 64 if not a power of two */
-    uint32_t pad2;
+    uint32_t wrap64;     /* CTR: 64-bit counter increment */
     SplitClaim cl;       /* CLAIM kernels: units taken from the back of the buffer */
+    uint64_t head;       /* CLAIM: unit u is blocks head + u * 2048 (CTR: the bitsliced kernel's task grid) */
 };
 
 struct DecParams {
@@ -334,15 +335,18 @@ __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_ke
     tbl4_lane_consts(lane, lk);
     constexpr uint64_t PER = (uint64_t)THREADS * B;
 
-    /* B blocks per lane: i0 + 64 b, b < B; `full`: all in range (wave-uniform) */
-    auto chunk = [&](uint64_t i0, bool full) {
+    /* B blocks per lane: i0 + 64 b, b < B; `full`: all below lim (wave-uniform) */
+    auto chunk = [&](uint64_t i0, bool full, uint64_t lim) {
         uint32_t s[B][4];
         uint4 x[B];
 #pragma unroll
         for (int b = 0; b < B; ++b) {
             const uint64_t i = i0 + 64u * b;
-            const bool ok = full || i < P.nfull;
-            if (MODE == E_ECB) {
+            const bool ok = full || i < lim;
+            if (MODE == E_CTR) {
+                x[b] = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
+                ctr_words(P.ctr, i, P.wrap64 != 0, s[b][0], s[b][1], s[b][2], s[b][3]);
+            } else if (MODE == E_ECB) {
                 uint4 v = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
                 s[b][0] = v.x; s[b][1] = v.y; s[b][2] = v.z; s[b][3] = v.w;
             } else if (MODE == E_CFB_DEC) { /* cipher input is the previous ciphertext */
@@ -375,25 +379,31 @@ __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_ke
             } else {
                 o = make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]);
             }
-            if (full || i < P.nfull) st16(P.out, i, o);
+            if (full || i < lim) st16(P.out, i, o);
         }
     };
 
     if constexpr (CLAIM) {
         strace(1);
-        const uint64_t done = (uint64_t)P.cl.nunits * CLAIM_UNIT; /* the rest: workgroup 0, first */
-        if (blockIdx.x == 0)
-            for (uint64_t base = done; base < P.nfull; base += PER) chunk(base + (uint64_t)wave * 64u * B + lane, false);
+        /* the blocks outside the units -- [0, head) and past the last one --
+         * workgroup 0, first */
+        const uint64_t done = P.head + (uint64_t)P.cl.nunits * CLAIM_UNIT;
+        if (blockIdx.x == 0) {
+            for (uint64_t base = 0; base < P.head; base += PER) chunk(base + (uint64_t)wave * 64u * B + lane, false, P.head);
+            for (uint64_t base = done; base < P.nfull; base += PER)
+                chunk(base + (uint64_t)wave * 64u * B + lane, false, P.nfull);
+        }
         for (;;) {
             const int64_t u = claim_unit(P.cl, true);
             if (u < 0) break;
+            const uint64_t u0 = P.head + (uint64_t)u * CLAIM_UNIT;
 #pragma unroll 1
-            for (uint32_t it = 0; it < CLAIM_UNIT / (64u * B); ++it) chunk((uint64_t)u * CLAIM_UNIT + it * 64u * B + lane, true);
+            for (uint32_t it = 0; it < CLAIM_UNIT / (64u * B); ++it) chunk(u0 + it * 64u * B + lane, true, 0);
         }
         return;
     }
     for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nfull; base += (uint64_t)gridDim.x * PER)
-        chunk(base + (uint64_t)wave * 64u * B + lane, base + PER <= P.nfull);
+        chunk(base + (uint64_t)wave * 64u * B + lane, base + PER <= P.nfull, P.nfull);
 }
 
 template <int NR, int MODE, int B, int THREADS>
@@ -424,6 +434,13 @@ template <int NR>
 __global__ __launch_bounds__(1024) void k_aes_cfb_tt_claim(EncParams P, otc_aes_key K)
 {
     enc_tt_body<NR, E_CFB_DEC, OTC_TT_CLAIM_B, 1024, true>(P, K);
+}
+/* CTR beside the bitsliced CTR claim kernel (counter caching on that side,
+ * 32 KiB of LDS staging: 128 + 32 KiB fill the CU) */
+template <int NR>
+__global__ __launch_bounds__(1024) void k_aes_ctr_tt_claim(EncParams P, otc_aes_key K)
+{
+    enc_tt_body<NR, E_CTR, OTC_TT_CLAIM_B, 1024, true>(P, K);
 }
 template <int NR>
 __global__ __launch_bounds__(1024) void k_aes_cfbseg_tt_claim(EncParams P, otc_aes_key K)
@@ -1206,6 +1223,7 @@ hipError_t launch_enc_claim(const EncParams &P, const otc_aes_key &K, hipStream_
     auto go = [&](auto nr) {
         constexpr int NR = decltype(nr)::value;
         if constexpr (MODE == E_ECB) return launch_dyn<k_aes_ecb_tt_claim<NR>>(g, b, ENC_LDS, st, P, K);
+        else if constexpr (MODE == E_CTR) return launch_dyn<k_aes_ctr_tt_claim<NR>>(g, b, ENC_LDS, st, P, K);
         else if constexpr (MODE == E_CFB_DEC) return launch_dyn<k_aes_cfb_tt_claim<NR>>(g, b, ENC_LDS, st, P, K);
         else return launch_dyn<k_aes_cfbseg_tt_claim<NR>>(g, b, ENC_LDS, st, P, K);
     };
@@ -1376,6 +1394,22 @@ hipError_t tt_ecb_encrypt_claim(const void *in, void *out, uint64_t nblocks, con
     P.nfull = nblocks;
     P.cl = cl;
     return launch_enc_claim<E_ECB>(P, K, st);
+}
+
+/* the T-table half of the CTR split: units of 2048 blocks from `head`
+ * (the bitsliced kernel's full tasks), the blocks outside them in workgroup 0 */
+hipError_t tt_ctr_claim(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, Ctr128 c, bool wrap64,
+                        uint64_t head, SplitClaim cl, hipStream_t st)
+{
+    EncParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nblocks;
+    P.ctr = c;
+    P.wrap64 = wrap64 ? 1u : 0u;
+    P.head = head;
+    P.cl = cl;
+    return launch_enc_claim<E_CTR>(P, K, st);
 }
 
 hipError_t tt_cfb_decrypt_claim(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K,

@@ -435,14 +435,17 @@ def test_bitslice_launch_structures(gpu, bits):
 def test_auto_routing_rule(gpu):
     """impl="auto" by size (docs/PERF.md, profiles/r3/auto_impl,
     profiles/r4/ecb_split): bitsliced CTR from 2 GiB (AES-128/192) or 1 GiB
-    (AES-256), the co-resident split for ECB encryption from 2 GiB (round 5,
+    (AES-256) and the CTR split from 8 / 4 / 1 GiB (AES-128 / 192 / 256,
+    profiles/r5/ctr_split), the co-resident split for ECB encryption from 2 GiB (round 5,
     measured with the halves truly co-resident), T-table for everything else;
-    the boundaries are exact.  "split" is an
-    ECB-encryption form: for CTR it routes as auto."""
+    the boundaries are exact.  "split" is explicit for both
+    (CTR: the co-resident T-table + bitsliced CTR claim kernels)."""
     G = 1 << 30
-    cases = [(128, "ctr", 64 * G, "bitslice"), (128, "ctr", 2 * G - 16, "ttable"), (128, "ctr", 2 * G, "bitslice"),
-             (256, "ctr", 1 * G, "bitslice"), (256, "ctr", 1 * G - 16, "ttable"), (256, "ctr", 4 * G, "bitslice"),
+    cases = [(128, "ctr", 64 * G, "split"), (128, "ctr", 2 * G - 16, "ttable"), (128, "ctr", 2 * G, "bitslice"),
+             (128, "ctr", 8 * G - 16, "bitslice"), (128, "ctr", 8 * G, "split"),
+             (256, "ctr", 1 * G, "split"), (256, "ctr", 1 * G - 16, "ttable"), (256, "ctr", 4 * G, "split"),
              (192, "ctr", 2 * G, "bitslice"), (192, "ctr", 2 * G - 16, "ttable"), (192, "ctr", 1 * G, "ttable"),
+             (192, "ctr", 4 * G, "split"), (192, "ctr", 4 * G - 16, "bitslice"),
              (256, "ecb", 64 * G, "split"), (128, "ecb", 2 * G, "split"), (192, "ecb", 2 * G - 16, "ttable"),
              (256, "ecb", 1 * G, "ttable"),
              (128, "ctr", 16, "ttable")]
@@ -450,7 +453,7 @@ def test_auto_routing_rule(gpu):
         assert ops.pick_impl("auto", bits, mode, n) == want, (bits, mode, n)
         assert ops.pick_impl("ttable", bits, mode, n) == "ttable"
         assert ops.pick_impl("bitslice", bits, mode, n) == "bitslice"
-        assert ops.pick_impl("split", bits, mode, n) == ("split" if mode == "ecb" else want)
+        assert ops.pick_impl("split", bits, mode, n) == "split"
     with pytest.raises(ValueError):
         ops.pick_impl("hybrid")
 
@@ -583,6 +586,36 @@ def test_segment_encrypt_persistent_ttable(gpu, seg):
         assert torch.equal(x, y), (name, seg, "in place")
         del y
         ops.fill_random_(x, seed=seg)
+
+
+@pytest.mark.parametrize("bits", [128, 256])
+def test_ctr_split_matches_oracle(gpu, bits):
+    """CTR as a co-resident split (bitsliced CTR claim kernel with counter
+    caching + T-table CTR claim kernel, engine.cpp ctr_split): equal to the
+    bitsliced kernel alone and to the oracle, for counters that start a task
+    and that do not (the T-table's workgroup 0 runs the partial first and last
+    task), a trailing partial block, a carry out of the low 64 bits, in place;
+    under two full tasks the T-table runs alone."""
+    key = os.urandom(bits // 8)
+    for n, ctr in ((16 * 2048 * 7, bytes(16)),
+                   (16 * 2048 * 9 + 16 * 37 + 5, os.urandom(8) + (2**64 - 2048 * 3 - 100).to_bytes(8, "big")),
+                   (16 * 2048 * 64 + 48, os.urandom(16)),
+                   (16 * 2048 * 2 + 16, os.urandom(16))):
+        x = torch.empty(n, dtype=torch.uint8, device=gpu)
+        ops.fill_random_(x, seed=n ^ bits)
+        b = ops.ctr(x, key, ctr, impl="bitslice")
+        y = ops.ctr(x, key, ctr, impl="split")
+        shift, nb = int.from_bytes(ctr, "big") & 2047, n // 16
+        nunits = (nb + shift) // 2048 - (1 if shift else 0)
+        assert ops.last_impl() == ("split" if nunits >= 2 else "ttable"), (n, shift, ops.last_impl())
+        w = x.clone()
+        ops.ctr(w, key, ctr, out=w, impl="split")
+        torch.cuda.synchronize()
+        assert torch.equal(y, b), (bits, n)
+        assert torch.equal(w, b), (bits, n, "in place")
+        S = 1 << 13
+        for off in (0, (n // 3) & ~15, (n - S) & ~15, n - n % 16 - 16):
+            assert host(y[off:off + S]) == cpu_ref.ctr(key, sh.ctr_add(ctr, off // 16), host(x[off:off + S])), (n, off)
 
 
 def test_ecb_split_stream_order(gpu):
