@@ -660,17 +660,18 @@ def test_split_concurrent_calls(gpu):
             assert torch.equal(y, f(x, "ttable"))
 
 
-@pytest.mark.parametrize("bits,n", [(128, (2 << 30) + 3), (192, (2 << 30) + 3), (256, (1 << 30) + 3)])
-def test_ctr_auto_large_bitsliced(gpu, bits, n):
-    """impl="auto" sends bulk AES CTR to the bitsliced kernel (the
-    measured winner there; the call must actually run it): head, a middle
-    window and the tail against the oracle, and equal to the forced T-table
-    output."""
+@pytest.mark.parametrize("bits,n,want", [(128, (2 << 30) + 3, "bitslice"), (192, (2 << 30) + 3, "bitslice"),
+                                         (256, (1 << 30) + 3, "split"), (192, (4 << 30) + 3, "split")])
+def test_ctr_auto_large_bitsliced(gpu, bits, n, want):
+    """impl="auto" sends bulk AES CTR to the bitsliced kernel, and larger
+    calls to the co-resident CTR split (the measured winners there; the call
+    must actually run them): head, a middle window and the tail against the
+    oracle, and equal to the forced T-table output."""
     key, ctr0 = os.urandom(bits // 8), os.urandom(8) + (2**64 - 12345).to_bytes(8, "big")
     x = torch.empty(n, dtype=torch.uint8, device=gpu)
     ops.fill_random_(x, seed=bits)
     y = ops.ctr(x, key, ctr0, impl="auto")
-    assert ops.last_impl() == "bitslice"
+    assert ops.last_impl() == want
     t = ops.ctr(x, key, ctr0, impl="ttable")
     assert ops.last_impl() == "ttable"
     torch.cuda.synchronize()
