@@ -160,8 +160,7 @@ using namespace otc_rt;
 namespace {
 
 /* OTC_IMPL_AUTO: the measured winner (docs/PERF.md).  CTR calls of >= 2 GiB
- * (AES-256: >= 1 GiB) run bitsliced, and from 8 GiB (AES-192: 4, AES-256: 1)
- * as the co-resident CTR split, the thresholds below; smaller CTR calls
+ * (AES-256: >= 1 GiB) run bitsliced, the thresholds below; smaller CTR calls
  * (the bitsliced grid needs ~768 workgroups to fill the chip, plus two table
  * kernels per call) take the T-table.  ECB, CBC / CFB decryption: the
  * co-resident split (split_claim below) from split_min() bytes, the T-table
@@ -192,15 +191,13 @@ int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
     /* measured crossover (profiles/r3/auto_impl/xover_after_round2_tables):
      * AES-128 2 GiB 1520 vs 1506 GB/s, 1 GiB 1353 vs 1360; AES-256 1 GiB
      * 1056 vs 1049.  AES-192 takes the AES-128 threshold (not measured at
-     * 1 GiB; its margin lies between the two).  From there the bitsliced
-     * kernel alone, and from min_split the co-resident CTR split (ctr_split),
-     * which beats it at every size measured above those (round 5,
-     * profiles/r5/ctr_split/thresholds_ab.jsonl, prepared_tables_ab.jsonl):
-     * AES-128 8 GiB +1%, 16-64 GiB +1.3-1.9% (4 GiB: even); AES-192 4 GiB
-     * +3%, 64 GiB +3.4%; AES-256 1 GiB +1-2%, 2 GiB +3%, 4 and 64 GiB +4.4%. */
+     * 1 GiB; its margin lies between the two).  The co-resident CTR split
+     * (ctr_split, impl "split") is not routed: it beat the bitsliced kernel
+     * by 1-4% in otbench (profiles/r5/ctr_split/thresholds_ab.jsonl) but
+     * lost to it inside a process with torch's and RCCL's streams -- bench.py
+     * 1534-1607 vs 1688 GB/s (bench_with_ctr_split*.json) -- whether its
+     * halves share pooled hardware queues or run on CU-masked ones. */
     const size_t min_bs = bits == 256 ? ((size_t)1 << 30) : ((size_t)2 << 30);
-    const size_t min_split = bits == 128 ? ((size_t)8 << 30) : bits == 192 ? ((size_t)4 << 30) : ((size_t)1 << 30);
-    if (ctr_bytes >= min_split) return OTC_IMPL_SPLIT;
     return ctr_bytes >= min_bs ? OTC_IMPL_BITSLICE : OTC_IMPL_TTABLE;
 }
 
@@ -218,9 +215,9 @@ int check_impl(int impl)
  * the VALU-bound bitsliced kernels hold the ~1.37 kW cap (profiles/r4/power).
  * A T-table workgroup (1024 threads = 4 waves per SIMD at 78-85 VGPRs, 128 or
  * 160 KiB LDS) leaves room for one bitsliced wave per SIMD (152-168 VGPRs, no
- * LDS).  So both kernels run at once on every CU over ONE buffer -- the
- * T-table on the caller's stream, the bitsliced kernel on a pooled auxiliary
- * stream (fork / join events) -- and take 2048-block units from a shared
+ * LDS).  So both kernels run at once on every CU over ONE buffer -- each on
+ * a pooled CU-masked stream with a hardware queue of its own (fork / join
+ * events with the caller's stream, aux_take) -- and take 2048-block units from a shared
  * counter, the bitsliced kernel from the front and the T-table from the back
  * (otc_device.h SplitClaim), so they finish together on any box: no share to
  * tune, no tail where one kernel runs alone.  Measured: docs/PERF.md
@@ -228,8 +225,8 @@ int check_impl(int impl)
  * dec_split, cfb_split). */
 struct AuxStream {
     int dev = -1;
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t s = nullptr, t = nullptr; /* the bitsliced / the T-table half */
+    hipEvent_t fork = nullptr, join = nullptr, join_t = nullptr;
 };
 
 /* pooled per device: a call takes one (creating it on first use), enqueues,
@@ -251,12 +248,23 @@ hipError_t aux_take(int dev, AuxStream &out)
     }
     AuxStream a;
     a.dev = dev;
-    hipError_t e = hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking);
+    /* both halves on streams with an all-CU mask: HIP gives a CU-masked
+     * stream a hardware queue of its own.  On pooled queues (4 per process
+     * here) a library stream can share one with the caller's stream or with
+     * the other half, and then the two kernels run one after the other: in
+     * bench.py, beside torch's and RCCL's streams, the CTR split ran at the
+     * T-table's speed (1534 GB/s) */
+    std::vector<uint32_t> mask((size_t)(otc_dev::device_cus() + 31) / 32, 0xFFFFFFFFu);
+    hipError_t e = hipExtStreamCreateWithCUMask(&a.s, (uint32_t)mask.size(), mask.data());
+    if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&a.t, (uint32_t)mask.size(), mask.data());
     if (e == hipSuccess) e = hipEventCreateWithFlags(&a.fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&a.join, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&a.join_t, hipEventDisableTiming);
     if (e != hipSuccess) {
+        if (a.join_t) (void)hipEventDestroy(a.join_t);
         if (a.join) (void)hipEventDestroy(a.join);
         if (a.fork) (void)hipEventDestroy(a.fork);
+        if (a.t) (void)hipStreamDestroy(a.t);
         if (a.s) (void)hipStreamDestroy(a.s);
         return e;
     }
@@ -344,8 +352,9 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
      * queued on st */
     if ((e = hipMemsetAsync(ctr, 0, sizeof *ctr, st)) == hipSuccess &&
         (e = hipMemsetAsync(ctr + 1, bs_only ? 0xFF : 0, sizeof *ctr, st)) == hipSuccess &&
-        (!fork || ((e = hipEventRecord(a.fork, st)) == hipSuccess && (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess)) &&
-        (e = tt(cl_tt)) == hipSuccess) {
+        (!fork || ((e = hipEventRecord(a.fork, st)) == hipSuccess && (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess &&
+                   (e = hipStreamWaitEvent(a.t, a.fork, 0)) == hipSuccess)) &&
+        (e = tt(cl_tt, fork ? a.t : st)) == hipSuccess) {
         /* the bitsliced half failing (no memory for its key table) leaves the
          * T-table claim kernel to take every unit -- unless it was told to
          * take none (bs_only): then the T-table alone redoes the call.  The
@@ -353,7 +362,9 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
          * be waited for). */
         const hipError_t eb = bs_wgs ? bs(cl, a.s) : hipSuccess;
         if (eb != hipSuccess) (void)hipGetLastError();
-        if (fork && (e = hipEventRecord(a.join, a.s)) == hipSuccess) e = hipStreamWaitEvent(st, a.join, 0);
+        if (fork && (e = hipEventRecord(a.join, a.s)) == hipSuccess && (e = hipEventRecord(a.join_t, a.t)) == hipSuccess &&
+            (e = hipStreamWaitEvent(st, a.join, 0)) == hipSuccess)
+            e = hipStreamWaitEvent(st, a.join_t, 0);
         if (e == hipSuccess) {
             if (eb == hipSuccess && bs_wgs) *ran = bs_only ? OTC_IMPL_BITSLICE : OTC_IMPL_SPLIT;
             else if (bs_only) e = plain();
@@ -381,7 +392,9 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
                 }
             }
         } else if (fork) {
-            (void)hipStreamSynchronize(a.s); /* no join on st: the counter must outlive the bitsliced kernel */
+            /* no join on st: the counter must outlive both kernels */
+            (void)hipStreamSynchronize(a.s);
+            (void)hipStreamSynchronize(a.t);
         }
     }
     const hipError_t f = hipFreeAsync(ctr, st); /* after the join: both kernels are done with it */
@@ -400,12 +413,12 @@ hipError_t ecb_split(const void *in, void *out, uint64_t nblocks, const otc_aes_
     if (K.dir == OTC_DIR_ENCRYPT)
         return split_claim(
             nunits, 2, bs_only, bs_wgs_for(bs_only), st, ran,
-            [&](SplitClaim cl) { return otc_impl::tt_ecb_encrypt_claim(in, out, nblocks, K, cl, st); },
+            [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_ecb_encrypt_claim(in, out, nblocks, K, cl, ts); },
             [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_ECB, in, out, nblocks, K, nullptr, cl, s); },
             [&]() { return otc_impl::tt_ecb_encrypt(in, out, nblocks, K, st); });
     return split_claim(
         nunits, 2, bs_only, bs_wgs_for(bs_only), st, ran,
-        [&](SplitClaim cl) { return otc_impl::tt_ecb_decrypt_claim(in, out, nblocks, K, cl, st); },
+        [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_ecb_decrypt_claim(in, out, nblocks, K, cl, ts); },
         [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_ECB_DEC, in, out, nblocks, K, nullptr, cl, s); },
         [&]() { return otc_impl::tt_ecb_decrypt(in, out, nblocks, K, st); });
 }
@@ -418,7 +431,7 @@ hipError_t cbc_dec_split(const void *in, void *out, uint64_t nblocks, const otc_
     const Ctr128 ivc = ctr_from_bytes(iv);
     return split_claim(
         nblocks / otc_dev::CLAIM_UNIT, 2, bs_only, bs_wgs_for(bs_only), st, ran,
-        [&](SplitClaim cl) { return otc_impl::tt_cbc_decrypt_claim(in, out, nblocks, K, ivc, cl, st); },
+        [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_cbc_decrypt_claim(in, out, nblocks, K, ivc, cl, ts); },
         [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_CBC_DEC, in, out, nblocks, K, ivw, cl, s); },
         [&]() { return otc_impl::tt_cbc_decrypt(in, out, nblocks, K, ivc, st); });
 }
@@ -428,7 +441,7 @@ hipError_t cfb_dec_split(const void *in, void *out, uint64_t nblocks, const otc_
 {
     return split_claim(
         nblocks / otc_dev::CLAIM_UNIT, 2, bs_only, bs_wgs_for(bs_only), st, ran,
-        [&](SplitClaim cl) { return otc_impl::tt_cfb_decrypt_claim(in, out, nblocks, K, ivw, cl, st); },
+        [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_cfb_decrypt_claim(in, out, nblocks, K, ivw, cl, ts); },
         [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_CFB_DEC, in, out, nblocks, K, ivw, cl, s); },
         [&]() { return otc_impl::tt_cfb_decrypt(in, out, nblocks, K, ivw, st); });
 }
@@ -466,7 +479,7 @@ hipError_t ctr_split(const void *in, void *out, size_t nbytes, const otc_aes_key
     bool used = false;
     const hipError_t e = split_claim(
         nunits, 2, false, bs_wgs_for(false), st, ran,
-        [&](SplitClaim cl) { return otc_impl::tt_ctr_claim(in, out, nblocks, K, c, wrap64, head, cl, st); },
+        [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_ctr_claim(in, out, nblocks, K, c, wrap64, head, cl, ts); },
         [&](SplitClaim cl, hipStream_t s) {
             used = true;
             return otc_impl::bs_ctr_claim(in, out, nblocks, K, c, wrap64, &pre, cl, s);
@@ -504,9 +517,9 @@ hipError_t seg_dec_split(bool cfb, const void *in, void *out, size_t seg_blocks,
     };
     return split_claim(
         nblocks / otc_dev::CLAIM_UNIT, 2, bs_only, bs_wgs_for(bs_only), st, ran,
-        [&](SplitClaim cl) {
-            return cfb ? otc_impl::tt_cfb_decrypt_seg_claim(in, out, nblocks, K, iv0, sh, cl, st)
-                       : otc_impl::tt_cbc_decrypt_seg_claim(in, out, nblocks, K, iv0, sh, cl, st);
+        [&](SplitClaim cl, hipStream_t ts) {
+            return cfb ? otc_impl::tt_cfb_decrypt_seg_claim(in, out, nblocks, K, iv0, sh, cl, ts)
+                       : otc_impl::tt_cbc_decrypt_seg_claim(in, out, nblocks, K, iv0, sh, cl, ts);
         },
         [&](SplitClaim cl, hipStream_t s) {
             return otc_impl::bs_claim_seg(cfb ? BS_CFB_DEC_SEG : BS_CBC_DEC_SEG, in, out, nblocks, K, iv0, sh, cl, s);
@@ -567,7 +580,7 @@ hipError_t seg_enc_run(bool cfb, const void *in, void *out, size_t seg_bytes, si
     const unsigned bs_wgs = persistent ? 0u : (unsigned)otc_dev::device_cus() * (bs_only ? 4u : 1u);
     return split_claim(
         nseg / SEG_UNIT, 16, bs_only, bs_wgs, st, &g_last_impl,
-        [&](SplitClaim cl) { return otc_impl::tt_seg_encrypt_claim(cfb, in, out, seg_blocks, nseg, K, iv0, cl, st); },
+        [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_seg_encrypt_claim(cfb, in, out, seg_blocks, nseg, K, iv0, cl, ts); },
         [&](SplitClaim cl, hipStream_t s) {
             return otc_impl::bs8_seg_encrypt_claim(cfb, in, out, seg_blocks, K, iv0, cl, s);
         },

@@ -177,6 +177,8 @@ def _declare_gpu(lib):
         "otc_last_error": (ctypes.c_char_p, []),
         "otc_pick_impl": (c_int, [c_int, c_int, c_int, c_u64]),
         "otc_last_impl": (c_int, []),
+        "otc_split_stats": (None, [c_int]),
+        "otc_split_last_units": (c_int, [ctypes.POINTER(c_u64), ctypes.POINTER(c_u64), ctypes.POINTER(c_u64)]),
         "otc_aes_key_init": (c_int, [K, c_u8p, c_int, c_int]),
         "otc_aes_ecb": (c_int, [c_vp, c_vp, c_sz, K, c_int, c_vp]),
         "otc_aes_ctr": (c_int, [c_vp, c_vp, c_sz, K, c_u8p, c_u64, c_int, c_vp]),

@@ -435,17 +435,15 @@ def test_bitslice_launch_structures(gpu, bits):
 def test_auto_routing_rule(gpu):
     """impl="auto" by size (docs/PERF.md, profiles/r3/auto_impl,
     profiles/r4/ecb_split): bitsliced CTR from 2 GiB (AES-128/192) or 1 GiB
-    (AES-256) and the CTR split from 8 / 4 / 1 GiB (AES-128 / 192 / 256,
-    profiles/r5/ctr_split), the co-resident split for ECB encryption from 2 GiB (round 5,
+    (AES-256) -- the CTR split only on request (profiles/r5/ctr_split) --,
+    the co-resident split for ECB encryption from 2 GiB (round 5,
     measured with the halves truly co-resident), T-table for everything else;
     the boundaries are exact.  "split" is explicit for both
     (CTR: the co-resident T-table + bitsliced CTR claim kernels)."""
     G = 1 << 30
-    cases = [(128, "ctr", 64 * G, "split"), (128, "ctr", 2 * G - 16, "ttable"), (128, "ctr", 2 * G, "bitslice"),
-             (128, "ctr", 8 * G - 16, "bitslice"), (128, "ctr", 8 * G, "split"),
-             (256, "ctr", 1 * G, "split"), (256, "ctr", 1 * G - 16, "ttable"), (256, "ctr", 4 * G, "split"),
+    cases = [(128, "ctr", 64 * G, "bitslice"), (128, "ctr", 2 * G - 16, "ttable"), (128, "ctr", 2 * G, "bitslice"),
+             (256, "ctr", 1 * G, "bitslice"), (256, "ctr", 1 * G - 16, "ttable"), (256, "ctr", 4 * G, "bitslice"),
              (192, "ctr", 2 * G, "bitslice"), (192, "ctr", 2 * G - 16, "ttable"), (192, "ctr", 1 * G, "ttable"),
-             (192, "ctr", 4 * G, "split"), (192, "ctr", 4 * G - 16, "bitslice"),
              (256, "ecb", 64 * G, "split"), (128, "ecb", 2 * G, "split"), (192, "ecb", 2 * G - 16, "ttable"),
              (256, "ecb", 1 * G, "ttable"),
              (128, "ctr", 16, "ttable")]
@@ -661,12 +659,11 @@ def test_split_concurrent_calls(gpu):
 
 
 @pytest.mark.parametrize("bits,n,want", [(128, (2 << 30) + 3, "bitslice"), (192, (2 << 30) + 3, "bitslice"),
-                                         (256, (1 << 30) + 3, "split"), (192, (4 << 30) + 3, "split")])
+                                         (256, (1 << 30) + 3, "bitslice")])
 def test_ctr_auto_large_bitsliced(gpu, bits, n, want):
-    """impl="auto" sends bulk AES CTR to the bitsliced kernel, and larger
-    calls to the co-resident CTR split (the measured winners there; the call
-    must actually run them): head, a middle window and the tail against the
-    oracle, and equal to the forced T-table output."""
+    """impl="auto" sends bulk AES CTR to the bitsliced kernel (the measured
+    winner there; the call must actually run it): head, a middle window and
+    the tail against the oracle, and equal to the forced T-table output."""
     key, ctr0 = os.urandom(bits // 8), os.urandom(8) + (2**64 - 12345).to_bytes(8, "big")
     x = torch.empty(n, dtype=torch.uint8, device=gpu)
     ops.fill_random_(x, seed=bits)
