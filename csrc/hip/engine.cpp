@@ -402,45 +402,70 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
     return e != hipSuccess ? e : f;
 }
 
-/* bitsliced claim workgroups: one per CU beside the T-table (4 T-table waves
- * + 1 bitsliced wave per SIMD), three per CU alone (<= 168 VGPRs) */
-unsigned bs_wgs_for(bool bs_only) { return (unsigned)otc_dev::device_cus() * (bs_only ? 3u : 1u); }
+/* The claimed forms of ECB and the decryptions: the co-resident split, the
+ * bitsliced claim kernel alone (impl "bitslice"), or the persistent T-table
+ * claim kernel alone -- one workgroup per CU, its LDS table filled once,
+ * units claimed until none are left.  auto runs the last for the T-table
+ * calls of [896 MiB, 2 GiB): against the grid kernel ECB-256 1000 MiB 1089
+ * vs 1039, ECB-dec 1073 vs 966, CBC-dec 1049 vs 1017 (round 4's "split", which
+ * was this kernel alone: profiles/r4/claim_split/mid_sizes.jsonl); 1 GiB
+ * ECB-256 1026 vs 988, AES-128 1282 vs 1238 (profiles/r5/split_thresholds/);
+ * round 5 at 1000 MiB (midsize_persistent_vs_grid.jsonl, 2 reps): ECB-256
+ * 1068-1074 vs 1027-1031, ECB-dec-256 1053-1056 vs 872-911, CBC / CFB-dec
+ * +1%, ECB-128 +2-9%; 1.5 GiB -4..+7%; at 512 MiB and below it ties or
+ * loses. */
+enum { FORM_SPLIT = 0, FORM_BS = 1, FORM_TT = 2 };
+size_t tt_persistent_min() { return (size_t)896 << 20; }
+int split_form(int picked, size_t nbytes)
+{
+    if (picked == OTC_IMPL_SPLIT) return FORM_SPLIT;
+    if (picked == OTC_IMPL_BITSLICE) return FORM_BS;
+    return nbytes >= tt_persistent_min() ? FORM_TT : -1;
+}
 
-hipError_t ecb_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, bool bs_only, hipStream_t st,
+/* bitsliced claim workgroups: one per CU beside the T-table (4 T-table waves
+ * + 1 bitsliced wave per SIMD), three per CU alone (<= 168 VGPRs), none for
+ * the T-table alone */
+unsigned bs_wgs_for(int form)
+{
+    return form == FORM_TT ? 0u : (unsigned)otc_dev::device_cus() * (form == FORM_BS ? 3u : 1u);
+}
+
+hipError_t ecb_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, int form, hipStream_t st,
                      int *ran)
 {
     const uint64_t nunits = nblocks / otc_dev::CLAIM_UNIT;
     if (K.dir == OTC_DIR_ENCRYPT)
         return split_claim(
-            nunits, 2, bs_only, bs_wgs_for(bs_only), st, ran,
+            nunits, 2, form == FORM_BS, bs_wgs_for(form), st, ran,
             [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_ecb_encrypt_claim(in, out, nblocks, K, cl, ts); },
             [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_ECB, in, out, nblocks, K, nullptr, cl, s); },
             [&]() { return otc_impl::tt_ecb_encrypt(in, out, nblocks, K, st); });
     return split_claim(
-        nunits, 2, bs_only, bs_wgs_for(bs_only), st, ran,
+        nunits, 2, form == FORM_BS, bs_wgs_for(form), st, ran,
         [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_ecb_decrypt_claim(in, out, nblocks, K, cl, ts); },
         [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_ECB_DEC, in, out, nblocks, K, nullptr, cl, s); },
         [&]() { return otc_impl::tt_ecb_decrypt(in, out, nblocks, K, st); });
 }
 
 hipError_t cbc_dec_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, const uint8_t iv[16],
-                         bool bs_only, hipStream_t st, int *ran)
+                         int form, hipStream_t st, int *ran)
 {
     uint32_t ivw[4];
     memcpy(ivw, iv, 16); /* the bitsliced kernel's IV: LE words of the bytes */
     const Ctr128 ivc = ctr_from_bytes(iv);
     return split_claim(
-        nblocks / otc_dev::CLAIM_UNIT, 2, bs_only, bs_wgs_for(bs_only), st, ran,
+        nblocks / otc_dev::CLAIM_UNIT, 2, form == FORM_BS, bs_wgs_for(form), st, ran,
         [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_cbc_decrypt_claim(in, out, nblocks, K, ivc, cl, ts); },
         [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_CBC_DEC, in, out, nblocks, K, ivw, cl, s); },
         [&]() { return otc_impl::tt_cbc_decrypt(in, out, nblocks, K, ivc, st); });
 }
 
 hipError_t cfb_dec_split(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, const uint32_t ivw[4],
-                         bool bs_only, hipStream_t st, int *ran)
+                         int form, hipStream_t st, int *ran)
 {
     return split_claim(
-        nblocks / otc_dev::CLAIM_UNIT, 2, bs_only, bs_wgs_for(bs_only), st, ran,
+        nblocks / otc_dev::CLAIM_UNIT, 2, form == FORM_BS, bs_wgs_for(form), st, ran,
         [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_cfb_decrypt_claim(in, out, nblocks, K, ivw, cl, ts); },
         [&](SplitClaim cl, hipStream_t s) { return otc_impl::bs_claim(BS_CFB_DEC, in, out, nblocks, K, ivw, cl, s); },
         [&]() { return otc_impl::tt_cfb_decrypt(in, out, nblocks, K, ivw, st); });
@@ -478,7 +503,7 @@ hipError_t ctr_split(const void *in, void *out, size_t nbytes, const otc_aes_key
     }
     bool used = false;
     const hipError_t e = split_claim(
-        nunits, 2, false, bs_wgs_for(false), st, ran,
+        nunits, 2, false, bs_wgs_for(FORM_SPLIT), st, ran,
         [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_ctr_claim(in, out, nblocks, K, c, wrap64, head, cl, ts); },
         [&](SplitClaim cl, hipStream_t s) {
             used = true;
@@ -507,7 +532,7 @@ int pick_seg_impl(int impl, int bits, size_t nbytes, size_t seg_blocks)
 }
 
 hipError_t seg_dec_split(bool cfb, const void *in, void *out, size_t seg_blocks, size_t nseg, const otc_aes_key &K,
-                         Ctr128 iv0, bool bs_only, hipStream_t st, int *ran)
+                         Ctr128 iv0, int form, hipStream_t st, int *ran)
 {
     const uint64_t nblocks = (uint64_t)seg_blocks * nseg;
     const uint32_t sh = (uint32_t)seg_shift_of(seg_blocks);
@@ -516,7 +541,7 @@ hipError_t seg_dec_split(bool cfb, const void *in, void *out, size_t seg_blocks,
                    : otc_impl::tt_cbc_decrypt_seg(in, out, seg_blocks, nseg, K, iv0, st);
     };
     return split_claim(
-        nblocks / otc_dev::CLAIM_UNIT, 2, bs_only, bs_wgs_for(bs_only), st, ran,
+        nblocks / otc_dev::CLAIM_UNIT, 2, form == FORM_BS, bs_wgs_for(form), st, ran,
         [&](SplitClaim cl, hipStream_t ts) {
             return cfb ? otc_impl::tt_cfb_decrypt_seg_claim(in, out, nblocks, K, iv0, sh, cl, ts)
                        : otc_impl::tt_cbc_decrypt_seg_claim(in, out, nblocks, K, iv0, sh, cl, ts);
@@ -705,8 +730,8 @@ extern "C" int otc_aes_ecb(const void *in, void *out, size_t nbytes, const otc_a
     } else {
         g_last_impl = pick_dec_impl(impl, k->bits, nbytes);
     }
-    if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE)
-        e = ecb_split(in, out, nbytes / 16, *k, g_last_impl == OTC_IMPL_BITSLICE, st, &g_last_impl);
+    if (const int form = split_form(g_last_impl, nbytes); form >= 0)
+        e = ecb_split(in, out, nbytes / 16, *k, form, st, &g_last_impl);
     else if (k->dir == OTC_DIR_ENCRYPT)
         e = otc_impl::tt_ecb_encrypt(in, out, nbytes / 16, *k, st);
     else
@@ -874,8 +899,8 @@ extern "C" int otc_aes_cbc_decrypt_impl(const void *in, void *out, size_t nbytes
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     g_last_impl = pick_dec_impl(impl, k->bits, nbytes);
-    if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE) {
-        e = cbc_dec_split(in, out, nbytes / 16, *k, iv, g_last_impl == OTC_IMPL_BITSLICE, st, &g_last_impl);
+    if (const int form = split_form(g_last_impl, nbytes); form >= 0) {
+        e = cbc_dec_split(in, out, nbytes / 16, *k, iv, form, st, &g_last_impl);
     } else {
         e = otc_impl::tt_cbc_decrypt(in, out, nbytes / 16, *k, ctr_from_bytes(iv), st);
     }
@@ -930,9 +955,8 @@ extern "C" int otc_aes_cbc_decrypt_segments_impl(const void *in, void *out, size
     if (nseg == 0) return OTC_OK;
     hipError_t e;
     g_last_impl = pick_seg_impl(impl, k->bits, seg_bytes * nseg, sb);
-    if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE)
-        e = seg_dec_split(false, in, out, sb, nseg, *k, ctr_from_bytes(iv0), g_last_impl == OTC_IMPL_BITSLICE,
-                          (hipStream_t)stream, &g_last_impl);
+    if (const int form = seg_shift_of(sb) < 0 ? -1 : split_form(g_last_impl, seg_bytes * nseg); form >= 0)
+        e = seg_dec_split(false, in, out, sb, nseg, *k, ctr_from_bytes(iv0), form, (hipStream_t)stream, &g_last_impl);
     else
         e = otc_impl::tt_cbc_decrypt_seg(in, out, sb, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "cbc_decrypt_segments launch");
@@ -966,9 +990,9 @@ static int cfb_seg_common(const void *in, void *out, size_t seg_bytes, size_t ns
     hipError_t e;
     if (decrypt) {
         g_last_impl = pick_seg_impl(impl, k->bits, seg_bytes * nseg, seg_bytes / 16);
-        if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE)
-            e = seg_dec_split(true, in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
-                              g_last_impl == OTC_IMPL_BITSLICE, (hipStream_t)stream, &g_last_impl);
+        if (const int form = seg_shift_of(seg_bytes / 16) < 0 ? -1 : split_form(g_last_impl, seg_bytes * nseg); form >= 0)
+            e = seg_dec_split(true, in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0), form, (hipStream_t)stream,
+                              &g_last_impl);
         else
             e = otc_impl::tt_cfb_decrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
                                              (hipStream_t)stream);
@@ -1023,8 +1047,8 @@ extern "C" int otc_aes_cfb128_decrypt_impl(const void *in, void *out, size_t nby
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     g_last_impl = pick_ecb_impl(impl, k->bits, nbytes);
-    if (g_last_impl == OTC_IMPL_SPLIT || g_last_impl == OTC_IMPL_BITSLICE)
-        e = cfb_dec_split(in, out, nbytes / 16, *k, ivw, g_last_impl == OTC_IMPL_BITSLICE, st, &g_last_impl);
+    if (const int form = split_form(g_last_impl, nbytes); form >= 0)
+        e = cfb_dec_split(in, out, nbytes / 16, *k, ivw, form, st, &g_last_impl);
     else
         e = otc_impl::tt_cfb_decrypt(in, out, nbytes / 16, *k, ivw, st);
     if (e != hipSuccess) return hip_fail(e, "cfb_decrypt launch");
