@@ -616,6 +616,38 @@ def test_ctr_split_matches_oracle(gpu, bits):
             assert host(y[off:off + S]) == cpu_ref.ctr(key, sh.ctr_add(ctr, off // 16), host(x[off:off + S])), (n, off)
 
 
+def test_persistent_ttable_midsize(gpu):
+    """ECB (both directions), CBC / CFB decryption and their segment forms
+    between 896 MiB and 2 GiB run the persistent T-table claim kernel alone
+    (engine.cpp split_form FORM_TT): equal to the bitsliced claim kernel alone
+    and, on samples, to the oracle -- a size with a partial last unit, so
+    workgroup 0's remainder path runs too."""
+    key, iv = os.urandom(32), os.urandom(16)
+    n = (960 << 20) + 16 * 2048 * 3 + 16 * 5
+    x = torch.empty(n, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(x, seed=11)
+    seg = 4096
+    m = n - n % seg
+    calls = {
+        "ecb": (lambda i: ops.ecb_encrypt(x, key, impl=i), lambda h: cpu_ref.ecb(key, h), 0),
+        "ecb-dec": (lambda i: ops.ecb_decrypt(x, key, impl=i), lambda h: cpu_ref.ecb(key, h, decrypt=True), 0),
+        "cbc-dec": (lambda i: ops.cbc_decrypt(x, key, iv, impl=i), None, 0),
+        "cfb-dec": (lambda i: ops.cfb128_decrypt(x, key, iv, impl=i), None, 0),
+        "cbc-dec-seg": (lambda i: ops.cbc_decrypt_segments(x[:m], key, iv, seg, impl=i), None, 0),
+        "cfb-dec-seg": (lambda i: ops.cfb128_decrypt_segments(x[:m], key, iv, seg, impl=i), None, 0),
+    }
+    for name, (f, ref, _) in calls.items():
+        y = f("auto")
+        assert ops.last_impl() == "ttable", name
+        b = f("bitslice")
+        torch.cuda.synchronize()
+        assert torch.equal(y, b), name
+        if ref is not None:
+            for off in (0, (n // 2) & ~15, (n - 4096) & ~15):
+                assert host(y[off:off + 4096]) == ref(host(x[off:off + 4096])), (name, off)
+        del y, b
+
+
 def test_ecb_split_stream_order(gpu):
     """The caller's stream waits for BOTH kernels: work queued behind the
     split on the same stream sees the whole output, and the split starts only
