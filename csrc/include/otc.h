@@ -58,18 +58,21 @@ typedef struct {
 int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 
 /* ---- implementation selection ------------------------------------------- */
-#define OTC_IMPL_AUTO 0     /* the measured winner: bitsliced for CTR calls >= 2 GiB (AES-256:
-                               >= 1 GiB), the split below for ECB / CBC / CFB decrypt and the segment modes
-                               >= 896 MiB, T-table otherwise (OTC_IMPL=ttable|bitslice|split env overrides for
-                               the whole process) */
+#define OTC_IMPL_AUTO 0     /* the measured winner (docs/PERF.md round 5): bitsliced for CTR calls >= 2 GiB
+                               (AES-256: >= 1 GiB); for ECB / CBC / CFB decryption and the power-of-two segment
+                               decryptions the split below from 2 GiB and the persistent T-table claim kernel
+                               alone from 896 MiB; segment encryption: the persistent T-table claim kernel from
+                               2 GiB (1 GiB for segments <= 1 KiB); the grid T-table otherwise
+                               (OTC_IMPL=ttable|bitslice|split env overrides for the whole process) */
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
 #define OTC_IMPL_BITSLICE 2 /* bitsliced VALU kernel alone: 32 blocks per lane (CTR, ECB, the decryptions; their
                                claim kernels take every 2048-block unit and one T-table workgroup the blocks past
                                the last), 8 chains per lane for segment encryption (bs8) */
-#define OTC_IMPL_SPLIT 3    /* ECB, the CBC / CFB decryptions and the segment modes: the T-table and the bitsliced
-                               kernel CONCURRENTLY over one buffer (the bitsliced one on an auxiliary stream),
-                               co-resident on every CU -- LDS and VALU busy at once -- claiming units from one
-                               counter; "auto" for these calls >= 896 MiB.  CTR: as auto */
+#define OTC_IMPL_SPLIT 3    /* the T-table and the bitsliced kernel CONCURRENTLY over one buffer, each on a
+                               pooled CU-masked stream, co-resident on every CU -- LDS and VALU busy at once --
+                               claiming units from one counter: ECB, the CBC / CFB decryptions and the segment
+                               modes ("auto" for these >= 2 GiB), and CTR (on request only: +1-4% in a bare
+                               process, slower than the bitsliced kernel inside bench.py) */
 
 /* The kernel family `impl` resolves to for a call of nbytes with a bits-bit
  * key (mode 1: CTR, 0: ECB encryption, 2: ECB / CBC decryption, 3: CFB128
