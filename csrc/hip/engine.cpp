@@ -680,9 +680,12 @@ void otc_rt::aux_release_all()
     for (AuxStream &a : g_aux_free) {
         (void)hipSetDevice(a.dev);
         (void)hipStreamSynchronize(a.s);
+        (void)hipStreamSynchronize(a.t);
         (void)hipEventDestroy(a.fork);
         (void)hipEventDestroy(a.join);
+        (void)hipEventDestroy(a.join_t);
         (void)hipStreamDestroy(a.s);
+        (void)hipStreamDestroy(a.t);
     }
     g_aux_free.clear();
     (void)hipSetDevice(cur);

@@ -648,6 +648,25 @@ def test_persistent_ttable_midsize(gpu):
         del y, b
 
 
+def test_split_after_release_resources(gpu):
+    """otc_release_resources destroys the pooled split streams (both halves'
+    CU-masked streams and their events); the next split builds them afresh
+    and still equals the T-table."""
+    from our_tree_amd import _native
+
+    key = os.urandom(32)
+    n = 16 * 2048 * 40 + 48
+    x = torch.empty(n, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(x, seed=3)
+    t = ops.ecb_encrypt(x, key, impl="ttable")
+    for _ in range(2):
+        y = ops.ecb_encrypt(x, key, impl="split")
+        assert ops.last_impl() == "split"
+        torch.cuda.synchronize()
+        assert torch.equal(y, t)
+        _native.require_gpu_lib().otc_release_resources()
+
+
 def test_ecb_split_stream_order(gpu):
     """The caller's stream waits for BOTH kernels: work queued behind the
     split on the same stream sees the whole output, and the split starts only
