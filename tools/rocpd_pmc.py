@@ -84,6 +84,9 @@ def main():
             for k in ("FETCH_SIZE", "WRITE_SIZE"):
                 if k in c:
                     print(f"   {k + ' per payload byte':<36} {c[k] * 1024 / a.bytes:.3f}")
+        if "SQ_LDS_IDX_ACTIVE" in c and cyc:
+            # LDS pipe busy per CU-cycle (a conflict-free wave64 ds_read_b32 keeps it 2 cycles)
+            print(f"   LDS busy / CU-cycle                  {c['SQ_LDS_IDX_ACTIVE'] / a.cus / cyc:.3f}")
         if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
             tot = c["TCC_HIT_sum"] + c["TCC_MISS_sum"]
             print(f"   L2 hit rate                          {c['TCC_HIT_sum'] / tot if tot else 0:.3f}")
