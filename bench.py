@@ -392,6 +392,13 @@ def main():
                       "xgmi_write_kb")]
     table = per_rank_table(pdist.gather_floats(row))
     energy = node_energy(table)
+    # cycles/byte/CU at the clock amd-smi saw over each rank's energy window
+    # (all 8 XCDs sampled every 50 ms) and that rank's own rate, the largest
+    # over ranks: steadier than the one-wave probe's (r4/r5 records:
+    # 0.2690-0.2717 where the probe read 0.269-0.2808)
+    cpbs = [d["gfxclk_mhz_mean"] * 1e6 * cus / (d["gbps"] * 1e9) for d in table
+            if d.get("gfxclk_mhz_mean") and d.get("gbps")]
+    cpb_mean = max(cpbs) if cpbs and not cpu else None
     if pwv:
         energy["energy_window_s"] = pwv.get("window_s")  # rank 0's: timed steps + untimed extension
     if meter is not None and not pwv:
@@ -399,11 +406,9 @@ def main():
 
     extra = {}
     if not args.no_other and not cpu:
-        # the other AES-128 CTR kernels on the same shard, same protocol: the
-        # headline's "auto" runs the co-resident split at this size (round 5;
-        # the bitsliced VALU kernel alone before), and each single kernel --
-        # the bitsliced one BASELINE config 3 names, the LDS T-table -- is
-        # timed beside it
+        # the other AES-128 CTR kernel on the same shard, same protocol: the
+        # headline's "auto" runs the bitsliced VALU kernel at this size (the
+        # one BASELINE config 3 names); the LDS T-table is timed beside it
         for other in ("bitslice", "ttable"):
             if other == resolved:
                 continue
@@ -450,61 +455,15 @@ def main():
     # them (a transport error at N > 1, say) is recorded in the line instead
     # of losing the headline; a verification FAILURE still ends the run.
     extras_errors = {}
+    # the HIP runtime / RCCL this process runs on: in a torch process the
+    # library binds torch's bundled copies (HIP 7.0), in otbench /opt/rocm's
+    rt_info = None
+    if not cpu:
+        from our_tree_amd import _native
 
-    def guarded(name, fn):
-        try:
-            return fn()
-        except Exception as e:  # noqa: BLE001 -- reported in the JSON line
-            extras_errors[name] = f"{type(e).__name__}: {e}"[:500]
-            return None
+        rt_info = _native.runtime_info()
 
-    if not args.no_stream:
-        sp = guarded("stream", lambda: stream_pass(args, key, counter, rank, world, local, my_block0))
-        extra.update(sp or {"stream_ctr_verified": None})
-        if extra["stream_ctr_verified"] is False:
-            if rank == 0:
-                emit({"error": "host-streamed CTR verification failed", **extra})
-            sys.exit(1)
-
-    sc = None
-    if not args.no_scatter:
-        from our_tree_amd.parallel import jobs
-
-        del buf  # the scatter pass needs its own buffers (4 x world x chunk on the root)
-        if not cpu:
-            torch.cuda.empty_cache()
-        chunk = (args.scatter_mib << 20) if not cpu else 4096 * 8
-        sc = guarded("rccl_scatter", lambda: jobs.cbc_scatter_job(args.scatter_rounds, chunk, key256,
-                                                                  bytes(range(0xA0, 0xB0)), sector=4096, device=dev))
-    if not args.no_scatter and sc is not None:
-        extra["rccl_cbc256_scatter_gbps"] = round(sc["gbps"], 3)
-        extra["rccl_ranks"] = sc["ranks"]
-        extra["rccl_ranks_verified"] = sc["ranks_verified"]
-        extra["rccl_backend"] = sc["backend"]
-        extra["rccl_transport"] = sc["transport"]  # "xgmi" only over RCCL; gloo rehearsals: "host"
-        extra["rccl_xgmi_bytes_verified"] = sc["xgmi_bytes_verified"]
-        extra["rccl_xgmi_bytes_timed"] = sc["xgmi_bytes_timed"]
-        extra["rccl_host_bytes_verified"] = sc["host_bytes_verified"]
-        extra["rccl_scatter_bytes"] = sc["total_bytes"]
-        extra["rccl_scatter_verified"] = sc["verified"]
-        if not sc["verified"]:
-            if rank == 0:
-                emit({"error": "RCCL scatter/gather verification failed", "per_rank_ok": sc["per_rank_ok"], **extra})
-            sys.exit(1)
-
-    if not args.no_refmethod:
-        from our_tree_amd.utils import refmethod
-
-        if rank == 0:
-            extra.update(guarded("refmethod", lambda: refmethod.ecb256_three_ways(device=local))
-                         or {"refmethod_verified": None})
-        if torch.distributed.is_initialized():
-            torch.distributed.barrier()
-        if rank == 0 and extra["refmethod_verified"] is False:
-            emit({"error": "reference-methodology ECB verification failed", **extra})
-            sys.exit(1)
-
-    if rank == 0:
+    def final_line() -> dict:
         line = {
             "metric": "GB/s AES-128-CTR (whole node)",
             "value": round(value, 3),
@@ -531,6 +490,7 @@ def main():
             },
             "cycles_per_byte_per_cu": round(cpb, 4),
             "cycles_per_byte_per_cu_at_held_clock": round(cpb_eff, 4) if cpb_eff else None,
+            "cycles_per_byte_per_cu_at_mean_gfxclk": round(cpb_mean, 4) if cpb_mean else None,
             "held_clock_ghz": round(clk_ghz, 3) if clk_ghz else None,
             "per_gpu_gbps": round(value / world, 3),
             "per_rank_gbps_min": round(min(d["gbps"] for d in table), 3),
@@ -541,11 +501,82 @@ def main():
             "baseline": {"value_gbps": BASELINE_GBPS, "what": "AES-NI CTR-256 1000MiB 8thr (BASELINE.md)",
                          "gpu_headline_gbps": BASELINE_GPU_GBPS},
             "verified_sample": all(d["verified"] for d in table),
+            "runtime": rt_info,
             **extra,
         }
         if extras_errors:
             line["extras_errors"] = extras_errors
-        emit(line)
+        return line
+
+    def guarded(name, fn):
+        """Run one extra stage.  At N = 1 an exception is recorded in the line
+        and the run goes on.  At N > 1 the other ranks may be waiting inside
+        this stage's collectives, and a rank that skipped ahead would pair its
+        next collective with theirs: so the failing rank ends the run (rank 0
+        first emits the line with what was measured and the error; the
+        launcher stops the other ranks when one exits non-zero)."""
+        try:
+            return fn()
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+            extras_errors[name] = f"{type(e).__name__}: {e}"[:500]
+            if world > 1:
+                print(json.dumps({"rank": rank, "stage_failed": name, "error": extras_errors[name]}),
+                      file=sys.stderr, flush=True)
+                if rank == 0:
+                    emit({**final_line(), "error": f"extra stage '{name}' failed at N > 1"})
+                os._exit(1)
+            return None
+
+    if not args.no_stream:
+        sp = guarded("stream", lambda: stream_pass(args, key, counter, rank, world, local, my_block0))
+        extra.update(sp or {"stream_ctr_verified": None})
+        if extra["stream_ctr_verified"] is False:
+            if rank == 0:
+                emit({"error": "host-streamed CTR verification failed", **extra})
+            sys.exit(1)
+
+    sc = None
+    if not args.no_scatter:
+        from our_tree_amd.parallel import jobs
+
+        # The shard stays allocated: the scatter pass needs only 4 x world x
+        # chunk more on the root (16 GiB at N = 8), and freeing 64 GiB here made
+        # the driver clear it in the background over the next seconds, which
+        # slowed every D2H copy of the later pinned pipeline row from 49 to
+        # 37 GB/s (round 6, profiles/r6/pipeline/).
+        chunk = (args.scatter_mib << 20) if not cpu else 4096 * 8
+        sc = guarded("rccl_scatter", lambda: jobs.cbc_scatter_job(args.scatter_rounds, chunk, key256,
+                                                                  bytes(range(0xA0, 0xB0)), sector=4096, device=dev))
+    if not args.no_scatter and sc is not None:
+        extra["rccl_cbc256_scatter_gbps"] = round(sc["gbps"], 3)
+        extra["rccl_ranks"] = sc["ranks"]
+        extra["rccl_ranks_verified"] = sc["ranks_verified"]
+        extra["rccl_backend"] = sc["backend"]
+        extra["rccl_transport"] = sc["transport"]  # "xgmi" over RCCL at N > 1, "local" at N = 1, gloo: "host"
+        extra["rccl_xgmi_bytes_verified"] = sc["xgmi_bytes_verified"]
+        extra["rccl_xgmi_bytes_timed"] = sc["xgmi_bytes_timed"]
+        extra["rccl_host_bytes_verified"] = sc["host_bytes_verified"]
+        extra["rccl_scatter_bytes"] = sc["total_bytes"]
+        extra["rccl_scatter_verified"] = sc["verified"]
+        if not sc["verified"]:
+            if rank == 0:
+                emit({"error": "RCCL scatter/gather verification failed", "per_rank_ok": sc["per_rank_ok"], **extra})
+            sys.exit(1)
+
+    if not args.no_refmethod:
+        from our_tree_amd.utils import refmethod
+
+        if rank == 0:
+            extra.update(guarded("refmethod", lambda: refmethod.ecb256_three_ways(device=local))
+                         or {"refmethod_verified": None})
+        if torch.distributed.is_initialized():
+            torch.distributed.barrier()
+        if rank == 0 and extra["refmethod_verified"] is False:
+            emit({"error": "reference-methodology ECB verification failed", **extra})
+            sys.exit(1)
+
+    if rank == 0:
+        emit(final_line())
     if meter is not None:
         meter.close()
     if torch.distributed.is_initialized():

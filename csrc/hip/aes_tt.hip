@@ -81,6 +81,18 @@ __device__ __forceinline__ uint32_t lds_at(const uint32_t *tbl, uint32_t byte_ad
  * lookups take the integer LDS address instead. */
 struct DynTbl {
 };
+
+/* Negative control for the co-residency test (tests/test_gpu_queues.py):
+ * `make variant NAME=padclaim VFLAGS=-DOTC_DIAG_PAD_CLAIM` pads the T-table
+ * claim kernels' register descriptors to a 4-waves-per-SIMD budget -- what the
+ * round-4 static-LDS build did by accident -- so no bitsliced wave fits beside
+ * them and the split's halves run one after the other.  Never in the release
+ * build. */
+#ifdef OTC_DIAG_PAD_CLAIM
+#define OTC_CLAIM_ATTR __attribute__((amdgpu_waves_per_eu(4, 4)))
+#else
+#define OTC_CLAIM_ATTR
+#endif
 __device__ __forceinline__ uint32_t lds_at(DynTbl, uint32_t byte_addr)
 {
     return *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t)byte_addr;
@@ -426,24 +438,24 @@ __global__ __launch_bounds__(THREADS) void k_aes_enc_tt(EncParams P, otc_aes_key
 #define OTC_TT_ECB_CLAIM_B OTC_TT_ENC_B
 #endif
 template <int NR>
-__global__ __launch_bounds__(1024) void k_aes_ecb_tt_claim(EncParams P, otc_aes_key K)
+__global__ __launch_bounds__(1024) OTC_CLAIM_ATTR void k_aes_ecb_tt_claim(EncParams P, otc_aes_key K)
 {
     enc_tt_body<NR, E_ECB, OTC_TT_ECB_CLAIM_B, 1024, true>(P, K);
 }
 template <int NR>
-__global__ __launch_bounds__(1024) void k_aes_cfb_tt_claim(EncParams P, otc_aes_key K)
+__global__ __launch_bounds__(1024) OTC_CLAIM_ATTR void k_aes_cfb_tt_claim(EncParams P, otc_aes_key K)
 {
     enc_tt_body<NR, E_CFB_DEC, OTC_TT_CLAIM_B, 1024, true>(P, K);
 }
 /* CTR beside the bitsliced CTR claim kernel (counter caching on that side,
  * 32 KiB of LDS staging: 128 + 32 KiB fill the CU) */
 template <int NR>
-__global__ __launch_bounds__(1024) void k_aes_ctr_tt_claim(EncParams P, otc_aes_key K)
+__global__ __launch_bounds__(1024) OTC_CLAIM_ATTR void k_aes_ctr_tt_claim(EncParams P, otc_aes_key K)
 {
     enc_tt_body<NR, E_CTR, OTC_TT_CLAIM_B, 1024, true>(P, K);
 }
 template <int NR>
-__global__ __launch_bounds__(1024) void k_aes_cfbseg_tt_claim(EncParams P, otc_aes_key K)
+__global__ __launch_bounds__(1024) OTC_CLAIM_ATTR void k_aes_cfbseg_tt_claim(EncParams P, otc_aes_key K)
 {
     enc_tt_body<NR, E_CFB_DEC_SEG, OTC_TT_CLAIM_B, 1024, true>(P, K);
 }
@@ -634,7 +646,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_dec_tt(DecParams P, otc_aes_key
 /* Claimed split: the bitsliced inverse-cipher kernels take 168 registers,
  * leaving 80 per T-table wave: B = 2 (ECB 51, CBC 66; at 4: 83 / 106) */
 template <int NR, int MODE>
-__global__ __launch_bounds__(1024) void k_aes_dec_tt_claim(DecParams P, otc_aes_key K)
+__global__ __launch_bounds__(1024) OTC_CLAIM_ATTR void k_aes_dec_tt_claim(DecParams P, otc_aes_key K)
 {
     dec_tt_body<NR, MODE, OTC_TT_CLAIM_B, 1024, true>(P, K);
 }
@@ -810,7 +822,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg_g(CbcSegParams P, o
  * The bitsliced half (aes_bs8.hip) takes 8 units at a time from the front. */
 constexpr uint32_t SEG_UNIT = 64;
 template <int NR, int G, bool CFB>
-__global__ __launch_bounds__(1024) void k_aes_seg_enc_tt_claim(CbcSegParams P, otc_aes_key K)
+__global__ __launch_bounds__(1024) OTC_CLAIM_ATTR void k_aes_seg_enc_tt_claim(CbcSegParams P, otc_aes_key K)
 {
     uint32_t *tbl = tt_lds<true, 2 * 256 * 64>();
     fill_tbl4<1024>(tbl, g_tab.te0);

@@ -254,9 +254,8 @@ hipError_t aux_take(int dev, AuxStream &out)
      * the other half, and then the two kernels run one after the other: in
      * bench.py, beside torch's and RCCL's streams, the CTR split ran at the
      * T-table's speed (1534 GB/s) */
-    std::vector<uint32_t> mask((size_t)(otc_dev::device_cus() + 31) / 32, 0xFFFFFFFFu);
-    hipError_t e = hipExtStreamCreateWithCUMask(&a.s, (uint32_t)mask.size(), mask.data());
-    if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&a.t, (uint32_t)mask.size(), mask.data());
+    hipError_t e = dedicated_stream_create(&a.s);
+    if (e == hipSuccess) e = dedicated_stream_create(&a.t);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&a.fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&a.join, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&a.join_t, hipEventDisableTiming);
@@ -1359,4 +1358,42 @@ extern "C" const char *otc_build_info(void)
 {
     return "otc: MI355X (gfx950) cipher engine; kernels: aes_tt (LDS T-table), aes_bs (bitsliced VALU), "
            "rc4_multi, xor; runtime: pinned 3-stream pipeline, RCCL multi-GPU";
+}
+
+/* Which HIP runtime and RCCL this process actually runs on.  libotc.so links
+ * libamdhip64.so.7 / librccl.so.1 by SONAME, and torch ships libraries with
+ * the same SONAMEs: inside a torch process the library runs on torch's HIP
+ * (7.0) and RCCL, in otbench and the CLIs on /opt/rocm's (7.2).  Every A/B
+ * record carries this so the two are never compared unawares. */
+extern "C" int otc_runtime_info(char *buf, size_t n)
+{
+    if (!buf || n == 0) return set_err(OTC_ERR_ARG, "null buffer");
+    int rt = 0, drv = 0;
+    if (hipRuntimeGetVersion(&rt) != hipSuccess) {
+        (void)hipGetLastError();
+        rt = -1;
+    }
+    if (hipDriverGetVersion(&drv) != hipSuccess) {
+        (void)hipGetLastError();
+        drv = -1;
+    }
+    int rccl = 0;
+    if (ncclGetVersion(&rccl) != ncclSuccess) rccl = -1;
+    std::string hip_path, rccl_path;
+    if (FILE *f = fopen("/proc/self/maps", "r")) {
+        char line[4096];
+        while (fgets(line, sizeof line, f)) {
+            char *p = strchr(line, '/');
+            if (!p) continue;
+            p[strcspn(p, "\n")] = 0;
+            if (hip_path.empty() && strstr(p, "libamdhip64.so")) hip_path = p;
+            if (rccl_path.empty() && strstr(p, "librccl.so")) rccl_path = p;
+        }
+        fclose(f);
+    }
+    const int w = snprintf(buf, n,
+                           "{\"hip_runtime_version\": %d, \"hip_driver_version\": %d, \"rccl_version\": %d, "
+                           "\"libamdhip64\": \"%s\", \"librccl\": \"%s\"}",
+                           rt, drv, rccl, hip_path.c_str(), rccl_path.c_str());
+    return w < 0 || (size_t)w >= n ? set_err(OTC_ERR_ARG, "buffer too small") : OTC_OK;
 }

@@ -10,6 +10,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <string>
+#include <vector>
 
 #include "otc.h"
 #include "otc_device.h"
@@ -37,6 +38,18 @@ struct Range {
     Range(const Range &) = delete;
     Range &operator=(const Range &) = delete;
 };
+
+/* A stream with a hardware queue of its own: HIP maps ordinary streams onto
+ * GPU_MAX_HW_QUEUES (4) pooled queues per device per process, so in a process
+ * that also holds torch's, RCCL's and a profiler's streams a library stream can
+ * share a queue with an unrelated one and its work waits behind that stream's
+ * (barrier packets are processed in queue order).  A stream created with a CU
+ * mask -- here all CUs -- always gets a dedicated queue. */
+inline hipError_t dedicated_stream_create(hipStream_t *s)
+{
+    std::vector<uint32_t> mask((size_t)(otc_dev::device_cus() + 31) / 32, 0xFFFFFFFFu);
+    return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
 
 /* hipMalloc behind the fault-injection hook */
 inline hipError_t dev_alloc(void **p, size_t n)

@@ -166,6 +166,7 @@ struct otc_engine {
     int numa_node = -1;
     size_t chunk = 0;
     int depth = 0;                   /* ring slots */
+    int flags = 0;                   /* OTC_ENGINE_* */
     std::vector<void *> d_in, d_out; /* device ring */
     std::vector<PinnedBuf> h_in, h_out; /* pinned staging ring (pageable callers only) */
     hipStream_t s_h2d = nullptr, s_k = nullptr, s_d2h = nullptr;
@@ -175,6 +176,11 @@ struct otc_engine {
 
 extern "C" otc_engine *otc_engine_create(int device, size_t chunk_bytes, int depth)
 {
+    return otc_engine_create_ex(device, chunk_bytes, depth, OTC_ENGINE_DEFAULT);
+}
+
+extern "C" otc_engine *otc_engine_create_ex(int device, size_t chunk_bytes, int depth, int flags)
+{
     if (chunk_bytes == 0) chunk_bytes = 256ull << 20;
     chunk_bytes = (chunk_bytes + 15) & ~(size_t)15;
     if (depth < 2) depth = 3;
@@ -182,15 +188,18 @@ extern "C" otc_engine *otc_engine_create(int device, size_t chunk_bytes, int dep
     e->device = device;
     e->chunk = chunk_bytes;
     e->depth = depth;
+    e->flags = flags;
     if (hipSetDevice(device) != hipSuccess) {
         set_err(OTC_ERR_HIP, "hipSetDevice");
         delete e;
         return nullptr;
     }
     e->numa_node = gpu_numa_node(device);
-    bool ok = hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&e->s_k, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&e->s_d2h, hipStreamNonBlocking) == hipSuccess;
+    auto mk = [&](hipStream_t *s) {
+        return (flags & OTC_ENGINE_POOLED_QUEUES) ? hipStreamCreateWithFlags(s, hipStreamNonBlocking)
+                                                  : dedicated_stream_create(s);
+    };
+    bool ok = mk(&e->s_h2d) == hipSuccess && mk(&e->s_k) == hipSuccess && mk(&e->s_d2h) == hipSuccess;
     e->d_in.assign(depth, nullptr);
     e->d_out.assign(depth, nullptr);
     e->h_in.assign(depth, PinnedBuf{});
@@ -469,7 +478,9 @@ static int rccl_job_init(RcclJob &J, int ngpus, size_t S)
     const size_t round = S * (size_t)ngpus;
     for (int g = 0; g < ngpus; ++g) {
         HIPCHK(hipSetDevice(g));
-        for (hipStream_t *s : {&J.sc[g], &J.kst[g], &J.ga[g]}) HIPCHK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+        /* queues of their own: beside a caller's torch / RCCL streams, pooled
+         * queues would let scatter, cipher and gather wait behind each other */
+        for (hipStream_t *s : {&J.sc[g], &J.kst[g], &J.ga[g]}) HIPCHK(dedicated_stream_create(s));
         for (int b = 0; b < 2; ++b) {
             HIPCHK(dev_alloc(&J.pin[b][g], S));
             HIPCHK(dev_alloc(&J.pout[b][g], S));

@@ -300,6 +300,14 @@ int otc_stream_join(void *a, void *b);
 typedef struct otc_engine otc_engine;
 
 otc_engine *otc_engine_create(int device, size_t chunk_bytes, int depth);
+/* flags: OTC_ENGINE_DEFAULT -- the three streams get hardware queues of their
+ * own (all-CU-masked streams), so the pipeline overlaps in a process whose
+ * other streams (torch, RCCL) fill the 4 pooled queues HIP gives a process;
+ * OTC_ENGINE_POOLED_QUEUES -- plain non-blocking streams on the pooled queues
+ * (the A/B arm; docs/PERF.md "Round 6"). */
+#define OTC_ENGINE_DEFAULT 0
+#define OTC_ENGINE_POOLED_QUEUES 1
+otc_engine *otc_engine_create_ex(int device, size_t chunk_bytes, int depth, int flags);
 void otc_engine_destroy(otc_engine *e);
 
 #define OTC_MODE_ECB 0
@@ -411,6 +419,10 @@ int otc_bitslice_selftest(int verbose);
 /* the row-sliced chain kernel's arithmetic (otc_bs8.h) against the C oracle */
 int otc_bs8_selftest(int verbose);
 const char *otc_build_info(void);
+/* JSON object naming the HIP runtime / driver and RCCL versions this process
+ * runs on and the mapped libamdhip64 / librccl paths (/proc/self/maps): in a
+ * torch process they are torch's bundled copies, elsewhere /opt/rocm's. */
+int otc_runtime_info(char *buf, size_t n);
 
 #ifdef __cplusplus
 }

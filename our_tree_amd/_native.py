@@ -230,16 +230,31 @@ def _declare_gpu(lib):
         "otc_ptr_kind": (c_int, [c_vp]),
         "otc_host_free_pinned": (None, [c_vp]),
         "otc_engine_create": (c_vp, [c_int, c_sz, c_int]),
+        "otc_engine_create_ex": (c_vp, [c_int, c_sz, c_int, c_int]),
         "otc_engine_destroy": (None, [c_vp]),
         "otc_engine_run": (c_int, [c_vp, c_int, c_vp, c_vp, c_sz, K, c_u8p, c_u64, c_int, P(StreamStats)]),
         "otc_multi_run": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_sz, K, c_u8p, c_int, c_sz, P(MultiStats)]),
         "otc_multi_ctr_resident": (c_int, [c_int, P(c_vp), c_sz, K, c_u8p, c_int, P(ctypes.c_double)]),
         "otc_build_info": (ctypes.c_char_p, []),
+        "otc_runtime_info": (c_int, [ctypes.c_char_p, c_sz]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+
+
+def runtime_info() -> dict:
+    """The HIP runtime / driver and RCCL versions this process runs on and the
+    mapped libamdhip64 / librccl paths (otc_runtime_info): in a torch process
+    the library binds torch's bundled HIP 7.0 and RCCL, in otbench and the
+    CLIs /opt/rocm's 7.2 -- every A/B record names which."""
+    import json
+
+    lib = require_gpu_lib()
+    buf = ctypes.create_string_buffer(4096)
+    check(lib.otc_runtime_info(buf, len(buf)), "otc_runtime_info")
+    return json.loads(buf.value.decode())
 
 
 def gpu_lib_available() -> bool:

@@ -238,7 +238,8 @@ def cbc_scatter_job(rounds: int, chunk: int, key: bytes, iv0: bytes, sector: int
         "backend": backend,
         "collectives": bool(pipe.comm),
         "overlap": pipe.overlap,
-        "transport": "xgmi" if xgmi else ("host" if pipe.comm else "none"),
+        # a 1-rank group moves nothing between GPUs: its "scatter" is a local copy
+        "transport": ("local" if world == 1 else "xgmi" if xgmi else "host") if pipe.comm else "none",
         "peer_bytes_verified": peer_verified,
         "peer_bytes_timed": peer_timed,
         "xgmi_bytes_verified": peer_verified if xgmi else 0,

@@ -44,9 +44,12 @@ def _nb(a):
 class StreamEngine:
     """Pinned double/triple-buffered host<->GPU pipeline on one device."""
 
-    def __init__(self, device: int = 0, chunk_bytes: int = 256 << 20, depth: int = 3):
+    def __init__(self, device: int = 0, chunk_bytes: int = 256 << 20, depth: int = 3, pooled_queues: bool = False):
+        """``pooled_queues``: run the three streams on HIP's pooled hardware
+        queues instead of queues of their own (otc_engine_create_ex; the A/B
+        arm of docs/PERF.md "Round 6")."""
         self._lib = _native.require_gpu_lib()
-        self._h = self._lib.otc_engine_create(device, chunk_bytes, depth)
+        self._h = self._lib.otc_engine_create_ex(device, chunk_bytes, depth, 1 if pooled_queues else 0)
         if not self._h:
             _native.check(-5, "otc_engine_create")
         self.device = device

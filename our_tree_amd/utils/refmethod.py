@@ -8,9 +8,10 @@ a synchronous pageable H2D, the launch, a synchronous D2H and cudaFree x2
 every call.  ``ecb256_three_ways`` times exactly that sequence (key
 expansion, hipMalloc x2, pageable hipMemcpy H2D, kernel, pageable hipMemcpy
 D2H, hipFree x2, all inside the timer, 10 iterations averaged as the
-reference prints "Average"), then the same buffer through the native pinned
-3-stream pipeline (key setup + H2D | kernel | D2H) and kernel-only on
-device-resident data.  Every variant's output is checked against the C
+reference prints "Average"), beside the same buffer through the native
+pinned 3-stream pipeline (key setup + H2D | kernel | D2H) and kernel-only on
+device-resident data -- those two are timed first, before the reference's
+allocate / free sequence runs.  Every variant's output is checked against the C
 oracle on a head and a tail sample.
 """
 from __future__ import annotations
@@ -60,20 +61,18 @@ def ecb256_three_ways(nbytes: int = 1000 << 20, iters: int = 10, device: int = 0
         lib.otc_dev_free(d_out)
         return time.perf_counter() - t0
 
-    one_ref()  # first call: context / module warm-up, as the reference's runs 2-10 (results.baryon)
-    ref_s = [one_ref() for _ in range(iters)]
-    ref_ok = _ok(key, host_in, host_out)
-
     # pinned pipeline: H2D(k+1) | kernel(k) | D2H(k-1), key setup inside the timer
     pin_in, pin_out = pstream.pinned_empty(nbytes), pstream.pinned_empty(nbytes)
     pin_in[:] = host_in
     with pstream.StreamEngine(device, chunk_bytes=64 << 20, depth=3) as eng:
         eng.run("ecb", pin_in, pin_out, key)
-        pin_s = []
+        pin_s, h2d_ms, d2h_ms = [], 0.0, 0.0
         for _ in range(iters):
             t0 = time.perf_counter()
-            eng.run("ecb", pin_in, pin_out, key)
+            st = eng.run("ecb", pin_in, pin_out, key)
             pin_s.append(time.perf_counter() - t0)
+            h2d_ms += st["h2d_ms"]
+            d2h_ms += st["d2h_ms"]
     pin_ok = _ok(key, host_in, pin_out)
     del pin_in, pin_out
 
@@ -96,6 +95,14 @@ def ecb256_three_ways(nbytes: int = 1000 << 20, iters: int = 10, device: int = 0
     kern_ok = _ok(key, host_in, d_out.cpu().numpy())
     del d_in, d_out
 
+    # the reference's own sequence last: its hipFree x2 per call leaves the
+    # driver reclaiming the freed device memory for a while afterwards, and a
+    # pinned row timed right behind it lost its D2H rate (49.5 -> 37 GB/s for
+    # ~3 s after freeing 64 GiB, ~0.4 s after 8 GiB; profiles/r6/pipeline/)
+    one_ref()  # first call: context / module warm-up, as the reference's runs 2-10 (results.baryon)
+    ref_s = [one_ref() for _ in range(iters)]
+    ref_ok = _ok(key, host_in, host_out)
+
     ref_avg = sum(ref_s) / len(ref_s)
     pin_avg = sum(pin_s) / len(pin_s)
     return {
@@ -103,6 +110,9 @@ def ecb256_three_ways(nbytes: int = 1000 << 20, iters: int = 10, device: int = 0
         "refmethod_ecb256_1000mib_avg_us": round(ref_avg * 1e6, 1),
         "refmethod_vs_reference": round(nbytes / ref_avg / 1e9 / REF_GBPS, 2),
         "pinned_e2e_ecb256_1000mib_gbps": round(nbytes / pin_avg / 1e9, 3),
+        # per-direction PCIe rates while the copies were in flight (event sums)
+        "pinned_e2e_h2d_gbps": round(nbytes * iters / (h2d_ms * 1e6), 2) if h2d_ms else None,
+        "pinned_e2e_d2h_gbps": round(nbytes * iters / (d2h_ms * 1e6), 2) if d2h_ms else None,
         "kernel_only_ecb256_1000mib_gbps": round(nbytes / kern_s / 1e9, 3),
         "refmethod_verified": bool(ref_ok and pin_ok and kern_ok),
         "refmethod_what": "AES-256 ECB 1000 MiB, timer around key setup + hipMalloc x2 + pageable H2D + kernel + "

@@ -12,7 +12,14 @@ J/GB each, and their median within 0.278.  The same kernel reads 0.2713
 (BENCH_r04), 0.2755 (profiles/r5/validate) and 0.2816 (a round-4 builder
 record) on different boxes -- the held-clock probe and the box move it by
 ~2-4% -- so a single record gets that much slack and the median guards the
-trend.  The reference has no such metric: it timed wall-clock microseconds
+trend.
+
+Round 6 adds the figure at amd-smi's mean GFX clock over the energy window
+(``cycles_per_byte_per_cu_at_mean_gfxclk``; derived from ``per_rank`` for older
+records).  The seven r4/r5 records spread 0.2690-0.2717 on it (median 0.2701,
++-0.5%) where the probe's figure spread 0.269-0.2808, so its guard is 2% over
+that median: a 2% regression in work per byte fails, box-to-box noise does
+not.  The reference has no such metric: it timed wall-clock microseconds
 only (/root/reference/test.c:31-40)."""
 import glob
 import json
@@ -23,6 +30,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CYC_MAX, CYC_MEDIAN_MAX, JGB_MAX = 0.285, 0.278, 0.83
+CYC_MEAN_CLK_MAX = round(0.2701 * 1.02, 4)  # 0.2755
 FIRST_ROUND = 4          # driver records
 FIRST_BUILDER_ROUND = 5  # profiles/rN validation records
 
@@ -86,3 +94,28 @@ def test_headline_cycles_median():
     assert cyc
     med = cyc[len(cyc) // 2] if len(cyc) % 2 else (cyc[len(cyc) // 2 - 1] + cyc[len(cyc) // 2]) / 2
     assert med <= CYC_MEDIAN_MAX, (med, cyc)
+
+
+def cycles_at_mean_gfxclk(b):
+    """the record's key, or the same figure from its per-rank clock and rate"""
+    v = b.get("cycles_per_byte_per_cu_at_mean_gfxclk")
+    if v is not None:
+        return v
+    vals = [d["gfxclk_mhz_mean"] * 1e6 * 256 / (d["gbps"] * 1e9) for d in b.get("per_rank") or []
+            if d.get("gfxclk_mhz_mean") and d.get("gbps")]
+    return max(vals) if vals else None
+
+
+@pytest.mark.parametrize("path,b", [r for r in records() if headline(r[1])], ids=lambda x: x if isinstance(x, str) else "")
+def test_headline_cycles_at_mean_gfxclk(path, b):
+    cyc = cycles_at_mean_gfxclk(b)
+    assert cyc is not None, (path, "record lacks gfxclk_mhz_mean")
+    assert cyc <= CYC_MEAN_CLK_MAX, (path, cyc)
+
+
+def test_mean_gfxclk_guard_catches_2pct():
+    """the guard's margin: a record 2% slower per clock than the r4/r5 median fails"""
+    base = [cycles_at_mean_gfxclk(b) for _, b in records() if headline(b)]
+    base = sorted(v for v in base if v is not None)
+    med = base[len(base) // 2]
+    assert med * 1.021 > CYC_MEAN_CLK_MAX >= max(base)

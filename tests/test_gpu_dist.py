@@ -7,7 +7,6 @@ allreduce_max runs an RCCL all-reduce on a device tensor.  Results are checked
 against the CPU oracle.  Multi-rank correctness is covered by
 tests/test_dist_cpu.py (gloo, world sizes 2 and 3)."""
 import os
-import socket
 
 import pytest
 import torch
@@ -15,32 +14,6 @@ import torch
 from our_tree_amd.models import cpu_ref
 
 pytestmark = pytest.mark.gpu
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-@pytest.fixture
-def rccl_world1(gpu):
-    import torch.distributed as dist
-
-    from our_tree_amd.parallel import dist as pdist
-
-    if dist.is_initialized():
-        pytest.skip("a process group already exists in this process")
-    store = dist.TCPStore("127.0.0.1", _free_port(), 1, is_master=True)
-    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=gpu)
-    pdist.reset_groups()
-    try:
-        yield pdist
-    finally:
-        dist.destroy_process_group()
-        pdist.reset_groups()
 
 
 def test_rccl_scatter_gather_pipeline(gpu, rccl_world1):
