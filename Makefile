@@ -37,7 +37,7 @@ OBJ    := build/obj
 
 CPU_SRC := csrc/cpu/aes.c csrc/cpu/arc4.c csrc/cpu/rc4.c csrc/cpu/aesni.c csrc/cpu/numa.c csrc/cpu/rccl_plan.c
 CPU_OBJ := $(patsubst csrc/cpu/%.c,$(OBJ)/cpu/%.o,$(CPU_SRC)) $(OBJ)/cpu/bs_selftest.o
-HIP_SRC := csrc/hip/aes_tt.hip csrc/hip/aes_bs.hip csrc/hip/aes_bs8.hip csrc/hip/stream_ops.hip
+HIP_SRC := csrc/hip/aes_tt.hip csrc/hip/aes_bs.hip csrc/hip/stream_ops.hip
 HIP_OBJ := $(patsubst csrc/hip/%.hip,$(OBJ)/hip/%.o,$(HIP_SRC)) $(OBJ)/hip/engine.o $(OBJ)/hip/pipeline.o
 
 BINS := bin/test bin/aes_test bin/aes_ecb_e bin/aes_ecb_d bin/otbench bin/bc_test
@@ -61,7 +61,7 @@ $(OBJ)/cpu/bs_selftest.o: csrc/cpu/bs_selftest.cpp $(wildcard csrc/include/*.h)
 # -fno-slp-vectorize: the SLP vectorizer packs the 4 independent transposes /
 # 16 S-boxes of the bitsliced kernel into lock-stepped vector ops, which doubles
 # the live register set (1 wave/SIMD + AGPR spills).  See docs/PERF.md.
-$(OBJ)/hip/aes_bs.o $(OBJ)/hip/aes_bs8.o: HIPFLAGS += -fno-slp-vectorize
+$(OBJ)/hip/aes_bs.o: HIPFLAGS += -fno-slp-vectorize
 
 $(OBJ)/hip/%.o: csrc/hip/%.hip $(wildcard csrc/hip/*.h) $(wildcard csrc/include/*.h)
 	@mkdir -p $(dir $@)

@@ -344,6 +344,15 @@ static int corrupt(void *out, size_t off, bool device)
     return 0;
 }
 
+/* the HIP runtime / RCCL this process is bound to (otc_runtime_info): every
+ * record says which, so A/Bs across the /opt/rocm and torch runtimes are
+ * never compared unawares */
+static std::string runtime_json()
+{
+    char buf[1024];
+    return otc_runtime_info(buf, sizeof buf) == OTC_OK ? std::string(buf) : std::string("null");
+}
+
 /* --mark lines, flushed at once: on the GPU box the runtime leaves stderr
  * buffered, and a mark that arrives late shrinks the power window */
 static void mark(const char *what)
@@ -486,9 +495,9 @@ int main(int argc, char **argv)
             ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
         }
         printf("{\"mode\": \"%s\", \"bits\": %d, \"bytes\": %zu, \"e2e\": true, \"gpus\": %d, \"strategy\": \"%s\", "
-               "\"chunk\": %zu, \"ms\": %.3f, \"gbps\": %.3f, \"verified\": %s}\n",
+               "\"chunk\": %zu, \"ms\": %.3f, \"gbps\": %.3f, \"runtime\": %s, \"verified\": %s}\n",
                c.mode.c_str(), c.bits, c.bytes, c.gpus, c.strategy ? "rccl" : "direct", c.chunk, ms,
-               c.bytes / (ms * 1e6), verdict(c.verify, v));
+               c.bytes / (ms * 1e6), runtime_json().c_str(), verdict(c.verify, v));
         otc_engine_destroy(eng);
         otc_host_free_pinned(hin);
         otc_host_free_pinned(hout);
@@ -561,24 +570,24 @@ int main(int argc, char **argv)
     char split_units[96] = "";
     if (c.strace) { /* diagnostic builds: when each kernel's waves started, one more call */
         std::vector<unsigned long long> rec(2 * 16384);
-        for (int w = 0; w < 3; ++w) (void)otc_split_trace(w, rec.data(), 16384); /* reset */
+        for (int w = 0; w < 2; ++w) (void)otc_split_trace(w, rec.data(), 16384); /* reset */
         if (run_op(&a) || otc_device_sync()) return 1;
         unsigned long long t0 = ~0ull;
-        std::vector<std::vector<unsigned long long>> st(3);
-        for (int w = 0; w < 3; ++w) {
+        std::vector<std::vector<unsigned long long>> st(2);
+        for (int w = 0; w < 2; ++w) {
             const int n = otc_split_trace(w, rec.data(), 16384);
             for (int i = 0; i < n; ++i) {
                 st[w].push_back(rec[2 * i]);
                 if (w == 0) t0 = std::min(t0, rec[2 * i]);
             }
         }
-        for (int w = 0; w < 3; ++w) {
+        for (int w = 0; w < 2; ++w) {
             auto &v = st[w];
             if (v.empty()) continue;
             std::sort(v.begin(), v.end());
             auto us = [&](unsigned long long t) { return t0 == ~0ull ? 0.0 : ((double)t - (double)t0) / 100.0; };
             fprintf(stderr, "strace %s: %zu waves, start (us after the first T-table wave) min %.1f median %.1f p90 %.1f max %.1f\n",
-                    w == 0 ? "ttable" : w == 1 ? "bitslice" : "bs8", v.size(), us(v.front()), us(v[v.size() / 2]),
+                    w == 0 ? "ttable" : "bitslice", v.size(), us(v.front()), us(v[v.size() / 2]),
                     us(v[v.size() * 9 / 10]), us(v.back()));
         }
     }
@@ -610,13 +619,14 @@ int main(int argc, char **argv)
     const int ran = otc_last_impl(); /* what the last timed call ran (this thread) */
     printf("{\"mode\": \"%s\", \"bits\": %d, \"bytes\": %zu, \"impl\": \"%s\", \"ran\": \"%s\", \"inplace\": %s, "
            "\"iters\": %d, \"ms\": %.4f, \"gbps\": %.2f, \"cycles_per_byte_per_cu\": %.3f, \"cus\": %d, \"clock_mhz\": %.0f, %s"
-           "\"verified\": %s}\n",
+           "\"runtime\": %s, \"verified\": %s}\n",
            c.mode.c_str(), c.bits, c.bytes,
            c.impl == OTC_IMPL_TTABLE ? "ttable" : c.impl == OTC_IMPL_BITSLICE ? "bitslice"
            : c.impl == OTC_IMPL_SPLIT    ? "split"  : "auto",
            ran == OTC_IMPL_TTABLE ? "ttable" : ran == OTC_IMPL_BITSLICE ? "bitslice" : ran == OTC_IMPL_SPLIT ? "split"
                                                                                                           : "auto",
-           c.inplace ? "true" : "false", c.iters, ms, gbps, cpb, cus, clk_hz / 1e6, clk, verdict(c.verify, v));
+           c.inplace ? "true" : "false", c.iters, ms, gbps, cpb, cus, clk_hz / 1e6, clk, runtime_json().c_str(),
+           verdict(c.verify, v));
     otc_dev_free(a.in);
     if (!c.inplace) otc_dev_free(a.out);
     otc_dev_free(a.keys);

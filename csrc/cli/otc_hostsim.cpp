@@ -65,6 +65,11 @@ int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir)
 int otc_last_impl(void) { return OTC_IMPL_TTABLE; }
 void otc_split_stats(int) {}
 int otc_split_trace(int, unsigned long long *, int) { return -1; }
+int otc_runtime_info(char *buf, size_t n)
+{
+    const int w = snprintf(buf, n, "{\"hip_runtime_version\": -1, \"host_simulation\": true}");
+    return w < 0 || (size_t)w >= n ? OTC_ERR_ARG : OTC_OK;
+}
 int otc_split_last_units(uint64_t *f, uint64_t *b, uint64_t *n)
 {
     *f = *b = *n = 0;

@@ -11,7 +11,6 @@
 
 #include "aes.h"
 #include "otc_bitslice.h"
-#include "otc_bs8.h"
 
 using namespace otc_bs;
 
@@ -263,93 +262,4 @@ extern "C" int otc_bitslice_selftest(int verbose)
         }
     }
     return fails ? 1 : 0;
-}
-
-/* Row-sliced bs8 (otc_bs8.h), the chained segment-encryption kernel's
- * arithmetic on the host: 8 chains of `nb` blocks through the kernel's loop
- * (aes_bs8.hip bs8_task: planes -> words, store / add the plaintext, words
- * -> planes, rounds), against aes_crypt_cbc / aes_crypt_cfb128 per chain,
- * AES-128/192/256, CBC and CFB. */
-extern "C" int otc_bs8_selftest(int verbose)
-{
-    int fails = 0;
-    const int nb = 5;
-    for (int bits = 128; bits <= 256; bits += 64)
-        for (int cfb = 0; cfb < 2; ++cfb) {
-            uint8_t key[32], iv[8][16], pt[8][nb * 16], ct[8][nb * 16], ref[8][nb * 16];
-            uint64_t z = 0x2545F4914F6CDD1Dull * (uint64_t)(bits + cfb + 1);
-            auto rnd = [&]() {
-                z ^= z << 13;
-                z ^= z >> 7;
-                z ^= z << 17;
-                return (uint8_t)z;
-            };
-            for (auto &b : key) b = rnd();
-            for (int k = 0; k < 8; ++k) {
-                for (auto &b : iv[k]) b = rnd();
-                for (auto &b : pt[k]) b = rnd();
-            }
-            aes_context ctx;
-            aes_setkey_enc(&ctx, key, bits);
-            uint32_t rk[60];
-            aes_export_rk32(&ctx, rk);
-            const int nr = ctx.nr;
-            for (int k = 0; k < 8; ++k) {
-                uint8_t v[16];
-                memcpy(v, iv[k], 16);
-                int off = 0;
-                if (cfb) aes_crypt_cfb128(&ctx, AES_ENCRYPT, nb * 16, &off, v, pt[k], ref[k]);
-                else aes_crypt_cbc(&ctx, AES_ENCRYPT, nb * 16, v, pt[k], ref[k]);
-            }
-            auto word = [](const uint8_t *p) {
-                return (W)p[0] | (W)p[1] << 8 | (W)p[2] << 16 | (W)p[3] << 24;
-            };
-            const otc_bs8::HostKT kt{rk, nr};
-            auto rounds = [&](W *s) {
-                switch (nr) {
-                case 10: otc_bs8::rounds<10>(s, kt); break;
-                case 12: otc_bs8::rounds<12>(s, kt); break;
-                default: otc_bs8::rounds<14>(s, kt); break;
-                }
-            };
-            W s[32];
-            for (int k = 0; k < 8; ++k)
-                for (int c = 0; c < 4; ++c) s[8 * c + k] = word(iv[k] + 4 * c) ^ rk[4 * nr + c];
-            transpose32(s);
-            auto store = [&](int j) {
-                for (int k = 0; k < 8; ++k)
-                    for (int c = 0; c < 4; ++c) {
-                        const W w = s[8 * c + k] ^ rk[4 * nr + c];
-                        for (int i = 0; i < 4; ++i) ct[k][16 * j + 4 * c + i] = (uint8_t)(w >> (8 * i));
-                    }
-            };
-            auto add_pt = [&](int j) {
-                for (int k = 0; k < 8; ++k)
-                    for (int c = 0; c < 4; ++c) s[8 * c + k] ^= word(pt[k] + 16 * j + 4 * c);
-            };
-            if (cfb) rounds(s);
-            for (int j = 0; j < nb; ++j) {
-                transpose32(s);
-                if (cfb) {
-                    add_pt(j);
-                    store(j);
-                } else {
-                    if (j > 0) store(j - 1);
-                    add_pt(j);
-                }
-                if (cfb && j + 1 == nb) break;
-                transpose32(s);
-                rounds(s);
-            }
-            if (!cfb) {
-                transpose32(s);
-                store(nb - 1);
-            }
-            if (memcmp(ct, ref, sizeof ct)) {
-                if (verbose) printf("  bs8 %s AES-%d mismatch\n", cfb ? "CFB" : "CBC", bits);
-                ++fails;
-            }
-        }
-    if (verbose && !fails) printf("  bs8 CBC / CFB128 chains (AES-128/192/256): passed\n");
-    return fails;
 }

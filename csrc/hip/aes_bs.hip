@@ -347,6 +347,34 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
 #ifndef OTC_BS_PRE
 #define OTC_BS_PRE 2
 #endif
+/* Streaming cache policy for the bytes a task reads and writes once (round 6
+ * energy A/B, docs/PERF.md): 1 sets the non-temporal bit on the plaintext
+ * loads (LDS DMA and register slots) and the ciphertext stores, so the 64
+ * GiB stream does not allocate in L2 / MALL.  A compile-time switch
+ * (make variant VFLAGS=-DOTC_BS_NT=1); the release build takes the default. */
+#ifndef OTC_BS_NT
+#define OTC_BS_NT 0
+#endif
+constexpr int BS_LDS_AUX = OTC_BS_NT ? 2 : 0; /* CPol: NT (SLC) bit */
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_stream(const uint8_t *p)
+{
+    if constexpr (OTC_BS_NT) {
+        const u32x4 v = __builtin_nontemporal_load((const u32x4 *)p);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *(const uint4 *)p;
+    }
+}
+__device__ __forceinline__ void st_stream(uint8_t *p, uint4 v)
+{
+    if constexpr (OTC_BS_NT) {
+        const u32x4 w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, (u32x4 *)p);
+    } else {
+        *(uint4 *)p = v;
+    }
+}
 template <int NR, int MODE, int LS, bool CACHE, bool FO, int MIX = 2, int PRE = OTC_BS_PRE, int D = 8>
 __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key &K, uint4 *stage,
                                             int64_t claimed = -1)
@@ -375,7 +403,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
             const bool ok = full || (si >= 0 && (uint64_t)si < P.nblocks);
             __builtin_amdgcn_global_load_lds((const void *)(ok ? ib0 + 1024u * k : P.in),
                                              (__attribute__((address_space(3))) void *)&stage[(wave * LS + k) * 64],
-                                             16, 0, 0);
+                                             16, 0, BS_LDS_AUX);
         }
     }
     };
@@ -479,7 +507,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
                 const uint4 v = slot_ok(j) ? *(const uint4 *)(ib + lo + (first ? 0 : XOFF)) : make_uint4(0, 0, 0, 0);
                 pt[j] = blend_iv(v, first, P);
             } else {
-                pt[j] = slot_ok(j) ? *(const uint4 *)(ib + lo + 1024u * j + XOFF) : make_uint4(0, 0, 0, 0);
+                pt[j] = slot_ok(j) ? ld_stream(ib + lo + 1024u * j + XOFF) : make_uint4(0, 0, 0, 0);
             }
         }
     };
@@ -520,7 +548,7 @@ __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key
         if (slot_ok(k)) {
             const uint4 o = XIN ? ks_xor(k, k < LS ? stage[(wave * LS + k) * 64 + (lo >> 4)] : pt[k])
                                 : make_uint4(s[k] ^ k0, s[32 + k] ^ k1, s[64 + k] ^ k2, s[96 + k] ^ k3);
-            *(uint4 *)(ob + lo + 1024u * k) = o;
+            st_stream(ob + lo + 1024u * k, o);
         }
     }
 }

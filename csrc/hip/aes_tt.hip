@@ -819,7 +819,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg_g(CbcSegParams P, o
 /* The T-table half of the chained segment encryption split (engine.cpp
  * seg_enc_run): a claim unit is 64 segments, one per lane of a wave, taken
  * from the back; workgroup 0 first runs the segments past the last full unit.
- * The bitsliced half (aes_bs8.hip) takes 8 units at a time from the front. */
+ * It runs alone (engine.cpp seg_enc_run): no VALU half claims from the front. */
 constexpr uint32_t SEG_UNIT = 64;
 template <int NR, int G, bool CFB>
 __global__ __launch_bounds__(1024) OTC_CLAIM_ATTR void k_aes_seg_enc_tt_claim(CbcSegParams P, otc_aes_key K)

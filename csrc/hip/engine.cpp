@@ -57,11 +57,8 @@ hipError_t tt_cfb_encrypt_seg(const void *, void *, uint64_t, uint64_t, const ot
 hipError_t tt_cfb_decrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t tt_seg_encrypt_claim(bool, const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, SplitClaim,
                                 hipStream_t);
-hipError_t bs8_seg_encrypt_claim(bool, const void *, void *, uint64_t, const otc_aes_key &, Ctr128, SplitClaim,
-                                 hipStream_t);
 int strace_read_tt(unsigned long long *, int);
 int strace_read_bs(unsigned long long *, int);
-int strace_read_bs8(unsigned long long *, int);
 hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
 hipError_t tt_ctr_shift(const void *, void *, size_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t xor_small(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
@@ -234,6 +231,13 @@ struct AuxStream {
  * otc_multi_run) never share the events they order on */
 std::mutex g_aux_mu;
 std::vector<AuxStream> g_aux_free;
+/* AuxStreams created per device (in the pool or taken).  Each holds two
+ * dedicated hardware queues, so the pool is capped: past AUX_MAX concurrent
+ * split calls on one device a call runs the T-table alone and records why
+ * (otc_split_fallback_reason) instead of taking more device queues. */
+constexpr int AUX_MAX = 4;
+int g_aux_live[64];
+thread_local const char *g_split_fallback = "";
 
 hipError_t aux_take(int dev, AuxStream &out)
 {
@@ -245,6 +249,11 @@ hipError_t aux_take(int dev, AuxStream &out)
                 g_aux_free.erase(g_aux_free.begin() + (long)i);
                 return hipSuccess;
             }
+        if (dev < 0 || dev >= 64 || g_aux_live[dev] >= AUX_MAX) {
+            g_split_fallback = "auxiliary stream pool exhausted (AUX_MAX concurrent split calls on this device)";
+            return hipErrorOutOfMemory;
+        }
+        ++g_aux_live[dev]; /* reserved; released below if creation fails */
     }
     AuxStream a;
     a.dev = dev;
@@ -254,8 +263,15 @@ hipError_t aux_take(int dev, AuxStream &out)
      * the other half, and then the two kernels run one after the other: in
      * bench.py, beside torch's and RCCL's streams, the CTR split ran at the
      * T-table's speed (1534 GB/s) */
+#ifdef OTC_DIAG_POOLED_AUX
+    /* A/B arm only (make variant NAME=pooledaux VFLAGS=-DOTC_DIAG_POOLED_AUX):
+     * both halves on plain non-blocking streams, i.e. HIP's pooled queues */
+    hipError_t e = hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&a.t, hipStreamNonBlocking);
+#else
     hipError_t e = dedicated_stream_create(&a.s);
     if (e == hipSuccess) e = dedicated_stream_create(&a.t);
+#endif
     if (e == hipSuccess) e = hipEventCreateWithFlags(&a.fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&a.join, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&a.join_t, hipEventDisableTiming);
@@ -265,6 +281,9 @@ hipError_t aux_take(int dev, AuxStream &out)
         if (a.fork) (void)hipEventDestroy(a.fork);
         if (a.t) (void)hipStreamDestroy(a.t);
         if (a.s) (void)hipStreamDestroy(a.s);
+        std::lock_guard<std::mutex> lk(g_aux_mu);
+        --g_aux_live[dev];
+        g_split_fallback = "auxiliary stream creation failed";
         return e;
     }
     out = a;
@@ -324,13 +343,18 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
                        TT tt, BS bs, PLAIN plain)
 {
     *ran = OTC_IMPL_TTABLE;
-    if (nunits < (bs_only ? 1 : min_units) || nunits > 0x7FFFFFFFull) return plain();
+    g_split_fallback = "";
+    if (nunits < (bs_only ? 1 : min_units) || nunits > 0x7FFFFFFFull) {
+        g_split_fallback = "too few claim units";
+        return plain();
+    }
     unsigned long long *ctr = nullptr;
     /* word 0: the shared claim word; word 1 (bs_only): the T-table kernel's
      * own word, preset to "every unit taken" */
     hipError_t e = otc_dev::alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&ctr, 2 * sizeof *ctr, st);
     if (e != hipSuccess) {
         (void)hipGetLastError();
+        g_split_fallback = "no memory for the claim counter";
         return plain();
     }
     int dev = 0;
@@ -360,7 +384,10 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
          * join is recorded either way (a failure after its launch must still
          * be waited for). */
         const hipError_t eb = bs_wgs ? bs(cl, a.s) : hipSuccess;
-        if (eb != hipSuccess) (void)hipGetLastError();
+        if (eb != hipSuccess) {
+            (void)hipGetLastError();
+            g_split_fallback = "the bitsliced half failed to launch";
+        }
         if (fork && (e = hipEventRecord(a.join, a.s)) == hipSuccess && (e = hipEventRecord(a.join_t, a.t)) == hipSuccess &&
             (e = hipStreamWaitEvent(st, a.join, 0)) == hipSuccess)
             e = hipStreamWaitEvent(st, a.join_t, 0);
@@ -554,33 +581,21 @@ hipError_t seg_dec_split(bool cfb, const void *in, void *out, size_t seg_blocks,
 /* the kernel family the calling thread's last AES call ran (otc_last_impl) */
 thread_local int g_last_impl = OTC_IMPL_AUTO;
 
-/* Segment ENCRYPTION (CBC / CFB128, one serial chain per segment).  Three
- * forms: the grid T-table kernel; the persistent T-table claim kernel alone
- * (64-segment units from one counter, one workgroup per CU, no bitsliced
- * half); and the co-resident split with the row-sliced bs8 kernel
- * (aes_bs8.hip) taking 8-unit tasks from the front.  The bs8 split is
- * explicit only (impl "split" / "bitslice"): truly co-resident it LOSES at
- * every size -- a bs8 wave beside four T-table waves runs its 512-chain task
- * slowly, slows the latency-bound T-table chains, and its 8-unit tasks
- * outlast a 4 KiB-segment call (AES-256 4 GiB: 775 vs 1040 GB/s for the
- * claim kernel alone; profiles/r5/split_ab/remeasure_int_lds.jsonl).  auto
- * runs the T-table: the persistent kernel from 2 GiB (from 1 GiB for
- * segments <= 1 KiB), where it beats the grid kernel by 4-15% (AES-256 4 KiB
- * segments: 2 GiB 1027 vs 986, 4 GiB 1040 vs 969, 32 GiB 1142 vs 995; 512 B
- * at 1 GiB 986 vs 951; AES-128 4 GiB 1383 vs 1267), the grid kernel below
- * (1 GiB of 4 KiB segments: 916 vs 948; profiles/r5/split_thresholds/).
- * bs8 needs segments of < 8 MiB (32-bit lane offsets); at least 16 units
- * (1024 segments) to claim. */
+/* Segment ENCRYPTION (CBC / CFB128, one serial chain per segment): T-table
+ * kernels only, for every impl.  Two forms: the grid kernel, and the
+ * persistent claim kernel (64-segment units from one counter, one workgroup
+ * per CU, its LDS table filled once), from 2 GiB (from 1 GiB for segments <=
+ * 1 KiB), where it beats the grid kernel by 4-15% (AES-256 4 KiB segments:
+ * 2 GiB 1027 vs 986, 4 GiB 1040 vs 969, 32 GiB 1142 vs 995; 512 B at 1 GiB
+ * 986 vs 951; AES-128 4 GiB 1383 vs 1267); below that the grid kernel (1 GiB
+ * of 4 KiB segments: 916 vs 948; profiles/r5/split_thresholds/).  A VALU
+ * half for this mode (the row-sliced 8-chains-per-lane kernel of round 5)
+ * lost at every size -- AES-256 4 GiB 775 vs 1040 GB/s for the claim kernel
+ * alone (profiles/r5/split_ab/remeasure_int_lds.jsonl) -- and was removed
+ * in round 6 (profiles/r6/retired/). */
 constexpr uint64_t SEG_UNIT = 64;
-bool segenc_bs8_ok(size_t seg_bytes) { return seg_bytes >= 16 && seg_bytes * SEG_UNIT * 8 <= 0xFFFFFFFFull; }
 
-int pick_segenc_impl(int impl, size_t, size_t seg_bytes)
-{
-    if (!segenc_bs8_ok(seg_bytes)) return OTC_IMPL_TTABLE;
-    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_SPLIT) return impl;
-    const int env = env_impl();
-    return env != OTC_IMPL_AUTO ? env : OTC_IMPL_TTABLE;
-}
+int pick_segenc_impl(int, size_t, size_t) { return OTC_IMPL_TTABLE; }
 
 bool segenc_persistent(size_t nbytes, size_t seg_bytes, size_t nseg)
 {
@@ -589,25 +604,19 @@ bool segenc_persistent(size_t nbytes, size_t seg_bytes, size_t nseg)
 }
 
 hipError_t seg_enc_run(bool cfb, const void *in, void *out, size_t seg_bytes, size_t nseg, const otc_aes_key &K,
-                       Ctr128 iv0, int impl, hipStream_t st)
+                       Ctr128 iv0, hipStream_t st)
 {
     const size_t seg_blocks = seg_bytes / 16;
-    const int pick = pick_segenc_impl(impl, seg_bytes * nseg, seg_bytes);
-    g_last_impl = pick;
+    g_last_impl = OTC_IMPL_TTABLE;
     auto grid = [&]() {
         return cfb ? otc_impl::tt_cfb_encrypt_seg(in, out, seg_blocks, nseg, K, iv0, st)
                    : otc_impl::tt_cbc_encrypt_seg(in, out, seg_blocks, nseg, K, iv0, st);
     };
-    const bool persistent = pick == OTC_IMPL_TTABLE && segenc_persistent(seg_bytes * nseg, seg_bytes, nseg);
-    if (pick == OTC_IMPL_TTABLE && !persistent) return grid();
-    const bool bs_only = pick == OTC_IMPL_BITSLICE;
-    const unsigned bs_wgs = persistent ? 0u : (unsigned)otc_dev::device_cus() * (bs_only ? 4u : 1u);
+    if (!segenc_persistent(seg_bytes * nseg, seg_bytes, nseg)) return grid();
     return split_claim(
-        nseg / SEG_UNIT, 16, bs_only, bs_wgs, st, &g_last_impl,
+        nseg / SEG_UNIT, 16, false, 0u, st, &g_last_impl,
         [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_seg_encrypt_claim(cfb, in, out, seg_blocks, nseg, K, iv0, cl, ts); },
-        [&](SplitClaim cl, hipStream_t s) {
-            return otc_impl::bs8_seg_encrypt_claim(cfb, in, out, seg_blocks, K, iv0, cl, s);
-        },
+        [&](SplitClaim, hipStream_t) { return hipErrorInvalidValue; /* no VALU half: bs_wgs = 0 never calls it */ },
         grid);
 }
 
@@ -685,6 +694,7 @@ void otc_rt::aux_release_all()
         (void)hipEventDestroy(a.join_t);
         (void)hipStreamDestroy(a.s);
         (void)hipStreamDestroy(a.t);
+        if (a.dev >= 0 && a.dev < 64) --g_aux_live[a.dev];
     }
     g_aux_free.clear();
     (void)hipSetDevice(cur);
@@ -693,13 +703,15 @@ void otc_rt::aux_release_all()
 extern "C" int otc_last_impl(void) { return g_last_impl; }
 
 /* which: 0 the T-table kernels' records, 1 the bitsliced (32-block) claim
- * kernels', 2 bs8's; -1 in a build without OTC_SPLIT_TRACE */
+ * kernels'; -1 in a build without OTC_SPLIT_TRACE */
 extern "C" int otc_split_trace(int which, unsigned long long *buf, int max)
 {
     if (!buf || max < 0) return set_err(OTC_ERR_ARG, "bad trace buffer");
-    return which == 0 ? otc_impl::strace_read_tt(buf, max) : which == 1 ? otc_impl::strace_read_bs(buf, max)
-                                                                         : otc_impl::strace_read_bs8(buf, max);
+    if (which != 0 && which != 1) return set_err(OTC_ERR_ARG, "which must be 0 (T-table) or 1 (bitsliced)");
+    return which == 0 ? otc_impl::strace_read_tt(buf, max) : otc_impl::strace_read_bs(buf, max);
 }
+
+extern "C" const char *otc_split_fallback_reason(void) { return g_split_fallback; }
 
 extern "C" void otc_split_stats(int on) { g_split_stats.store(on ? 1 : 0, std::memory_order_relaxed); }
 
@@ -930,7 +942,7 @@ extern "C" int otc_aes_cbc_encrypt_segments_impl(const void *in, void *out, size
     if (nseg == 0 || seg_bytes == 0) return OTC_OK;
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
-    e = seg_enc_run(false, in, out, seg_bytes, nseg, *k, ctr_from_bytes(iv0), impl, st);
+    e = seg_enc_run(false, in, out, seg_bytes, nseg, *k, ctr_from_bytes(iv0), st);
     if (e != hipSuccess) return hip_fail(e, "cbc_encrypt_segments launch");
     return OTC_OK;
 }
@@ -999,7 +1011,7 @@ static int cfb_seg_common(const void *in, void *out, size_t seg_bytes, size_t ns
             e = otc_impl::tt_cfb_decrypt_seg(in, out, seg_bytes / 16, nseg, *k, ctr_from_bytes(iv0),
                                              (hipStream_t)stream);
     } else {
-        e = seg_enc_run(true, in, out, seg_bytes, nseg, *k, ctr_from_bytes(iv0), impl, (hipStream_t)stream);
+        e = seg_enc_run(true, in, out, seg_bytes, nseg, *k, ctr_from_bytes(iv0), (hipStream_t)stream);
     }
     if (e != hipSuccess) return hip_fail(e, what);
     return OTC_OK;

@@ -122,11 +122,11 @@ enum : int { BS_CTR = 0, BS_ECB = 1, BS_ECB_DEC = 2, BS_CBC_DEC = 3, BS_CFB_DEC 
  * Every claim is one atomic add on the whole word, valid iff front + back
  * units claimed before it < nunits, so the two ends never overlap and a
  * failed claim (nothing left) hides nothing.  A T-table claim adds one unit;
- * a front claim adds n units and gets [f, f + min(n, nunits - used)).
+ * a front claim adds one unit too.
  * Units: 2048 blocks for the whole-buffer modes (one bitsliced task; 1024-
  * block units and a reserve left to the T-table measured 1-11% slower and
- * were removed, profiles/r4/claim_unit/); 64 segments for the chained
- * segment encryption (one T-table wave; a bs8 task is 8 of them, aes_bs8.hip).
+ * were removed, profiles/r4/claim_unit/); 64 segments for the persistent
+ * segment-encryption kernel (one T-table wave, back claims only).
  * A wave claims with one lane (a vector-memory atomic) and broadcasts. */
 constexpr uint32_t CLAIM_UNIT = 2048u;
 struct SplitClaim {
@@ -174,18 +174,6 @@ __device__ __forceinline__ int64_t claim_unit(const SplitClaim &c, bool back)
     const uint32_t f = (uint32_t)old, b = (uint32_t)(old >> 32);
     if ((uint64_t)f + b >= c.nunits) return -1;
     return back ? (int64_t)(c.nunits - 1u - b) : (int64_t)f;
-}
-
-/* front claim of up to n units: the first unit, and *got = how many (1..n);
- * -1 when nothing is left */
-__device__ __forceinline__ int64_t claim_front(const SplitClaim &c, uint32_t n, uint32_t *got)
-{
-    const uint64_t old = claim_add(c, n);
-    const uint32_t f = (uint32_t)old, b = (uint32_t)(old >> 32);
-    const uint64_t used = (uint64_t)f + b;
-    if (used >= c.nunits) return -1;
-    *got = (uint32_t)(c.nunits - used < n ? c.nunits - used : n);
-    return (int64_t)f;
 }
 
 /* Wave-start trace of the splits (a diagnostic build: make variant

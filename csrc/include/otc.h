@@ -67,7 +67,7 @@ int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
 #define OTC_IMPL_BITSLICE 2 /* bitsliced VALU kernel alone: 32 blocks per lane (CTR, ECB, the decryptions; their
                                claim kernels take every 2048-block unit and one T-table workgroup the blocks past
-                               the last), 8 chains per lane for segment encryption (bs8) */
+                               the last); segment encryption has no VALU kernel and runs the T-table */
 #define OTC_IMPL_SPLIT 3    /* the T-table and the bitsliced kernel CONCURRENTLY over one buffer, each on a
                                pooled CU-masked stream, co-resident on every CU -- LDS and VALU busy at once --
                                claiming units from one counter: ECB, the CBC / CFB decryptions and the segment
@@ -93,10 +93,16 @@ int otc_last_impl(void);
  * such call, of nunits (2048-block units, or 64-segment units for segment
  * encryption).  Under impl "bitslice" front == nunits. */
 void otc_split_stats(int on);
+/* Why the calling thread's last split / bitsliced-claim request ran the
+ * T-table alone ("" when it did not fall back): too few claim units, no
+ * memory for the claim counter, the per-device pool of auxiliary streams
+ * exhausted (at most 4 concurrent split calls per device, each holding two
+ * dedicated hardware queues), or the bitsliced half failing to launch. */
+const char *otc_split_fallback_reason(void);
 int otc_split_last_units(uint64_t *front, uint64_t *back, uint64_t *nunits);
 /* Diagnostic builds only (-DOTC_SPLIT_TRACE=1): copy out and reset the
- * wave-start records of the split's kernels (which: 0 T-table, 1 bitsliced,
- * 2 bs8), pairs {s_memrealtime, tag << 32 | HW_ID}; returns the count, or -1
+ * wave-start records of the split's kernels (which: 0 T-table, 1 bitsliced),
+ * pairs {s_memrealtime, tag << 32 | HW_ID}; returns the count, or -1
  * in the shipped build. */
 int otc_split_trace(int which, unsigned long long *buf, int max);
 
@@ -151,17 +157,17 @@ int otc_aes_cbc_decrypt_impl(const void *in, void *out, size_t nbytes, const otc
  * A single segment (nseg == 1) is exact single-stream CBC, serial. */
 int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                  const otc_aes_key *k, const uint8_t iv0[16], void *stream);
-/* _impl: with a kernel choice.  OTC_IMPL_SPLIT: the T-table segment kernel
- * beside the row-sliced bs8 kernel (8 chains per lane), both claiming
- * 64-segment units; OTC_IMPL_BITSLICE: bs8 alone (the T-table runs the
- * segments past the last unit); "auto" splits from 896 MiB.  Segments of
- * >= 8 MiB and calls under 1024 segments: the T-table. */
+/* _impl: accepted for symmetry; every impl runs the T-table kernels (one
+ * serial chain per lane): the persistent claim kernel from 2 GiB (1 GiB for
+ * segments <= 1 KiB, at least 1024 segments), the grid kernel below.  A VALU
+ * kernel for this mode lost at every size and was removed (round 6). */
 int otc_aes_cbc_encrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                       const otc_aes_key *k, const uint8_t iv0[16], int impl, void *stream);
 /* Same, decryption side (fully parallel).  _impl: with a kernel choice --
- * "auto" runs the T-table + bitsliced split for >= 896 MiB of power-of-two
- * segments (OTC_IMPL_BITSLICE means the split here: the bitsliced segment
- * kernels run only beside the T-table); other segment sizes: T-table. */
+ * "auto" runs the T-table + bitsliced split from 2 GiB of power-of-two
+ * segments and the persistent T-table claim kernel alone from 896 MiB;
+ * OTC_IMPL_BITSLICE runs the bitsliced segment claim kernel alone; other
+ * segment sizes: T-table. */
 int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                  const otc_aes_key *k, const uint8_t iv0[16], void *stream);
 int otc_aes_cbc_decrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
@@ -416,8 +422,6 @@ int otc_multi_ctr_resident(int ngpus, void *const *dev_bufs, size_t shard_bytes,
 
 /* Library self description / tests */
 int otc_bitslice_selftest(int verbose);
-/* the row-sliced chain kernel's arithmetic (otc_bs8.h) against the C oracle */
-int otc_bs8_selftest(int verbose);
 const char *otc_build_info(void);
 /* JSON object naming the HIP runtime / driver and RCCL versions this process
  * runs on and the mapped libamdhip64 / librccl paths (/proc/self/maps): in a

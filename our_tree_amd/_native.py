@@ -146,7 +146,6 @@ def _declare_cpu(lib):
         "AES_CTR_encrypt": (None, [c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int]),
         "AES_CTR_encrypt_at": (None, [c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_ulong, c_u8p, c_int, ctypes.c_ulonglong]),
         "otc_bitslice_selftest": (c_int, [c_int]),
-        "otc_bs8_selftest": (c_int, [c_int]),
         "otc_rccl_nrounds": (c_u64, [c_u64, c_int, c_u64]),
         "otc_rccl_plan_piece": (c_int, [c_u64, c_int, c_u64, c_u64, c_int, P(RcclPiece)]),
         "otc_rccl_halo_start": (c_u64, [c_u64, c_u64, c_u64]),
@@ -178,6 +177,7 @@ def _declare_gpu(lib):
         "otc_pick_impl": (c_int, [c_int, c_int, c_int, c_u64]),
         "otc_last_impl": (c_int, []),
         "otc_split_stats": (None, [c_int]),
+        "otc_split_fallback_reason": (ctypes.c_char_p, []),
         "otc_split_last_units": (c_int, [ctypes.POINTER(c_u64), ctypes.POINTER(c_u64), ctypes.POINTER(c_u64)]),
         "otc_aes_key_init": (c_int, [K, c_u8p, c_int, c_int]),
         "otc_aes_ecb": (c_int, [c_vp, c_vp, c_sz, K, c_int, c_vp]),

@@ -203,5 +203,4 @@ def self_tests(verbose: int = 0) -> dict:
         "aes": lib.aes_self_test(verbose),
         "arc4": lib.arc4_self_test(verbose),
         "bitslice": lib.otc_bitslice_selftest(verbose),
-        "bs8": lib.otc_bs8_selftest(verbose),
     }

@@ -51,6 +51,12 @@ def last_impl() -> str:
     return _IMPL_NAMES[_lib().otc_last_impl()]
 
 
+def split_fallback_reason() -> str:
+    """Why the calling thread's last split / bitsliced-claim request ran the
+    T-table alone ("" if it did not fall back; otc.h otc_split_fallback_reason)."""
+    return (_lib().otc_split_fallback_reason() or b"").decode()
+
+
 def _check_dev(t: torch.Tensor, name: str):
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name} must be a torch.Tensor")
@@ -469,8 +475,9 @@ def ecb_encrypt(x: torch.Tensor, key: bytes, out=None, impl="auto") -> torch.Ten
 
 def ecb_decrypt(x: torch.Tensor, key: bytes, out=None, impl="auto") -> torch.Tensor:
     """ECB decryption: the T-table inverse cipher, the bitsliced one (the
-    forward S-box as S^-1 = L S L), or both concurrently ("split", auto from
-    896 MiB)."""
+    forward S-box as S^-1 = L S L), or both concurrently ("split").  "auto":
+    the split from 2 GiB, the persistent T-table claim kernel alone from 896
+    MiB, the grid T-table below (engine.cpp pick_ecb_impl / split_form)."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     k = expand_key(key, decrypt=True)
@@ -498,10 +505,10 @@ def cbc_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None, impl="auto") -
 def cbc_encrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes: int, out=None,
                          impl="auto") -> torch.Tensor:
     """CBC encryption of independent contiguous segments; segment s uses
-    IV = iv0 + s (128-bit BE), one serial chain per segment.  ``impl``:
-    "ttable" (one chain per lane), "bitslice" (the row-sliced bs8 kernel, 8
-    chains per lane), "split" (both at once over the buffer, claiming
-    64-segment units) or "auto" (split from 896 MiB of segments < 8 MiB).  A
+    IV = iv0 + s (128-bit BE), one serial chain per segment, one chain per
+    lane on the T-table kernels for every ``impl`` (the persistent claim
+    kernel from 2 GiB -- 1 GiB for segments <= 1 KiB -- the grid kernel
+    below; a VALU kernel for this mode lost at every size and was removed).  A
     single segment is exact serial CBC on ONE lane -- use
     ``models.AES.cbc_encrypt`` (routes exact single-stream encryption to the
     host AES-NI chain) unless the buffer is small.  May run in place."""
@@ -512,8 +519,8 @@ def cbc_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes:
                          impl="auto") -> torch.Tensor:
     """Inverse of ``cbc_encrypt_segments``: fully parallel.  ``impl``:
     "ttable", "bitslice" (the bitsliced claim kernel alone), "split" (both at
-    once), "auto" = split from 896 MiB of power-of-two segments (other
-    segment sizes: the T-table)."""
+    once), "auto" = split from 2 GiB of power-of-two segments, the persistent
+    T-table claim kernel from 896 MiB (other segment sizes: the T-table)."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     n = _nbytes(x)
@@ -531,7 +538,7 @@ def cfb128_decrypt(x: torch.Tensor, key: bytes, iv: bytes, out=None, impl="auto"
     """Parallel CFB128 decryption, P_i = C_i ^ E(C_{i-1}) (encryption key).
     ``impl``: "ttable", "bitslice" (the forward bitsliced cipher on the input
     shifted one block), "split" (both at once, as ECB encryption) or "auto"
-    (split from 896 MiB).  In place runs through a copy of the input."""
+    (as ecb_decrypt).  In place runs through a copy of the input."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     k = expand_key(key)

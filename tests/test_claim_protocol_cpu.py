@@ -2,30 +2,25 @@
 claim_unit / claim_front), modelled on the CPU: one 64-bit word, front
 (bitsliced) count in the low half, back (T-table) count in the high half,
 every claim one atomic add.  Any interleaving of claims must hand out every
-unit exactly once -- front claims of n units (1 for the 2048-block split, 8
-for the bs8 segment-encryption kernel, which gets a partial task at the
-meeting point) and back claims of one -- and a failed claim takes nothing."""
+unit exactly once -- front and back claims of one unit each -- and a failed
+claim takes nothing."""
 import random
 
 import pytest
 
 
-def claim(counter, nunits, back, n=1):
+def claim(counter, nunits, back):
     """one atomic add; returns (new counter, list of units claimed)"""
     f, b = counter & 0xFFFFFFFF, counter >> 32
-    counter += (1 << 32) if back else n
-    used = f + b
-    if used >= nunits:
+    counter += (1 << 32) if back else 1
+    if f + b >= nunits:
         return counter, []
-    if back:
-        return counter, [nunits - 1 - b]
-    got = min(n, nunits - used)
-    return counter, list(range(f, f + got))
+    return counter, [nunits - 1 - b] if back else [f]
 
 
-@pytest.mark.parametrize("n", [1, 8])
-def test_every_unit_exactly_once(n):
-    rnd = random.Random(1234 + n)
+@pytest.mark.parametrize("seed", [1235, 1242])
+def test_every_unit_exactly_once(seed):
+    rnd = random.Random(seed)
     for _ in range(300):
         nunits = rnd.randint(1, 300)
         counter, seen, front = 0, [], []
@@ -33,7 +28,7 @@ def test_every_unit_exactly_once(n):
         live = list(waves)
         while live:
             w = rnd.randrange(len(live))  # any wave may claim next: the atomics' order
-            counter, us = claim(counter, nunits, live[w] == "b", n)
+            counter, us = claim(counter, nunits, live[w] == "b")
             if not us:
                 live.pop(w)  # a wave whose claim failed exits its loop
             elif live[w] == "f":
@@ -42,24 +37,6 @@ def test_every_unit_exactly_once(n):
         assert sorted(seen) == list(range(nunits)), (nunits, waves)  # all, none twice
         # the bitsliced side holds a prefix, the T-table side the matching suffix
         assert sorted(front) == list(range(len(front)))
-
-
-def test_front_partial_task_at_the_meeting_point():
-    """A bs8 front claim with fewer than 8 units left gets exactly the rest
-    (its chains past the claim load chain 0 and store nothing), and later
-    claims of either side fail."""
-    counter = 0
-    counter, us = claim(counter, 19, False, 8)
-    assert us == list(range(8))
-    counter, us = claim(counter, 19, True)
-    assert us == [18]
-    counter, us = claim(counter, 19, False, 8)
-    assert us == list(range(8, 16))
-    counter, us = claim(counter, 19, False, 8)
-    assert us == [16, 17]
-    for back in (True, False):
-        counter, us = claim(counter, 19, back, 8)
-        assert us == []
 
 
 def test_bitsliced_only_mode():
@@ -72,7 +49,7 @@ def test_bitsliced_only_mode():
     assert us == []
     counter, seen = 0, []
     while True:
-        counter, us = claim(counter, nunits, False, 8)
+        counter, us = claim(counter, nunits, False)
         if not us:
             break
         seen += us

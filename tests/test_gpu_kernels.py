@@ -516,14 +516,12 @@ def test_split_bitsliced_alone(gpu, k):
 
 
 @pytest.mark.parametrize("bits", KEYBITS)
-def test_segment_encrypt_split_matches_oracle(gpu, bits):
-    """CBC / CFB128 ENCRYPTION of independent segments through the row-sliced
-    bs8 kernel (8 chains per lane, aes_bs8.hip) -- alone ("bitslice") and
-    beside the T-table claim kernel ("split", 64-segment units from one
-    counter) -- equals the T-table kernel and the CPU oracle: 1-block,
-    512-byte, non-power-of-two and 4 KiB segments, a unit count that leaves a
-    partial last bs8 task, segments past the last unit (T-table workgroup 0),
-    an IV_s carry across the low 64 bits, in place and out of place."""
+def test_segment_encrypt_matches_oracle(gpu, bits):
+    """CBC / CFB128 ENCRYPTION of independent segments runs the T-table
+    kernels for every impl (the row-sliced VALU kernel was retired in round
+    6: engine.cpp seg_enc_run) and equals the CPU oracle: 1-block, 512-byte,
+    non-power-of-two and 4 KiB segments, an IV_s carry across the low 64
+    bits, in place and out of place."""
     key = os.urandom(bits // 8)
     iv0 = os.urandom(8) + (2**64 - 700).to_bytes(8, "big")
     for seg, nseg in ((16, 64 * 19 + 37), (512, 64 * 19 + 37), (528, 64 * 17 + 5), (4096, 64 * 40 + 63),
@@ -537,45 +535,48 @@ def test_segment_encrypt_split_matches_oracle(gpu, bits):
             ref = cpu_ref.cbc_segments if name == "cbc" else cpu_ref.cfb128_segments
             t = f(x, key, iv0, seg, impl="ttable")
             assert ops.last_impl() == "ttable"
-            for impl in ("bitslice", "split"):
+            for impl in ("auto", "bitslice", "split"):
                 y = f(x, key, iv0, seg, impl=impl)
-                assert ops.last_impl() == impl, (name, seg, nseg, impl)
-                w = x.clone()
-                f(w, key, iv0, seg, out=w, impl=impl)
-                torch.cuda.synchronize()
+                assert ops.last_impl() == "ttable", (name, seg, nseg, impl)
                 assert torch.equal(y, t), (name, bits, seg, nseg, impl)
-                assert torch.equal(w, t), (name, bits, seg, nseg, impl, "in place")
+            w = x.clone()
+            f(w, key, iv0, seg, out=w)
+            torch.cuda.synchronize()
+            assert torch.equal(w, t), (name, bits, seg, nseg, "in place")
             hy = host(t)
             for s0 in (0, nseg // 2, nseg - 4):
                 lo, hi = s0 * seg, (s0 + 4) * seg
                 assert hy[lo:hi] == ref(key, sh.ctr_add(iv0, s0), hx[lo:hi], seg), (name, bits, seg, s0)
-    # auto never picks the bs8 split: it loses at every size (engine.cpp seg_enc_run)
     for n in (896 << 20, 4 << 30, 64 << 30):
-        assert ops.pick_impl("auto", 256, "seg-enc", n) == "ttable"
+        for impl in ("auto", "bitslice", "split"):
+            assert ops.pick_impl(impl, 256, "seg-enc", n) == "ttable"
 
 
 @pytest.mark.parametrize("seg", [512, 1024])
 def test_segment_encrypt_persistent_ttable(gpu, seg):
     """Segment encryption of >= 4 GiB in segments of <= 1 KiB runs the
-    persistent T-table claim kernel alone (64-segment units from one counter,
-    the segments past the last unit in workgroup 0): byte-identical to the
-    bs8 kernel alone and, on sampled segments, to the CPU oracle, CBC and
-    CFB, in place."""
+    persistent T-table claim kernel (64-segment units from one counter, the
+    segments past the last unit in workgroup 0): two 32 MiB windows -- one
+    inside the claimed units, one covering the partial last unit -- equal the
+    grid kernel run on that window alone (IV iv0 + s0), sampled segments equal
+    the CPU oracle, CBC and CFB, in place."""
     key = os.urandom(32)
     iv0 = os.urandom(8) + (2**64 - 3).to_bytes(8, "big")
     nseg = ((4 << 30) + 64 * 7 * seg + 5 * seg) // seg  # a partial last unit
     n = nseg * seg
     x = torch.empty(n, dtype=torch.uint8, device=gpu)
     ops.fill_random_(x, seed=seg)
+    win = (32 << 20) // seg
     for name in ("cbc", "cfb"):
         f = ops.cbc_encrypt_segments if name == "cbc" else ops.cfb128_encrypt_segments
         ref = cpu_ref.cbc_segments if name == "cbc" else cpu_ref.cfb128_segments
         y = f(x, key, iv0, seg)
         assert ops.last_impl() == "ttable"
-        b = f(x, key, iv0, seg, impl="bitslice")
-        torch.cuda.synchronize()
-        assert torch.equal(y, b), (name, seg)
-        del b
+        for s0 in (nseg // 3, nseg - win):
+            lo, hi = s0 * seg, (s0 + win) * seg
+            g = f(x[lo:hi], key, sh.ctr_add(iv0, s0), seg)
+            torch.cuda.synchronize()
+            assert torch.equal(g, y[lo:hi]), (name, seg, s0, "window")
         for s0 in (0, nseg // 3, nseg - 70, nseg - 4):
             lo, hi = s0 * seg, (s0 + 4) * seg
             assert host(y[lo:hi]) == ref(key, sh.ctr_add(iv0, s0), host(x[lo:hi]), seg), (name, seg, s0)

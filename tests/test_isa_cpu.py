@@ -157,7 +157,7 @@ def test_descriptors_match_register_use():
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import isa_count
 
-    objs = [os.path.join(ROOT, "build", "obj", "hip", f"{o}.o") for o in ("aes_tt", "aes_bs", "aes_bs8")]
+    objs = [os.path.join(ROOT, "build", "obj", "hip", f"{o}.o") for o in ("aes_tt", "aes_bs")]
     if not all(os.path.exists(o) for o in objs) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):
         pytest.skip("no built objects (make) or no ROCm LLVM tools")
     seen = 0
@@ -171,31 +171,6 @@ def test_descriptors_match_register_use():
                 assert v == -(-used // 8) * 8, (k, v, used)
                 seen += 1
     assert seen >= 30
-
-
-def test_bs8_segment_pair_shares_a_simd():
-    """The chained segment-encryption split: the row-sliced bs8 kernel
-    (csrc/hip/aes_bs8.hip, no scratch) fits one wave per SIMD beside the 4
-    waves of the T-table segment claim kernel (single-buffered 8-block
-    bursts, <= 72 allocated), for CBC and CFB at every key size, counted
-    from the kernel descriptors."""
-    tt_obj = os.path.join(ROOT, "build", "obj", "hip", "aes_tt.o")
-    bs8_obj = os.path.join(ROOT, "build", "obj", "hip", "aes_bs8.o")
-    if not os.path.exists(tt_obj) or not os.path.exists(bs8_obj) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):
-        pytest.skip("no built objects (make) or no ROCm LLVM tools")
-    tt, b8 = _vgprs(tt_obj), _vgprs(bs8_obj)
-    alloc = lambda n: -(-n // 8) * 8
-    seen = 0
-    for nr in (10, 12, 14):
-        for cfb in ("0", "1"):
-            tn = [k for k in tt if "k_aes_seg_enc_tt_claim" in k and f"ILi{nr}E" in k and f"ELb{cfb}E" in k]
-            bn = [k for k in b8 if "k_aes_bs8_seg_claim" in k and f"ILi{nr}ELb{cfb}E" in k]
-            assert tn and bn, (nr, cfb, sorted(b8))
-            t, b = max(tt[k][0] for k in tn), max(b8[k][0] for k in bn)
-            assert all(b8[k][1] == 0 for k in bn), (nr, cfb, b)
-            assert 4 * alloc(t) + alloc(b) <= 512, (nr, cfb, t, b)
-            seen += 1
-    assert seen == 6
 
 
 def test_ttable_claim_kernels_have_no_static_lds():

@@ -20,8 +20,8 @@ def main(argv=None):
     rows = db.execute("select name, start, end from kernels order by start").fetchall()
     # the static split's kernels, or the claimed split's (k_aes_*_tt_claim, k_aes_bs_claim)
     tt = [(s, e) for n, s, e in rows if any(k in n for k in ("k_aes_enc_tt", "k_aes_dec_tt", "_tt_claim"))]
-    bsnames = [n for n, s, e in rows if "bs_claim" in n or "bs8" in n]
-    bs = [(s, e) for n, s, e in rows if "k_aes_bs_t3" in n or "k_aes_bs_claim" in n or "k_aes_bs8_seg_claim" in n]
+    bsnames = [n for n, s, e in rows if "bs_claim" in n]
+    bs = [(s, e) for n, s, e in rows if "k_aes_bs_t3" in n or "k_aes_bs_claim" in n]
     if not tt or not bs:
         print(f"{a.label}: no split calls (tt {len(tt)}, bs {len(bs)})")
         return 0
