@@ -595,42 +595,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     }
 }
 
-/* CTR beside the T-table CTR claim kernel (engine.cpp ctr_split): the full
- * 2048-block tasks from the front (unit u = task u + 1 when the counter does
- * not start a task), counter caching as the bulk kernel, 8 plaintext slots
- * per wave staged in LDS (32 KiB: with the T-table's 128 KiB the CU's 160). */
-/* LDS-staged plaintext slots per wave in the CTR claim kernel: 4 (16 KiB per
- * workgroup).  With 8 (32 KiB, 160 KiB with the T-table's table) the two
- * kernels never shared a CU; 4 and 6 co-ran at the same speed
- * (profiles/r5/ctr_split/ls_ab.jsonl, lds32k_ab.jsonl) */
-constexpr int CTR_CLAIM_LS = 4;
-template <int NR, bool CACHE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_aes_bs_ctr_claim(BsParams P,
-                                                                                                   otc_aes_key K)
-{
-    __shared__ uint4 stage[4 * CTR_CLAIM_LS * 64];
-    strace(3);
-    const int64_t t0 = P.shift ? 1 : 0;
-    for (;;) {
-        const int64_t u = claim_unit(P.cl, false);
-        if (u < 0) break;
-        BsParams Q = P;
-        auto gin = (__attribute__((address_space(1))) const uint8_t *)P.in;
-        auto gout = (__attribute__((address_space(1))) uint8_t *)P.out;
-        asm volatile("" : "+s"(gin), "+s"(gout));
-        Q.in = (const uint8_t *)gin;
-        Q.out = (uint8_t *)gout;
-        /* the task index addresses the scalar-loaded tables: keep it in SGPRs */
-        const uint64_t task = (uint64_t)(u + t0);
-        const uint32_t tlo = __builtin_amdgcn_readfirstlane((uint32_t)task),
-                       thi = __builtin_amdgcn_readfirstlane((uint32_t)(task >> 32));
-        aes_bs_task<NR, BS_CTR, CTR_CLAIM_LS, CACHE, true>(Q, K, stage, (int64_t)(((uint64_t)thi << 32) | tlo));
-    }
-}
-
 template <int NR, int MODE>
-hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st, BsCtrPrep *pre = nullptr,
-                     bool prep_only = false)
+hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
 {
     const uint64_t vt = P.nblocks + (MODE == BS_CTR ? P.shift : 0);
     const uint64_t tasks = (vt + 2047) / 2048;
@@ -651,23 +617,16 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st, Bs
      * without counter caching rather than failing. */
     uint32_t *tab = nullptr;
     hipError_t e = hipErrorOutOfMemory;
-    const bool built = pre && !prep_only; /* the tables came from a prep_only call */
-    if (built) {
-        tab = pre->tab;
-        cache = pre->cache;
-    } else {
-        if (cache) {
-            e = alloc_fault() ? hipErrorOutOfMemory
-                              : hipMallocAsync((void **)&tab, (kt_words + ctab_words) * 4, st);
-            if (e != hipSuccess) {
-                (void)hipGetLastError();
-                cache = false;
-            }
+    if (cache) {
+        e = alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&tab, (kt_words + ctab_words) * 4, st);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            cache = false;
         }
-        if (!cache) e = alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&tab, kt_words * 4, st);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_bs_key_table<MODE == BS_ECB_DEC || is_cbcd<MODE>>, dim3(1), dim3(256), 0, st, K, tab);
     }
+    if (!cache) e = alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&tab, kt_words * 4, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bs_key_table<MODE == BS_ECB_DEC || is_cbcd<MODE>>, dim3(1), dim3(256), 0, st, K, tab);
     BsParams Q = P;
     Q.ktab = tab;
     Q.tasks = tasks;
@@ -695,11 +654,6 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st, Bs
         auto run = [&](auto cachec) {
             constexpr bool C = decltype(cachec)::value;
             Q.part = BS_FULL_ONLY;
-            if (P.cl.ctr) { /* the bitsliced half of the CTR split: full tasks only */
-                hipLaunchKernelGGL((k_aes_bs_ctr_claim<NR, C>),
-                                   dim3(P.cl.wgs ? P.cl.wgs : (unsigned)otc_dev::device_cus()), b, 0, st, Q, K);
-                return;
-            }
             hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, true>), g, b, 0, st, Q, K);
             if (edge) {
                 Q.part = BS_EDGE_ONLY;
@@ -713,15 +667,8 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st, Bs
             Q.e0tab = e0;
             Q.e1tab = e1;
             const uint64_t n = ngroups * 65 + tasks;
-            if (!built)
-                hipLaunchKernelGGL(k_bs_ctr_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, P.cbase,
-                                   P.wrap64, ngroups, tasks, gt, e0, e1);
-        }
-        if (prep_only) { /* tables only: handed to the claim launch */
-            pre->tab = tab;
-            pre->cache = cache;
-            pre->tasks = tasks;
-            return hipGetLastError();
+            hipLaunchKernelGGL(k_bs_ctr_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, P.cbase,
+                               P.wrap64, ngroups, tasks, gt, e0, e1);
         }
         if (cache)
             run(std::true_type{});
@@ -734,13 +681,12 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st, Bs
 }
 
 template <int MODE>
-hipError_t launch(const BsParams &P, const otc_aes_key &K, hipStream_t st, BsCtrPrep *pre = nullptr,
-                  bool prep_only = false)
+hipError_t launch(const BsParams &P, const otc_aes_key &K, hipStream_t st)
 {
     switch (K.nr) {
-    case 10: return launch_nr<10, MODE>(P, K, st, pre, prep_only);
-    case 12: return launch_nr<12, MODE>(P, K, st, pre, prep_only);
-    case 14: return launch_nr<14, MODE>(P, K, st, pre, prep_only);
+    case 10: return launch_nr<10, MODE>(P, K, st);
+    case 12: return launch_nr<12, MODE>(P, K, st);
+    case 14: return launch_nr<14, MODE>(P, K, st);
     default: return hipErrorInvalidValue;
     }
 }
@@ -797,43 +743,6 @@ hipError_t bs_claim(int mode, const void *in, void *out, uint64_t nblocks, const
     case BS_CFB_DEC: return launch<BS_CFB_DEC>(P, K, st);
     default: return hipErrorInvalidValue;
     }
-}
-
-/* ... and of the CTR split: the full tasks of the counter's 2048-block task
- * grid (nblocks full blocks from counter c) */
-static BsParams ctr_params(const void *in, void *out, uint64_t nblocks, Ctr128 c, bool wrap64, SplitClaim cl)
-{
-    BsParams P{};
-    P.in = (const uint8_t *)in;
-    P.out = (uint8_t *)out;
-    P.nblocks = nblocks;
-    P.wrap64 = wrap64 ? 1u : 0u;
-    P.shift = c.lo & 2047u;
-    P.cbase.lo = c.lo & ~(uint64_t)2047u;
-    P.cbase.hi = c.hi;
-    P.cl = cl;
-    return P;
-}
-
-/* build the tables on st; *pre owns them until bs_ctr_claim (or
- * bs_ctr_discard) frees them */
-hipError_t bs_ctr_prepare(uint64_t nblocks, const otc_aes_key &K, Ctr128 c, bool wrap64, hipStream_t st,
-                          BsCtrPrep *pre)
-{
-    SplitClaim none{};
-    return launch<BS_CTR>(ctr_params(nullptr, nullptr, nblocks, c, wrap64, none), K, st, pre, true);
-}
-
-hipError_t bs_ctr_claim(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, Ctr128 c, bool wrap64,
-                        BsCtrPrep *pre, SplitClaim cl, hipStream_t st)
-{
-    return launch<BS_CTR>(ctr_params(in, out, nblocks, c, wrap64, cl), K, st, pre, false);
-}
-
-void bs_ctr_discard(BsCtrPrep *pre, hipStream_t st)
-{
-    if (pre && pre->tab) (void)hipFreeAsync(pre->tab, st);
-    if (pre) pre->tab = nullptr;
 }
 
 /* ... and of a claimed split over independent segments of 2^seg_shift

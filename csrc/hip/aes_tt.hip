@@ -270,20 +270,18 @@ __device__ __forceinline__ void st16(uint8_t *p, uint64_t blk, uint4 v)
 {
     *reinterpret_cast<uint4 *>(p + 16 * blk) = v;
 }
-enum : int { E_ECB = 0, E_CFB_DEC = 2, E_CFB_DEC_SEG = 3, E_CTR = 4 };
+enum : int { E_ECB = 0, E_CFB_DEC = 2, E_CFB_DEC_SEG = 3 };
 enum : int { D_ECB = 0, D_CBC = 1, D_CBC_SEG = 2 };
 
 struct EncParams {
     const uint8_t *in;
     uint8_t *out;
     uint64_t nfull;   /* full 16-byte blocks */
-    Ctr128 ctr;       /* CFB_DEC_SEG: IV of segment 0 (IV_s = ctr + s); CTR: the counter of block 0 */
+    Ctr128 ctr;       /* CFB_DEC_SEG: IV of segment 0 (IV_s = ctr + s) */
     uint32_t iv[4];   /* CFB: IV as LE words */
     uint64_t seg_blocks; /* CFB_DEC_SEG: blocks per segment */
     uint32_t seg_shift;  /* CFB_DEC_SEG: log2(seg_blocks), or 64 if not a power of two */
-    uint32_t wrap64;     /* CTR: 64-bit counter increment */
     SplitClaim cl;       /* CLAIM kernels: units taken from the back of the buffer */
-    uint64_t head;       /* CLAIM: unit u is blocks head + u * 2048 (CTR: the bitsliced kernel's task grid) */
 };
 
 struct DecParams {
@@ -355,10 +353,7 @@ __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_ke
         for (int b = 0; b < B; ++b) {
             const uint64_t i = i0 + 64u * b;
             const bool ok = full || i < lim;
-            if (MODE == E_CTR) {
-                x[b] = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
-                ctr_words(P.ctr, i, P.wrap64 != 0, s[b][0], s[b][1], s[b][2], s[b][3]);
-            } else if (MODE == E_ECB) {
+            if (MODE == E_ECB) {
                 uint4 v = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
                 s[b][0] = v.x; s[b][1] = v.y; s[b][2] = v.z; s[b][3] = v.w;
             } else if (MODE == E_CFB_DEC) { /* cipher input is the previous ciphertext */
@@ -397,18 +392,16 @@ __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_ke
 
     if constexpr (CLAIM) {
         strace(1);
-        /* the blocks outside the units -- [0, head) and past the last one --
-         * workgroup 0, first */
-        const uint64_t done = P.head + (uint64_t)P.cl.nunits * CLAIM_UNIT;
+        /* the blocks past the last unit: workgroup 0, first */
+        const uint64_t done = (uint64_t)P.cl.nunits * CLAIM_UNIT;
         if (blockIdx.x == 0) {
-            for (uint64_t base = 0; base < P.head; base += PER) chunk(base + (uint64_t)wave * 64u * B + lane, false, P.head);
             for (uint64_t base = done; base < P.nfull; base += PER)
                 chunk(base + (uint64_t)wave * 64u * B + lane, false, P.nfull);
         }
         for (;;) {
             const int64_t u = claim_unit(P.cl, true);
             if (u < 0) break;
-            const uint64_t u0 = P.head + (uint64_t)u * CLAIM_UNIT;
+            const uint64_t u0 = (uint64_t)u * CLAIM_UNIT;
 #pragma unroll 1
             for (uint32_t it = 0; it < CLAIM_UNIT / (64u * B); ++it) chunk(u0 + it * 64u * B + lane, true, 0);
         }
@@ -446,13 +439,6 @@ template <int NR>
 __global__ __launch_bounds__(1024) OTC_CLAIM_ATTR void k_aes_cfb_tt_claim(EncParams P, otc_aes_key K)
 {
     enc_tt_body<NR, E_CFB_DEC, OTC_TT_CLAIM_B, 1024, true>(P, K);
-}
-/* CTR beside the bitsliced CTR claim kernel (counter caching on that side,
- * 32 KiB of LDS staging: 128 + 32 KiB fill the CU) */
-template <int NR>
-__global__ __launch_bounds__(1024) OTC_CLAIM_ATTR void k_aes_ctr_tt_claim(EncParams P, otc_aes_key K)
-{
-    enc_tt_body<NR, E_CTR, OTC_TT_CLAIM_B, 1024, true>(P, K);
 }
 template <int NR>
 __global__ __launch_bounds__(1024) OTC_CLAIM_ATTR void k_aes_cfbseg_tt_claim(EncParams P, otc_aes_key K)
@@ -1235,7 +1221,6 @@ hipError_t launch_enc_claim(const EncParams &P, const otc_aes_key &K, hipStream_
     auto go = [&](auto nr) {
         constexpr int NR = decltype(nr)::value;
         if constexpr (MODE == E_ECB) return launch_dyn<k_aes_ecb_tt_claim<NR>>(g, b, ENC_LDS, st, P, K);
-        else if constexpr (MODE == E_CTR) return launch_dyn<k_aes_ctr_tt_claim<NR>>(g, b, ENC_LDS, st, P, K);
         else if constexpr (MODE == E_CFB_DEC) return launch_dyn<k_aes_cfb_tt_claim<NR>>(g, b, ENC_LDS, st, P, K);
         else return launch_dyn<k_aes_cfbseg_tt_claim<NR>>(g, b, ENC_LDS, st, P, K);
     };
@@ -1406,22 +1391,6 @@ hipError_t tt_ecb_encrypt_claim(const void *in, void *out, uint64_t nblocks, con
     P.nfull = nblocks;
     P.cl = cl;
     return launch_enc_claim<E_ECB>(P, K, st);
-}
-
-/* the T-table half of the CTR split: units of 2048 blocks from `head`
- * (the bitsliced kernel's full tasks), the blocks outside them in workgroup 0 */
-hipError_t tt_ctr_claim(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K, Ctr128 c, bool wrap64,
-                        uint64_t head, SplitClaim cl, hipStream_t st)
-{
-    EncParams P{};
-    P.in = (const uint8_t *)in;
-    P.out = (uint8_t *)out;
-    P.nfull = nblocks;
-    P.ctr = c;
-    P.wrap64 = wrap64 ? 1u : 0u;
-    P.head = head;
-    P.cl = cl;
-    return launch_enc_claim<E_CTR>(P, K, st);
 }
 
 hipError_t tt_cfb_decrypt_claim(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K,

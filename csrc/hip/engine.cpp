@@ -63,12 +63,6 @@ hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, boo
 hipError_t tt_ctr_shift(const void *, void *, size_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t xor_small(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
 hipError_t bs_claim(int, const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, SplitClaim, hipStream_t);
-hipError_t bs_ctr_prepare(uint64_t, const otc_aes_key &, Ctr128, bool, hipStream_t, otc_dev::BsCtrPrep *);
-hipError_t bs_ctr_claim(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, bool, otc_dev::BsCtrPrep *, SplitClaim,
-                        hipStream_t);
-void bs_ctr_discard(otc_dev::BsCtrPrep *, hipStream_t);
-hipError_t tt_ctr_claim(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, bool, uint64_t, SplitClaim,
-                        hipStream_t);
 hipError_t tt_ecb_encrypt_claim(const void *, void *, uint64_t, const otc_aes_key &, SplitClaim, hipStream_t);
 hipError_t tt_cfb_decrypt_claim(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, SplitClaim,
                                 hipStream_t);
@@ -163,7 +157,9 @@ namespace {
  * co-resident split (split_claim below) from split_min() bytes, the T-table
  * below that.  Segment encryption: T-table kernels only (seg_enc_run).
  * ctr_bytes = 0 for non-CTR calls.  OTC_IMPL=ttable|bitslice|split overrides
- * "auto" for the whole process. */
+ * "auto" for the whole process, each where it applies: "split" for ECB and
+ * the decryptions only (CTR keeps its auto choice), no override for segment
+ * encryption (T-table only). */
 int env_impl()
 {
     static const int env = [] {
@@ -182,18 +178,20 @@ int env_impl()
 
 int pick_impl(int impl, int bits, size_t ctr_bytes = 0)
 {
-    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE || impl == OTC_IMPL_SPLIT) return impl;
-    const int env = env_impl();
-    if (env != OTC_IMPL_AUTO) return env;
+    /* CTR has no split: "split" (per call, or OTC_IMPL=split set for the
+     * whole process to get the ECB / decryption split) takes the auto choice
+     * here.  The co-resident CTR split (bitsliced CTR claim + T-table CTR
+     * claim kernels) lost to the bitsliced kernel alone on both HIP runtimes
+     * -- AES-128 64 GiB 1600-1629 vs 1659-1669 GB/s, AES-256 16 GiB 1150-1220
+     * vs 1222-1229, AES-256 64 GiB within +-2.5% -- and was removed in round
+     * 6 (profiles/r6/ctr_split_rt/). */
+    if (impl == OTC_IMPL_TTABLE || impl == OTC_IMPL_BITSLICE) return impl;
+    const int env = impl == OTC_IMPL_SPLIT ? OTC_IMPL_AUTO : env_impl();
+    if (env == OTC_IMPL_TTABLE || env == OTC_IMPL_BITSLICE) return env;
     /* measured crossover (profiles/r3/auto_impl/xover_after_round2_tables):
      * AES-128 2 GiB 1520 vs 1506 GB/s, 1 GiB 1353 vs 1360; AES-256 1 GiB
      * 1056 vs 1049.  AES-192 takes the AES-128 threshold (not measured at
-     * 1 GiB; its margin lies between the two).  The co-resident CTR split
-     * (ctr_split, impl "split") is not routed: it beat the bitsliced kernel
-     * by 1-4% in otbench (profiles/r5/ctr_split/thresholds_ab.jsonl) but
-     * lost to it inside a process with torch's and RCCL's streams -- bench.py
-     * 1534-1607 vs 1688 GB/s (bench_with_ctr_split*.json) -- whether its
-     * halves share pooled hardware queues or run on CU-masked ones. */
+     * 1 GiB; its margin lies between the two). */
     const size_t min_bs = bits == 256 ? ((size_t)1 << 30) : ((size_t)2 << 30);
     return ctr_bytes >= min_bs ? OTC_IMPL_BITSLICE : OTC_IMPL_TTABLE;
 }
@@ -497,49 +495,6 @@ hipError_t cfb_dec_split(const void *in, void *out, uint64_t nblocks, const otc_
         [&]() { return otc_impl::tt_cfb_decrypt(in, out, nblocks, K, ivw, st); });
 }
 
-/* CTR as a co-resident split: the bitsliced CTR kernel (counter caching, 8
- * LDS-staged slots per wave) takes the full 2048-block tasks of the counter's
- * task grid from the front, the T-table CTR claim kernel takes them from the
- * back and runs the partial first / last task in its workgroup 0.  A
- * trailing partial block: the T-table, same counter stream. */
-hipError_t ctr_split(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
-                     hipStream_t st, int *ran)
-{
-    *ran = OTC_IMPL_TTABLE; /* until split_claim runs both halves */
-    const size_t full = nbytes - nbytes % 16;
-    if (nbytes % 16) {
-        Ctr128 ct = c;
-        ct.lo = c.lo + full / 16;
-        if (!wrap64 && ct.lo < c.lo) ct.hi += 1;
-        hipError_t e = otc_impl::tt_ctr((const uint8_t *)in + full, (uint8_t *)out + full, nbytes % 16, K, ct, wrap64, st);
-        if (e != hipSuccess || full == 0) {
-            *ran = OTC_IMPL_TTABLE;
-            return e;
-        }
-    }
-    const uint64_t nblocks = full / 16, shift = c.lo & 2047u;
-    const uint64_t t0 = shift ? 1 : 0, tf = (nblocks + shift) / 2048;
-    const uint64_t nunits = tf > t0 ? tf - t0 : 0;
-    const uint64_t head = std::min<uint64_t>(t0 ? 2048 - shift : 0, nblocks);
-    if (nunits < 2) return otc_impl::tt_ctr(in, out, full, K, c, wrap64, st);
-    otc_dev::BsCtrPrep pre;
-    if (otc_impl::bs_ctr_prepare(nblocks, K, c, wrap64, st, &pre) != hipSuccess) {
-        (void)hipGetLastError();
-        return otc_impl::tt_ctr(in, out, full, K, c, wrap64, st);
-    }
-    bool used = false;
-    const hipError_t e = split_claim(
-        nunits, 2, false, bs_wgs_for(FORM_SPLIT), st, ran,
-        [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_ctr_claim(in, out, nblocks, K, c, wrap64, head, cl, ts); },
-        [&](SplitClaim cl, hipStream_t s) {
-            used = true;
-            return otc_impl::bs_ctr_claim(in, out, nblocks, K, c, wrap64, &pre, cl, s);
-        },
-        [&]() { return otc_impl::tt_ctr(in, out, full, K, c, wrap64, st); });
-    if (!used) otc_impl::bs_ctr_discard(&pre, st);
-    return e;
-}
-
 /* Segment decryption (CBC / CFB128 over independent segments of 2^shift
  * blocks, IV_s = iv0 + s): the same split, each kernel computing the segment
  * IVs itself.  Non-power-of-two segments and short calls: the T-table. */
@@ -765,9 +720,8 @@ static int ctr_common(const void *in, void *out, size_t nbytes, const otc_aes_ke
     hipStream_t st = (hipStream_t)stream;
     const int im = pick_impl(impl, k->bits, nbytes);
     g_last_impl = im;
-    hipError_t e = im == OTC_IMPL_SPLIT       ? ctr_split(in, out, nbytes, *k, c, wrap64, st, &g_last_impl)
-                   : im == OTC_IMPL_BITSLICE ? otc_impl::bs_ctr(in, out, nbytes, *k, c, wrap64, st)
-                                             : otc_impl::tt_ctr(in, out, nbytes, *k, c, wrap64, st);
+    hipError_t e = im == OTC_IMPL_BITSLICE ? otc_impl::bs_ctr(in, out, nbytes, *k, c, wrap64, st)
+                                           : otc_impl::tt_ctr(in, out, nbytes, *k, c, wrap64, st);
     if (e != hipSuccess) return hip_fail(e, "aes_ctr launch");
     return OTC_OK;
 }

@@ -135,17 +135,6 @@ struct SplitClaim {
     uint32_t wgs;            /* host side: workgroups of the kernel given this claim (0: one per CU) */
 };
 
-/* bitsliced CTR tables built ahead of a CTR split (engine.cpp ctr_split: on
- * the caller's stream BEFORE the T-table claim kernel, so the bitsliced claim
- * kernel launches right behind it instead of behind its own table kernels --
- * behind them, at 64 GiB one kernel's workgroups held every CU before the
- * other's were placed, and took every unit) */
-struct BsCtrPrep {
-    uint32_t *tab = nullptr;
-    uint64_t tasks = 0;
-    bool cache = false;
-};
-
 /* lane id from the exec-mask count: nothing to keep live across a loop
  * (threadIdx.x lives in v0 from kernel entry; read in every trip of a long
  * loop body, hipcc keeps it -- and spills it) */

@@ -58,12 +58,13 @@ typedef struct {
 int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 
 /* ---- implementation selection ------------------------------------------- */
-#define OTC_IMPL_AUTO 0     /* the measured winner (docs/PERF.md round 5): bitsliced for CTR calls >= 2 GiB
+#define OTC_IMPL_AUTO 0     /* the measured winner (docs/PERF.md rounds 5-6): bitsliced for CTR calls >= 2 GiB
                                (AES-256: >= 1 GiB); for ECB / CBC / CFB decryption and the power-of-two segment
                                decryptions the split below from 2 GiB and the persistent T-table claim kernel
                                alone from 896 MiB; segment encryption: the persistent T-table claim kernel from
                                2 GiB (1 GiB for segments <= 1 KiB); the grid T-table otherwise
-                               (OTC_IMPL=ttable|bitslice|split env overrides for the whole process) */
+                               (OTC_IMPL=ttable|bitslice|split env overrides for the whole process, each where it
+                               applies: split for ECB and the decryptions only) */
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
 #define OTC_IMPL_BITSLICE 2 /* bitsliced VALU kernel alone: 32 blocks per lane (CTR, ECB, the decryptions; their
                                claim kernels take every 2048-block unit and one T-table workgroup the blocks past
@@ -71,8 +72,9 @@ int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 #define OTC_IMPL_SPLIT 3    /* the T-table and the bitsliced kernel CONCURRENTLY over one buffer, each on a
                                pooled CU-masked stream, co-resident on every CU -- LDS and VALU busy at once --
                                claiming units from one counter: ECB, the CBC / CFB decryptions and the segment
-                               modes ("auto" for these >= 2 GiB), and CTR (on request only: +1-4% in a bare
-                               process, slower than the bitsliced kernel inside bench.py) */
+                               decryptions ("auto" for these >= 2 GiB).  CTR has no split (it lost to the
+                               bitsliced kernel on both HIP runtimes, removed in round 6): a CTR call with
+                               OTC_IMPL_SPLIT takes the auto choice */
 
 /* The kernel family `impl` resolves to for a call of nbytes with a bits-bit
  * key (mode 1: CTR, 0: ECB encryption, 2: ECB / CBC decryption, 3: CFB128
@@ -188,8 +190,8 @@ int otc_aes_cfb128_decrypt_segments_impl(const void *in, void *out, size_t seg_b
 
 /* CFB128 decryption (parallel): P_i = C_i ^ E(C_{i-1}), C_{-1} = iv;
  * nbytes % 16 == 0; encryption key.  _impl: with a kernel choice (the plain
- * form is OTC_IMPL_AUTO: the T-table + bitsliced split from 896 MiB, like ECB
- * encryption). */
+ * form is OTC_IMPL_AUTO: the T-table + bitsliced split from 2 GiB, the
+ * persistent T-table claim kernel from 896 MiB, like ECB encryption). */
 int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
                            const uint8_t iv[16], void *stream);
 int otc_aes_cfb128_decrypt_impl(const void *in, void *out, size_t nbytes, const otc_aes_key *k,

@@ -19,6 +19,7 @@ code at all.
 from __future__ import annotations
 
 import os
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
@@ -41,6 +42,18 @@ def local_gpu() -> int:
             raise RuntimeError(f"LOCAL_RANK {local} but only {n} GPU(s) visible (OTC_SHARE_GPUS=1 to share)")
         return local % n
     return local
+
+
+def collective_timeout() -> timedelta:
+    """Bound on any one collective of the default and duplex groups
+    (OTC_COLLECTIVE_TIMEOUT_S, default 300 s; torch's default is 30 min).
+    With TORCH_NCCL_ASYNC_ERROR_HANDLING=1 (set here unless the caller chose)
+    torch's RCCL watchdog tears the rank down when one stalls past it, so a
+    dead peer ends the job instead of hanging it -- the Python-side
+    counterpart of the C job's ncclCommGetAsyncError poll
+    (csrc/hip/pipeline.cpp).  The bench's collectives move <= 2 GiB per rank
+    over xGMI (seconds at worst), so 300 s only trips on a real stall."""
+    return timedelta(seconds=float(os.environ.get("OTC_COLLECTIVE_TIMEOUT_S", "300")))
 
 
 def init_from_env(backend: str | None = None, force: bool = False):
@@ -71,9 +84,10 @@ def init_from_env(backend: str | None = None, force: bool = False):
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
-            dist.init_process_group(backend, device_id=torch.device("cuda", gpu))
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+            dist.init_process_group(backend, device_id=torch.device("cuda", gpu), timeout=collective_timeout())
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=collective_timeout())
     return rank, world, gpu
 
 
@@ -183,7 +197,7 @@ def duplex_groups():
         return None, None
     key = (dist.get_backend(), dist.get_world_size())
     if key not in _DUPLEX_GROUPS:
-        _DUPLEX_GROUPS[key] = (dist.new_group(), dist.new_group())
+        _DUPLEX_GROUPS[key] = (dist.new_group(timeout=collective_timeout()), dist.new_group(timeout=collective_timeout()))
     return _DUPLEX_GROUPS[key]
 
 

@@ -88,3 +88,16 @@ def test_gloo_data_parallel(world):
     for r in res:
         assert len(r) == 6, f"worker failed: {r}"
         assert all(r[1:]), f"rank {r[0]} mismatch: {r}"
+
+
+def test_collective_timeout_bound(monkeypatch):
+    """Every group the engine creates gets a bounded collective timeout
+    (default 300 s, OTC_COLLECTIVE_TIMEOUT_S overrides), not torch's 30 min."""
+    from datetime import timedelta
+
+    from our_tree_amd.parallel import dist as pdist
+
+    monkeypatch.delenv("OTC_COLLECTIVE_TIMEOUT_S", raising=False)
+    assert pdist.collective_timeout() == timedelta(seconds=300)
+    monkeypatch.setenv("OTC_COLLECTIVE_TIMEOUT_S", "12.5")
+    assert pdist.collective_timeout() == timedelta(seconds=12.5)

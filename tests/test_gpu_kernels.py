@@ -435,11 +435,11 @@ def test_bitslice_launch_structures(gpu, bits):
 def test_auto_routing_rule(gpu):
     """impl="auto" by size (docs/PERF.md, profiles/r3/auto_impl,
     profiles/r4/ecb_split): bitsliced CTR from 2 GiB (AES-128/192) or 1 GiB
-    (AES-256) -- the CTR split only on request (profiles/r5/ctr_split) --,
-    the co-resident split for ECB encryption from 2 GiB (round 5,
+    (AES-256), the co-resident split for ECB encryption from 2 GiB (round 5,
     measured with the halves truly co-resident), T-table for everything else;
-    the boundaries are exact.  "split" is explicit for both
-    (CTR: the co-resident T-table + bitsliced CTR claim kernels)."""
+    the boundaries are exact.  "split" is explicit for ECB; CTR
+    has no split (removed in round 6, profiles/r6/ctr_split_rt/), so a CTR
+    "split" request takes the auto choice."""
     G = 1 << 30
     cases = [(128, "ctr", 64 * G, "bitslice"), (128, "ctr", 2 * G - 16, "ttable"), (128, "ctr", 2 * G, "bitslice"),
              (256, "ctr", 1 * G, "bitslice"), (256, "ctr", 1 * G - 16, "ttable"), (256, "ctr", 4 * G, "bitslice"),
@@ -451,7 +451,7 @@ def test_auto_routing_rule(gpu):
         assert ops.pick_impl("auto", bits, mode, n) == want, (bits, mode, n)
         assert ops.pick_impl("ttable", bits, mode, n) == "ttable"
         assert ops.pick_impl("bitslice", bits, mode, n) == "bitslice"
-        assert ops.pick_impl("split", bits, mode, n) == "split"
+        assert ops.pick_impl("split", bits, mode, n) == (want if mode == "ctr" else "split")
     with pytest.raises(ValueError):
         ops.pick_impl("hybrid")
 
@@ -588,33 +588,18 @@ def test_segment_encrypt_persistent_ttable(gpu, seg):
 
 
 @pytest.mark.parametrize("bits", [128, 256])
-def test_ctr_split_matches_oracle(gpu, bits):
-    """CTR as a co-resident split (bitsliced CTR claim kernel with counter
-    caching + T-table CTR claim kernel, engine.cpp ctr_split): equal to the
-    bitsliced kernel alone and to the oracle, for counters that start a task
-    and that do not (the T-table's workgroup 0 runs the partial first and last
-    task), a trailing partial block, a carry out of the low 64 bits, in place;
-    under two full tasks the T-table runs alone."""
+def test_ctr_split_request_runs_auto(gpu, bits):
+    """CTR has no split: impl "split" runs what "auto" picks (the bitsliced
+    kernel from 2 GiB / 1 GiB, the T-table below) and equals the oracle."""
     key = os.urandom(bits // 8)
-    for n, ctr in ((16 * 2048 * 7, bytes(16)),
-                   (16 * 2048 * 9 + 16 * 37 + 5, os.urandom(8) + (2**64 - 2048 * 3 - 100).to_bytes(8, "big")),
-                   (16 * 2048 * 64 + 48, os.urandom(16)),
-                   (16 * 2048 * 2 + 16, os.urandom(16))):
-        x = torch.empty(n, dtype=torch.uint8, device=gpu)
-        ops.fill_random_(x, seed=n ^ bits)
-        b = ops.ctr(x, key, ctr, impl="bitslice")
-        y = ops.ctr(x, key, ctr, impl="split")
-        shift, nb = int.from_bytes(ctr, "big") & 2047, n // 16
-        nunits = (nb + shift) // 2048 - (1 if shift else 0)
-        assert ops.last_impl() == ("split" if nunits >= 2 else "ttable"), (n, shift, ops.last_impl())
-        w = x.clone()
-        ops.ctr(w, key, ctr, out=w, impl="split")
-        torch.cuda.synchronize()
-        assert torch.equal(y, b), (bits, n)
-        assert torch.equal(w, b), (bits, n, "in place")
-        S = 1 << 13
-        for off in (0, (n // 3) & ~15, (n - S) & ~15, n - n % 16 - 16):
-            assert host(y[off:off + S]) == cpu_ref.ctr(key, sh.ctr_add(ctr, off // 16), host(x[off:off + S])), (n, off)
+    ctr = os.urandom(8) + (2**64 - 2048 * 3 - 100).to_bytes(8, "big")
+    n = 16 * 2048 * 9 + 16 * 37 + 5
+    x = torch.empty(n, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(x, seed=n ^ bits)
+    y = ops.ctr(x, key, ctr, impl="split")
+    torch.cuda.synchronize()
+    assert ops.last_impl() == "ttable"
+    assert host(y) == cpu_ref.ctr(key, ctr, host(x))
 
 
 def test_persistent_ttable_midsize(gpu):

@@ -112,27 +112,6 @@ def test_split_pairs_share_a_simd():
             assert 4 * alloc(t) + alloc(b) <= 512, (mode, nr, t, b)
             seen += 1
     assert seen == 18
-    # CTR: the T-table CTR claim kernel beside the bitsliced CTR claim kernel
-    for nr in (10, 12, 14):
-        t = max(v for k, v in tt.items() if "k_aes_ctr_tt_claim" in k and f"ILi{nr}E" in k)
-        b = max(v for k, v in bs.items() if "k_aes_bs_ctr_claim" in k and f"ILi{nr}E" in k)
-        assert 4 * alloc(t) + alloc(b) <= 512, ("CTR", nr, t, b)
-
-
-def test_ctr_split_lds_fits():
-    """The CTR pair also shares LDS: the T-table's 128 KiB dynamic table plus
-    the bitsliced claim kernel's static staging fit a CU's 160 KiB."""
-    import tempfile
-
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    import isa_count
-
-    if not os.path.exists(OBJ) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):
-        pytest.skip("no built objects (make) or no ROCm LLVM tools")
-    with tempfile.TemporaryDirectory() as tmp:
-        d = isa_count.descriptor_vgprs(isa_count.code_object(OBJ, tmp), with_lds=True)
-    ctr = [lds for k, (vg, lds) in d.items() if "k_aes_bs_ctr_claim" in k]
-    assert len(ctr) == 6 and all(0 < lds <= 16 << 10 for lds in ctr), ctr
 
 
 def _vgprs(obj):
