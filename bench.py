@@ -540,10 +540,12 @@ def main():
         from our_tree_amd.parallel import jobs
 
         # The shard stays allocated: the scatter pass needs only 4 x world x
-        # chunk more on the root (16 GiB at N = 8), and freeing 64 GiB here made
-        # the driver clear it in the background over the next seconds, which
-        # slowed every D2H copy of the later pinned pipeline row from 49 to
-        # 37 GB/s (round 6, profiles/r6/pipeline/).
+        # chunk more on the root (16 GiB at N = 8).  (An earlier session saw
+        # the pinned row's D2H slow down after a 64 GiB free; the probe
+        # tools/free_wipe_probe.py did not reproduce it -- 57 GB/s both ways
+        # from 38 ms after the free, profiles/r6/validate_d1/free_wipe.jsonl.
+        # The row's loss was the engine's streams on pooled hardware queues:
+        # profiles/r6/pipeline/census.jsonl, docs/PERF.md round 6.)
         chunk = (args.scatter_mib << 20) if not cpu else 4096 * 8
         sc = guarded("rccl_scatter", lambda: jobs.cbc_scatter_job(args.scatter_rounds, chunk, key256,
                                                                   bytes(range(0xA0, 0xB0)), sector=4096, device=dev))

@@ -89,3 +89,24 @@ class JsonlWriter:
     def write(self, **rec):
         with open(self.path, "a") as f:
             f.write(json.dumps(rec, sort_keys=True) + "\n")
+
+
+def split_sections(text: str) -> list[list[dict]]:
+    """The records of a log in the order printed, cut at lines that are not
+    records: the ARC4 self-test lines end the CPU sweep of bin/test (so a
+    bin/test log followed by a ``--device gpu`` log gives two sections) and
+    ``## `` lines head a bin/aes_test log."""
+    chunks, cur = [], []
+    for ln in text.splitlines():
+        if ln.strip().startswith("ARC4 test #") or ln.startswith("## "):
+            chunks.append(cur)
+            cur = []
+        else:
+            cur.append(ln)
+    chunks.append(cur)
+    return [recs for recs in (parse("\n".join(c) + "\n") for c in chunks) if recs]
+
+
+def gbps_table(records: list[dict]) -> dict:
+    """(label, bytes, threads) -> median-of-iterations-2..N GB/s (summarize)."""
+    return {(r["label"], r["bytes"], r["threads"]): summarize(r)["gbps_median"] for r in records}
