@@ -171,6 +171,25 @@ __device__ __forceinline__ bool task_of(const BsParams &P, Task &t, int64_t clai
     return true;
 }
 
+/* Streaming cache policy (otc_device.h ld_u4 / st_u4).  OTC_BS_NT (default
+ * 1): the non-temporal bit on the CTR plaintext loads (LDS DMA and register
+ * slots) and on every ciphertext store -- each byte is read once and written
+ * once.  Round 6 A/B, 64 GiB in place, 3 reps (profiles/r6/nt_ab/): AES-128
+ * CTR 1705-1717 vs 1677-1687 GB/s at 0.795-0.803 vs 0.814-0.818 J/GB,
+ * AES-256 1275-1279 vs 1248-1260 at 1.061-1.062 vs 1.088-1.095.
+ * OTC_NT_ALL (variant builds): the same on the ECB / decryption plane loads. */
+#ifndef OTC_BS_NT
+#define OTC_BS_NT 1
+#endif
+#ifndef OTC_NT_ALL
+#define OTC_NT_ALL 0
+#endif
+constexpr bool BS_NT = OTC_BS_NT != 0;
+constexpr bool BS_NT_IN = OTC_NT_ALL != 0;
+constexpr int BS_LDS_AUX = BS_NT ? 2 : 0; /* CPol: NT (SLC) bit of the LDS DMA loads */
+__device__ __forceinline__ uint4 ld_stream(const uint8_t *p) { return ld_u4<BS_NT>(p); }
+__device__ __forceinline__ void st_stream(uint8_t *p, uint4 v) { st_u4<BS_NT>(p, v); }
+
 /* ECB input: load 32 blocks (uniform task base + 32-bit lane offsets: 64-bit
  * per-slot addresses would be CSE'd with the stores and kept live across the
  * rounds) and transpose each word column into 32 planes.  CFB decryption
@@ -195,7 +214,7 @@ __device__ __forceinline__ void ecb_load_planes(const BsParams &P, const Task &t
             const uint8_t *src = P.in + (int64_t)(t.vbase * 16) + lo - (first ? 0 : 16);
             blk[k] = blend_iv((full || i < P.nblocks) ? *(const uint4 *)src : make_uint4(0, 0, 0, 0), first, P);
         } else {
-            blk[k] = (full || i < P.nblocks) ? *(const uint4 *)(tb + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
+            blk[k] = (full || i < P.nblocks) ? ld_u4<BS_NT_IN>(tb + lo + 1024u * k) : make_uint4(0, 0, 0, 0);
         }
     }
 #pragma unroll
@@ -347,34 +366,6 @@ __device__ __forceinline__ void rounds_table(W *s, ktab_ptr tp)
 #ifndef OTC_BS_PRE
 #define OTC_BS_PRE 2
 #endif
-/* Streaming cache policy for the bytes a task reads and writes once (round 6
- * energy A/B, docs/PERF.md): 1 sets the non-temporal bit on the plaintext
- * loads (LDS DMA and register slots) and the ciphertext stores, so the 64
- * GiB stream does not allocate in L2 / MALL.  A compile-time switch
- * (make variant VFLAGS=-DOTC_BS_NT=1); the release build takes the default. */
-#ifndef OTC_BS_NT
-#define OTC_BS_NT 0
-#endif
-constexpr int BS_LDS_AUX = OTC_BS_NT ? 2 : 0; /* CPol: NT (SLC) bit */
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 ld_stream(const uint8_t *p)
-{
-    if constexpr (OTC_BS_NT) {
-        const u32x4 v = __builtin_nontemporal_load((const u32x4 *)p);
-        return make_uint4(v.x, v.y, v.z, v.w);
-    } else {
-        return *(const uint4 *)p;
-    }
-}
-__device__ __forceinline__ void st_stream(uint8_t *p, uint4 v)
-{
-    if constexpr (OTC_BS_NT) {
-        const u32x4 w = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(w, (u32x4 *)p);
-    } else {
-        *(uint4 *)p = v;
-    }
-}
 template <int NR, int MODE, int LS, bool CACHE, bool FO, int MIX = 2, int PRE = OTC_BS_PRE, int D = 8>
 __device__ __forceinline__ void aes_bs_task(const BsParams &P, const otc_aes_key &K, uint4 *stage,
                                             int64_t claimed = -1)

@@ -262,14 +262,13 @@ __device__ __forceinline__ void dec_rounds4(TBL tbl, const uint32_t (&lk)[4], ui
         for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
 }
 
-__device__ __forceinline__ uint4 ld16(const uint8_t *p, uint64_t blk)
-{
-    return *reinterpret_cast<const uint4 *>(p + 16 * blk);
-}
-__device__ __forceinline__ void st16(uint8_t *p, uint64_t blk, uint4 v)
-{
-    *reinterpret_cast<uint4 *>(p + 16 * blk) = v;
-}
+/* OTC_NT_ALL (variant builds, round 6 A/B): non-temporal block loads and
+ * stores in the T-table kernels too (otc_device.h ld_u4 / st_u4) */
+#ifndef OTC_NT_ALL
+#define OTC_NT_ALL 0
+#endif
+__device__ __forceinline__ uint4 ld16(const uint8_t *p, uint64_t blk) { return ld_u4<OTC_NT_ALL != 0>(p + 16 * blk); }
+__device__ __forceinline__ void st16(uint8_t *p, uint64_t blk, uint4 v) { st_u4<OTC_NT_ALL != 0>(p + 16 * blk, v); }
 enum : int { E_ECB = 0, E_CFB_DEC = 2, E_CFB_DEC_SEG = 3 };
 enum : int { D_ECB = 0, D_CBC = 1, D_CBC_SEG = 2 };
 

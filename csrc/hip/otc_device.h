@@ -138,6 +138,35 @@ struct SplitClaim {
 /* lane id from the exec-mask count: nothing to keep live across a loop
  * (threadIdx.x lives in v0 from kernel entry; read in every trip of a long
  * loop body, hipcc keeps it -- and spills it) */
+/* 16-byte global load / store with an optional non-temporal hint (the NT
+ * bit: the line is not kept in L2 / MALL).  Streaming data that is read once
+ * and written once -- every byte of a 64 GiB CTR call -- does not benefit
+ * from being cached, and the hint cut the headline kernel's J/GB by 2-3% and
+ * raised its rate 1.7-1.8% under the power cap (round 6,
+ * profiles/r6/nt_ab/).  The builtins take native vector types, not HIP's
+ * uint4 struct. */
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 ld_u4(const void *p)
+{
+    if constexpr (NT) {
+        const u32x4 v = __builtin_nontemporal_load((const u32x4 *)p);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *(const uint4 *)p;
+    }
+}
+template <bool NT>
+__device__ __forceinline__ void st_u4(void *p, uint4 v)
+{
+    if constexpr (NT) {
+        const u32x4 w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, (u32x4 *)p);
+    } else {
+        *(uint4 *)p = v;
+    }
+}
+
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 /* one atomic add of `inc` on the claim word; returns the old value (wave-uniform) */
