@@ -554,6 +554,7 @@ def main():
         extra["rccl_ranks"] = sc["ranks"]
         extra["rccl_ranks_verified"] = sc["ranks_verified"]
         extra["rccl_backend"] = sc["backend"]
+        extra["rccl_duplex"] = sc["overlap"]  # scatter / gather on two communicators (OTC_DUPLEX=0: one)
         extra["rccl_transport"] = sc["transport"]  # "xgmi" over RCCL at N > 1, "local" at N = 1, gloo: "host"
         extra["rccl_xgmi_bytes_verified"] = sc["xgmi_bytes_verified"]
         extra["rccl_xgmi_bytes_timed"] = sc["xgmi_bytes_timed"]

@@ -172,20 +172,19 @@ __device__ __forceinline__ bool task_of(const BsParams &P, Task &t, int64_t clai
 }
 
 /* Streaming cache policy (otc_device.h ld_u4 / st_u4).  OTC_BS_NT (default
- * 1): the non-temporal bit on the CTR plaintext loads (LDS DMA and register
- * slots) and on every ciphertext store -- each byte is read once and written
- * once.  Round 6 A/B, 64 GiB in place, 3 reps (profiles/r6/nt_ab/): AES-128
- * CTR 1705-1717 vs 1677-1687 GB/s at 0.795-0.803 vs 0.814-0.818 J/GB,
- * AES-256 1275-1279 vs 1248-1260 at 1.061-1.062 vs 1.088-1.095.
- * OTC_NT_ALL (variant builds): the same on the ECB / decryption plane loads. */
+ * 1): the non-temporal bit on every block this kernel reads or writes once --
+ * the CTR plaintext loads (LDS DMA and register slots), the ECB / decryption
+ * plane loads, the CBC / CFB XOR-block loads, every ciphertext store.  Round
+ * 6 A/B, 64 GiB in place, 3 reps (profiles/r6/nt_ab/): AES-128 CTR 1705-1717
+ * vs 1677-1687 GB/s at 0.795-0.803 vs 0.814-0.818 J/GB, AES-256 1275-1279 vs
+ * 1248-1260 at 1.061-1.062 vs 1.088-1.095; the splits' bitsliced halves with
+ * the T-table's streaming forms (aes_tt.hip OTC_TT_NT): +0.8-1.5%
+ * (profiles/r6/ntall_ab/). */
 #ifndef OTC_BS_NT
 #define OTC_BS_NT 1
 #endif
-#ifndef OTC_NT_ALL
-#define OTC_NT_ALL 0
-#endif
 constexpr bool BS_NT = OTC_BS_NT != 0;
-constexpr bool BS_NT_IN = OTC_NT_ALL != 0;
+constexpr bool BS_NT_IN = BS_NT;
 constexpr int BS_LDS_AUX = BS_NT ? 2 : 0; /* CPol: NT (SLC) bit of the LDS DMA loads */
 __device__ __forceinline__ uint4 ld_stream(const uint8_t *p) { return ld_u4<BS_NT>(p); }
 __device__ __forceinline__ void st_stream(uint8_t *p, uint4 v) { st_u4<BS_NT>(p, v); }

@@ -262,13 +262,22 @@ __device__ __forceinline__ void dec_rounds4(TBL tbl, const uint32_t (&lk)[4], ui
         for (int j = 0; j < 4; ++j) s[b][j] = t[b][j];
 }
 
-/* OTC_NT_ALL (variant builds, round 6 A/B): non-temporal block loads and
- * stores in the T-table kernels too (otc_device.h ld_u4 / st_u4) */
-#ifndef OTC_NT_ALL
-#define OTC_NT_ALL 0
+__device__ __forceinline__ uint4 ld16(const uint8_t *p, uint64_t blk) { return ld_u4<false>(p + 16 * blk); }
+__device__ __forceinline__ void st16(uint8_t *p, uint64_t blk, uint4 v) { st_u4<false>(p + 16 * blk, v); }
+/* Streaming forms (otc_device.h ld_u4 / st_u4) for the kernels whose wave
+ * loads / stores 1 KiB of consecutive blocks per instruction -- ECB, CTR, the
+ * CFB / CBC decryptions and their claim forms: the non-temporal bit
+ * (OTC_TT_NT, default 1).  Round 6 A/B (profiles/r6/ntall_ab/, AES-256, 2
+ * reps): the splits +0.8-1.5% (CBC-dec 8 GiB 1205-1208 vs 1188-1194), ECB-dec
+ * +1%, T-table CTR even.  NOT the serial segment chains: there each lane
+ * walks its own segment 16 B at a time, the next block sits in the line just
+ * read, and without the line in cache every block refetches it -- CBC
+ * segment encryption fell from 1114-1120 to 472-476 GB/s with the bit. */
+#ifndef OTC_TT_NT
+#define OTC_TT_NT 1
 #endif
-__device__ __forceinline__ uint4 ld16(const uint8_t *p, uint64_t blk) { return ld_u4<OTC_NT_ALL != 0>(p + 16 * blk); }
-__device__ __forceinline__ void st16(uint8_t *p, uint64_t blk, uint4 v) { st_u4<OTC_NT_ALL != 0>(p + 16 * blk, v); }
+__device__ __forceinline__ uint4 lds16(const uint8_t *p, uint64_t blk) { return ld_u4<OTC_TT_NT != 0>(p + 16 * blk); }
+__device__ __forceinline__ void sts16(uint8_t *p, uint64_t blk, uint4 v) { st_u4<OTC_TT_NT != 0>(p + 16 * blk, v); }
 enum : int { E_ECB = 0, E_CFB_DEC = 2, E_CFB_DEC_SEG = 3 };
 enum : int { D_ECB = 0, D_CBC = 1, D_CBC_SEG = 2 };
 
@@ -353,20 +362,20 @@ __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_ke
             const uint64_t i = i0 + 64u * b;
             const bool ok = full || i < lim;
             if (MODE == E_ECB) {
-                uint4 v = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
+                uint4 v = ok ? lds16(P.in, i) : make_uint4(0, 0, 0, 0);
                 s[b][0] = v.x; s[b][1] = v.y; s[b][2] = v.z; s[b][3] = v.w;
             } else if (MODE == E_CFB_DEC) { /* cipher input is the previous ciphertext */
-                x[b] = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
+                x[b] = ok ? lds16(P.in, i) : make_uint4(0, 0, 0, 0);
                 uint4 v = (i == 0) ? make_uint4(P.iv[0], P.iv[1], P.iv[2], P.iv[3])
-                                   : (ok ? ld16(P.in, i - 1) : make_uint4(0, 0, 0, 0));
+                                   : (ok ? lds16(P.in, i - 1) : make_uint4(0, 0, 0, 0));
                 s[b][0] = v.x; s[b][1] = v.y; s[b][2] = v.z; s[b][3] = v.w;
             } else { /* CFB decrypt of independent segments: IV_s at segment starts */
-                x[b] = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
+                x[b] = ok ? lds16(P.in, i) : make_uint4(0, 0, 0, 0);
                 const uint64_t sg = P.seg_shift < 64 ? (i >> P.seg_shift) : i / P.seg_blocks;
                 if (i == sg * P.seg_blocks) {
                     ctr_words(P.ctr, sg, false, s[b][0], s[b][1], s[b][2], s[b][3]);
                 } else {
-                    uint4 v = ok ? ld16(P.in, i - 1) : make_uint4(0, 0, 0, 0);
+                    uint4 v = ok ? lds16(P.in, i - 1) : make_uint4(0, 0, 0, 0);
                     s[b][0] = v.x; s[b][1] = v.y; s[b][2] = v.z; s[b][3] = v.w;
                 }
             }
@@ -385,7 +394,7 @@ __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_ke
             } else {
                 o = make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]);
             }
-            if (full || i < lim) st16(P.out, i, o);
+            if (full || i < lim) sts16(P.out, i, o);
         }
     };
 
@@ -514,7 +523,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_
         for (int b = 0; b < B; ++b) {
             const int64_t i = i0 + 64 * b;
             const bool ok = full || (i >= 0 && (uint64_t)i < P.nfull);
-            x[b] = ok ? ld16(P.in, (uint64_t)i) : make_uint4(0, 0, 0, 0);
+            x[b] = ok ? lds16(P.in, (uint64_t)i) : make_uint4(0, 0, 0, 0);
             /* round 1: only T3[byte 15] varies */
             const uint32_t c15 = (b15 | (uint32_t)(64 * b) | lane) ^ (K.rk[3] >> 24);
             const uint32_t s0 = U0 ^ lds_at(tbl, (c15 << 8) | lk[3]);
@@ -532,7 +541,7 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_
             const int64_t i = i0 + 64 * b;
             const bool ok = full || (i >= 0 && (uint64_t)i < P.nfull);
             if (ok) {
-                st16(P.out, (uint64_t)i,
+                sts16(P.out, (uint64_t)i,
                      make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
             } else if (i >= 0 && (uint64_t)i == P.nfull && P.tail) {
                 const uint32_t ks[4] = {s[b][0], s[b][1], s[b][2], s[b][3]};
@@ -568,7 +577,7 @@ __device__ __forceinline__ void dec_tt_body(const DecParams &P, const otc_aes_ke
         for (int b = 0; b < B; ++b) {
             const uint64_t i = i0 + 64u * b;
             const bool ok = full || i < P.nfull;
-            uint4 v = ok ? ld16(P.in, i) : make_uint4(0, 0, 0, 0);
+            uint4 v = ok ? lds16(P.in, i) : make_uint4(0, 0, 0, 0);
             s[b][0] = v.x ^ K.rk[0]; s[b][1] = v.y ^ K.rk[1];
             s[b][2] = v.z ^ K.rk[2]; s[b][3] = v.w ^ K.rk[3];
             if (MODE == D_CBC || MODE == D_CBC_SEG) {
@@ -587,7 +596,7 @@ __device__ __forceinline__ void dec_tt_body(const DecParams &P, const otc_aes_ke
                     ctr_words(ivv, 0, false, w0, w1, w2, w3);
                     prev[b] = make_uint4(w0, w1, w2, w3);
                 } else {
-                    prev[b] = ok ? ld16(P.in, i - 1) : make_uint4(0, 0, 0, 0);
+                    prev[b] = ok ? lds16(P.in, i - 1) : make_uint4(0, 0, 0, 0);
                 }
             }
         }
@@ -601,7 +610,7 @@ __device__ __forceinline__ void dec_tt_body(const DecParams &P, const otc_aes_ke
             if (MODE != D_ECB) {
                 o.x ^= prev[b].x; o.y ^= prev[b].y; o.z ^= prev[b].z; o.w ^= prev[b].w;
             }
-            if (full || i < P.nfull) st16(P.out, i, o);
+            if (full || i < P.nfull) sts16(P.out, i, o);
         }
     };
 

@@ -213,6 +213,13 @@ class ScatterGatherPipeline:
 
     Memory: 4 x chunk per rank, plus 4 x world x chunk on the root -- chunked
     rounds, so a stream larger than one GPU's 288 GB streams through the root.
+
+    ``OTC_DUPLEX=0`` in the environment turns the overlap off for every
+    pipeline of the process: scatter and gather then share the default
+    group's one communicator, one after the other -- the fallback if two
+    concurrent RCCL communicators per GPU ever misbehave on a node (RCCL
+    allows it; each communicator's collectives are issued in the same order
+    on every rank, so they cannot cross-wait).
     """
 
     def __init__(self, chunk_per_rank: int, root: int = 0, device=None, overlap: bool = True):
@@ -226,7 +233,7 @@ class ScatterGatherPipeline:
         # collectives whenever a process group exists, even at world size 1
         # (a 1-rank RCCL group runs the same scatter/gather code path)
         self.comm = _pg_on()
-        self.overlap = overlap and self.comm
+        self.overlap = overlap and self.comm and os.environ.get("OTC_DUPLEX", "1") != "0"
         self.g_sc, self.g_ga = duplex_groups() if self.overlap else (None, None)
         nslot = 2 if self.overlap else 1
 

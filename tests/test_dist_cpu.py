@@ -51,6 +51,11 @@ def _worker(rank, world, port, q):
             res = pdist.scatter_ctr(full[:n] if rank == 0 else None, n, key, ctr0, chunk_per_rank=1024,
                                     overlap=overlap)
             ok3 = ok3 and (res is None if rank != 0 else res.numpy().tobytes() == ref_ctr[:n])
+        # OTC_DUPLEX=0: every pipeline falls back to the one communicator
+        os.environ["OTC_DUPLEX"] = "0"
+        ok3 = ok3 and not pdist.ScatterGatherPipeline(1024).overlap
+        del os.environ["OTC_DUPLEX"]
+        ok3 = ok3 and pdist.ScatterGatherPipeline(1024).overlap
         m = pdist.allreduce_max(float(rank))
         ok4 = m == world - 1
 
