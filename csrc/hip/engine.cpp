@@ -376,7 +376,15 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
         (!fork || ((e = hipEventRecord(a.fork, st)) == hipSuccess && (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess &&
                    (e = hipStreamWaitEvent(a.t, a.fork, 0)) == hipSuccess)) &&
         (e = tt(cl_tt, fork ? a.t : st)) == hipSuccess) {
-        /* the bitsliced half failing (no memory for its key table) leaves the
+        /* The T-table half is enqueued first on purpose: its 1024-thread,
+         * 128-160 KiB-LDS workgroups fit one per CU only when they are placed
+         * before the bitsliced ones (two or three 168-VGPR bitsliced
+         * workgroups on one CU leave no room for a T-table workgroup there).
+         * The price is a start-up transient: in a process's FIRST split call
+         * the bitsliced half's one-time costs (code object, key-table pool
+         * allocation) let the T-table half take every unit (1 of 64 calls in
+         * profiles/r6/coresidency/matrix.jsonl, 19.7 ms instead of 1.9).
+         * The bitsliced half failing (no memory for its key table) leaves the
          * T-table claim kernel to take every unit -- unless it was told to
          * take none (bs_only): then the T-table alone redoes the call.  The
          * join is recorded either way (a failure after its launch must still
