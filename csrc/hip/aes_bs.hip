@@ -715,6 +715,17 @@ hipError_t bs_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K
     return launch<BS_CTR>(P, K, st);
 }
 
+/* One-time warm-up of the split's bitsliced half (engine.cpp aux_take, when
+ * a device's first auxiliary stream is created): the runtime loads this
+ * file's code object at the first lookup of one of its kernels, and a first
+ * split call otherwise paid for that after its T-table half had started --
+ * which then took every unit (profiles/r6/coresidency/matrix.jsonl). */
+hipError_t bs_preload()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&k_aes_bs_claim<14, BS_ECB>));
+}
+
 /* The bitsliced halves of a claimed split: the whole buffer (block 0's
  * predecessor is iv_le), units from the front of `cl` */
 hipError_t bs_claim(int mode, const void *in, void *out, uint64_t nblocks, const otc_aes_key &K,

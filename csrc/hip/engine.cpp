@@ -63,6 +63,7 @@ hipError_t bs_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, boo
 hipError_t tt_ctr_shift(const void *, void *, size_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t xor_small(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
 hipError_t bs_claim(int, const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, SplitClaim, hipStream_t);
+hipError_t bs_preload();
 hipError_t tt_ecb_encrypt_claim(const void *, void *, uint64_t, const otc_aes_key &, SplitClaim, hipStream_t);
 hipError_t tt_cfb_decrypt_claim(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, SplitClaim,
                                 hipStream_t);
@@ -237,6 +238,8 @@ constexpr int AUX_MAX = 4;
 int g_aux_live[64];
 thread_local const char *g_split_fallback = "";
 
+__global__ void k_aux_noop() {}
+
 hipError_t aux_take(int dev, AuxStream &out)
 {
     {
@@ -273,6 +276,19 @@ hipError_t aux_take(int dev, AuxStream &out)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&a.fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&a.join, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&a.join_t, hipEventDisableTiming);
+    /* A new AuxStream's one-time costs, paid here and not inside the first
+     * split (whose T-table half is already queued when the bitsliced half
+     * launches -- engine.cpp split_claim): the bitsliced code object, and a
+     * first submission on each queue.  Without this a process's first split
+     * ran its halves one after the other (front 0 in 1 of 64 calls,
+     * profiles/r6/coresidency/matrix.jsonl). */
+    if (e == hipSuccess) e = otc_impl::bs_preload();
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_aux_noop, dim3(1), dim3(1), 0, a.s);
+        hipLaunchKernelGGL(k_aux_noop, dim3(1), dim3(1), 0, a.t);
+        if ((e = hipGetLastError()) == hipSuccess && (e = hipStreamSynchronize(a.s)) == hipSuccess)
+            e = hipStreamSynchronize(a.t);
+    }
     if (e != hipSuccess) {
         if (a.join_t) (void)hipEventDestroy(a.join_t);
         if (a.join) (void)hipEventDestroy(a.join);
@@ -380,10 +396,12 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
          * 128-160 KiB-LDS workgroups fit one per CU only when they are placed
          * before the bitsliced ones (two or three 168-VGPR bitsliced
          * workgroups on one CU leave no room for a T-table workgroup there).
-         * The price is a start-up transient: in a process's FIRST split call
-         * the bitsliced half's one-time costs (code object, key-table pool
-         * allocation) let the T-table half take every unit (1 of 64 calls in
-         * profiles/r6/coresidency/matrix.jsonl, 19.7 ms instead of 1.9).
+         * The bitsliced half's one-time costs (its code object, a first
+         * submission on each auxiliary queue) are therefore paid when the
+         * AuxStream is created (aux_take), not here: paid here, they let a
+         * process's first split call run the T-table half alone (front 0,
+         * profiles/r6/coresidency/matrix.jsonl; with the warm-up the first
+         * call co-runs, matrix_warm_aux.jsonl).
          * The bitsliced half failing (no memory for its key table) leaves the
          * T-table claim kernel to take every unit -- unless it was told to
          * take none (bs_only): then the T-table alone redoes the call.  The

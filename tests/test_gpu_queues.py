@@ -116,14 +116,11 @@ def split_bufs(gpu):
     x = torch.empty(GIB2, dtype=torch.uint8, device=gpu)
     ops.fill_random_(x, seed=21)
     o = torch.empty_like(x)
-    # The first split call of a process creates the auxiliary CU-masked
-    # streams and loads the bitsliced claim kernel; meanwhile the T-table
-    # half, launched first, takes every unit (front 0 in 1 of 64 calls of
-    # profiles/r6/coresidency/matrix.jsonl: exactly the process's first call,
-    # 19.7 ms against 1.9).  Warm both up once, as any long-running caller is.
-    for dec in (False, True):
-        (ops.ecb_decrypt if dec else ops.ecb_encrypt)(x, bytes(range(32)), out=o)
-    torch.cuda.synchronize()
+    # No warm-up: the process's first split call must co-run too.  (It did
+    # not before the library paid the auxiliary streams' one-time costs at
+    # their creation -- the bitsliced code object, a first submission per
+    # queue: front 0 in exactly the first of 64 calls of
+    # profiles/r6/coresidency/matrix.jsonl, 19.7 ms against 1.9.)
     yield x, o
     del x, o
 
