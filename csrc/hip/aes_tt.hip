@@ -978,14 +978,26 @@ __device__ __forceinline__ uint64_t cld64(const uint64_t *p) { return *(cptr64)p
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 typedef __attribute__((address_space(1))) uint8_t g_u8;
+/* OTC_BATCH_NT (default 1): the non-temporal bit on the message loads /
+ * stores -- each tile is read and written once, lane-linear.  Round 6 A/B,
+ * 3 reps (profiles/r6/batch_nt/): 1024 x 1 MiB packed 1484-1492 vs 1446-1460
+ * GB/s, 16384 x 4 KiB packed 1156-1164 vs 1136-1144, 262144 x 4 KiB
+ * 1191-1212 vs 1173-1192, 65536 x 1504 B even. */
+#ifndef OTC_BATCH_NT
+#define OTC_BATCH_NT 1
+#endif
 __device__ __forceinline__ uint4 gld16(const uint8_t *p, uint64_t blk)
 {
-    const u32x4 v = *(const g_u32x4 *)(p + 16 * blk);
+    const g_u32x4 *q = (const g_u32x4 *)(p + 16 * blk);
+    const u32x4 v = OTC_BATCH_NT ? __builtin_nontemporal_load(q) : *q;
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void gst16(uint8_t *p, uint64_t blk, uint4 v)
 {
-    *(g_u32x4 *)(p + 16 * blk) = u32x4{v.x, v.y, v.z, v.w};
+    g_u32x4 *q = (g_u32x4 *)(p + 16 * blk);
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    if (OTC_BATCH_NT) __builtin_nontemporal_store(w, q);
+    else *q = w;
 }
 
 template <int NR, int B, int THREADS>
