@@ -15,6 +15,7 @@ reference-compatible ``aes.h`` / ``arc4.h`` / ``rc4.h`` / ``aesni.h``
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
@@ -280,7 +281,22 @@ def require_gpu_lib():
             lib = ctypes.CDLL(GPU_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
             _declare_gpu(lib)
             _gpu_lib = lib
+            atexit.register(_release_at_exit)
     return _gpu_lib
+
+
+def _release_at_exit():
+    """Return the library's pooled device objects (the split's auxiliary
+    streams, the multi-GPU job's RCCL communicators) while the HIP runtime is
+    still up: left to the runtime's own teardown, the CU-masked auxiliary
+    streams were destroyed after a profiler's finalisation had run, and
+    ``rocprofv3`` then crashed in ``__cxa_finalize`` at the process's exit
+    (profiles/r6/rocprof/bench_full_exit_segv.txt)."""
+    if _gpu_lib is not None:
+        try:
+            _gpu_lib.otc_release_resources()
+        except Exception:  # noqa: BLE001 -- best effort at interpreter exit
+            pass
 
 
 def cpu_lib():
