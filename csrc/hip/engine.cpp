@@ -282,7 +282,8 @@ hipError_t aux_take(int dev, AuxStream &out)
      * first submission on each queue.  Without this a process's first split
      * ran its halves one after the other (front 0 in 1 of 64 calls,
      * profiles/r6/coresidency/matrix.jsonl). */
-    if (e == hipSuccess) e = otc_impl::bs_preload();
+    if (e == hipSuccess && otc_impl::bs_preload() != hipSuccess)
+        (void)hipGetLastError(); /* only a warm-up: the split works without it */
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_aux_noop, dim3(1), dim3(1), 0, a.s);
         hipLaunchKernelGGL(k_aux_noop, dim3(1), dim3(1), 0, a.t);
@@ -358,8 +359,11 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
 {
     *ran = OTC_IMPL_TTABLE;
     g_split_fallback = "";
+    /* bs_wgs 0 (and not bs_only): the T-table claim kernel alone, no fork --
+     * not a split request, so nothing to report if it runs plain() */
+    const bool fork = bs_wgs != 0 || bs_only;
     if (nunits < (bs_only ? 1 : min_units) || nunits > 0x7FFFFFFFull) {
-        g_split_fallback = "too few claim units";
+        if (fork) g_split_fallback = "too few claim units";
         return plain();
     }
     unsigned long long *ctr = nullptr;
@@ -368,13 +372,11 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
     hipError_t e = otc_dev::alloc_fault() ? hipErrorOutOfMemory : hipMallocAsync((void **)&ctr, 2 * sizeof *ctr, st);
     if (e != hipSuccess) {
         (void)hipGetLastError();
-        g_split_fallback = "no memory for the claim counter";
+        if (fork) g_split_fallback = "no memory for the claim counter";
         return plain();
     }
     int dev = 0;
     AuxStream a;
-    /* bs_wgs 0 (and not bs_only): the T-table claim kernel alone, no fork */
-    const bool fork = bs_wgs != 0 || bs_only;
     if (fork && (hipGetDevice(&dev) != hipSuccess || aux_take(dev, a) != hipSuccess)) {
         /* no auxiliary stream: the T-table alone still gives the output */
         (void)hipGetLastError();
