@@ -240,7 +240,7 @@ thread_local const char *g_split_fallback = "";
 
 __global__ void k_aux_noop() {}
 
-hipError_t aux_take(int dev, AuxStream &out)
+hipError_t aux_take(int dev, AuxStream &out, bool warm)
 {
     {
         std::lock_guard<std::mutex> lk(g_aux_mu);
@@ -282,9 +282,11 @@ hipError_t aux_take(int dev, AuxStream &out)
      * first submission on each queue.  Without this a process's first split
      * ran its halves one after the other (front 0 in 1 of 64 calls,
      * profiles/r6/coresidency/matrix.jsonl). */
-    if (e == hipSuccess && otc_impl::bs_preload() != hipSuccess)
+    if (warm && e == hipSuccess && otc_impl::bs_preload() != hipSuccess)
         (void)hipGetLastError(); /* only a warm-up: the split works without it */
-    if (e == hipSuccess) {
+    /* not while the caller's stream is being captured into a graph: a
+     * synchronisation there would invalidate the caller's capture */
+    if (warm && e == hipSuccess) {
         hipLaunchKernelGGL(k_aux_noop, dim3(1), dim3(1), 0, a.s);
         hipLaunchKernelGGL(k_aux_noop, dim3(1), dim3(1), 0, a.t);
         if ((e = hipGetLastError()) == hipSuccess && (e = hipStreamSynchronize(a.s)) == hipSuccess)
@@ -377,7 +379,12 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
     }
     int dev = 0;
     AuxStream a;
-    if (fork && (hipGetDevice(&dev) != hipSuccess || aux_take(dev, a) != hipSuccess)) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (fork && hipStreamIsCapturing(st, &cap) != hipSuccess) {
+        (void)hipGetLastError();
+        cap = hipStreamCaptureStatusActive; /* unknown: take the safe side */
+    }
+    if (fork && (hipGetDevice(&dev) != hipSuccess || aux_take(dev, a, cap == hipStreamCaptureStatusNone) != hipSuccess)) {
         /* no auxiliary stream: the T-table alone still gives the output */
         (void)hipGetLastError();
         (void)hipFreeAsync(ctr, st);

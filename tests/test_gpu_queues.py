@@ -181,3 +181,31 @@ def test_split_fallback_reason(gpu):
 
 def host_bytes(t):
     return t.cpu().numpy().tobytes()
+
+
+def test_split_captured_in_graph(gpu):
+    """A split call captured into a HIP graph (torch.cuda.CUDAGraph: stream
+    capture of the fork / join events, the claim counter's stream-ordered
+    allocation and both halves' launches) replays to the right bytes; a call
+    made while capturing never synchronises (engine.cpp aux_take: no warm-up
+    under capture)."""
+    from our_tree_amd import ops
+
+    key = bytes(range(32))
+    x = torch.empty(64 * 2048 * 16, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(x, seed=8)
+    o = torch.empty_like(x)
+    ops.ecb_encrypt(x, key, out=o, impl="split")
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.ecb_encrypt(x, key, out=o, impl="split")
+        ran = ops.last_impl()
+    assert ran == "split", (ran, ops.split_fallback_reason())
+    o.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert host_bytes(o) == cpu_ref.ecb(key, host_bytes(x))
+    g.replay()
+    torch.cuda.synchronize()
+    assert host_bytes(o) == cpu_ref.ecb(key, host_bytes(x))
