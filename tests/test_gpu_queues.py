@@ -209,3 +209,23 @@ def test_split_captured_in_graph(gpu):
     g.replay()
     torch.cuda.synchronize()
     assert host_bytes(o) == cpu_ref.ecb(key, host_bytes(x))
+
+
+@pytest.mark.parametrize("pooled", [False, True])
+def test_engine_queue_modes_same_bytes(gpu, pooled):
+    """Both queue arms of the pinned pipeline (dedicated, the default; pooled,
+    the A/B arm) produce the oracle's bytes -- CTR across chunk boundaries
+    and a tail, CBC decryption with its cross-chunk halo."""
+    from our_tree_amd.parallel import stream as pstream
+
+    n = (24 << 20) + 16 * 7 + 5
+    rng = np.random.default_rng(5 + pooled)
+    key, ctr = bytes(rng.integers(0, 256, 16, dtype=np.uint8).tolist()), bytes(range(16))
+    hin, hout = pstream.pinned_empty(n), pstream.pinned_empty(n)
+    hin[:] = rng.integers(0, 256, n, dtype=np.uint8)
+    with pstream.StreamEngine(gpu.index, chunk_bytes=4 << 20, depth=3, pooled_queues=pooled) as eng:
+        eng.run("ctr", hin, hout, key, ctr)
+        assert hout.tobytes() == cpu_ref.ctr(key, ctr, hin.tobytes())
+        m = n - n % 16
+        eng.run("cbc-dec", hin[:m], hout[:m], key, ctr)
+        assert hout[:m].tobytes() == cpu_ref.cbc(key, ctr, hin[:m].tobytes(), decrypt=True)
