@@ -42,6 +42,24 @@ def targets():
     return out
 
 
+def joint_targets():
+    """MixColumns merged with the next S-box's first layer (round 6 check):
+    per output byte the forms the S-box reads -- x0 and the pairwise XORs
+    x6^x5, x6^x2, x3^x1, x4^x2, x7^x4, x7^x1, x1^x0 (U7, T7, T11, T5, T4, T1,
+    T3, T21 of otc_sbox_lut3.h) -- each with its own key variable (100000 + k, clear of the signal numbers),
+    since every one of them is XORed with a key term."""
+    mc = targets()
+    out = []
+    for r in range(4):
+        x = [set(mc[8 * r + i]) for i in range(8)]
+        for pair in ((0,), (6, 5), (6, 2), (3, 1), (4, 2), (7, 4), (7, 1), (1, 0)):
+            s = set()
+            for i in pair:
+                s ^= x[i]
+            out.append(s)
+    return [frozenset(t | {100000 + k}) for k, t in enumerate(out)]
+
+
 def cost(k):
     return 0 if k <= 1 else k // 2  # ceil((k - 1) / 2) XOR3 nodes
 
@@ -138,10 +156,17 @@ def emit(ops, outs, order, nops, peak, seed):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seeds", default="0:120")
+    ap.add_argument("--joint", action="store_true",
+                    help="only compare MixColumns + 32 key folds with the merged first-layer targets")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "csrc",
                                                   "include", "otc_mixcol.h"))
     a = ap.parse_args()
     lo, hi = (int(x) for x in a.seeds.split(":"))
+    if a.joint:
+        mc = min(greedy(s)[0] for s in range(lo, hi))
+        jt = min(greedy(s, joint_targets())[0] for s in range(lo, hi))
+        print(f"MixColumns {mc} + 32 key-folding first-layer LUTs = {mc + 32}; merged: {jt}")
+        return
     best = None
     for seed in range(lo, hi):
         nops, prog, ts = greedy(seed)
