@@ -172,3 +172,21 @@ def test_ttable_claim_kernels_have_no_static_lds():
         assert lds == 0, (k, lds)
     # the grid kernels keep their static tables (128 / 160 KiB)
     assert any(lds >= 128 << 10 for k, (vg, lds) in d.items() if "_claim" not in k)
+
+
+def test_operand_statistics_as_documented():
+    """The static operand facts docs/PERF.md (round 6, "three hypotheses")
+    prices with tools/ubench/valu_bank.hip: ~17% of the AES-128 CTR bulk
+    kernel's VALU read an SGPR (a stream costs extra only when most of its
+    instructions do), and 6,078 of its 9,476 three-VGPR v_bitop3 share a
+    register bank (tools/isa_operands.py)."""
+    if not os.path.exists(OBJ) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):
+        pytest.skip("no built aes_bs.o (make) or no ROCm LLVM tools")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_operands.py"), OBJ], check=True,
+                         capture_output=True, text=True).stdout
+    m = re.search(r"VALU (\d+), reading an SGPR (\d+)", out)
+    assert m, out
+    valu, sg = int(m.group(1)), int(m.group(2))
+    assert 12000 <= valu <= 12900 and 0.10 <= sg / valu <= 0.25, (valu, sg)
+    three = {int(k): int(v) for k, v in re.findall(r"\('bitop3', 3, (\d)\): (\d+)", out)}
+    assert sum(three.values()) > 8000 and 0.4 <= (three.get(1, 0) + three.get(2, 0)) / sum(three.values()) <= 0.8
