@@ -574,12 +574,24 @@ int main(int argc, char **argv)
         if (run_op(&a) || otc_device_sync()) return 1;
         unsigned long long t0 = ~0ull;
         std::vector<std::vector<unsigned long long>> st(2);
+        std::vector<unsigned long long> ends; /* tag 5: a T-table claim wave out of units */
         for (int w = 0; w < 2; ++w) {
             const int n = otc_split_trace(w, rec.data(), 16384);
             for (int i = 0; i < n; ++i) {
+                if ((rec[2 * i + 1] >> 32) == 5) {
+                    ends.push_back(rec[2 * i]);
+                    continue;
+                }
                 st[w].push_back(rec[2 * i]);
                 if (w == 0) t0 = std::min(t0, rec[2 * i]);
             }
+        }
+        if (!ends.empty() && t0 != ~0ull) {
+            std::sort(ends.begin(), ends.end());
+            auto us = [&](unsigned long long t) { return ((double)t - (double)t0) / 100.0; };
+            fprintf(stderr, "strace ttable ends: %zu waves, end (us after the first T-table wave) min %.1f p10 %.1f median %.1f p90 %.1f max %.1f\n",
+                    ends.size(), us(ends.front()), us(ends[ends.size() / 10]), us(ends[ends.size() / 2]),
+                    us(ends[ends.size() * 9 / 10]), us(ends.back()));
         }
         for (int w = 0; w < 2; ++w) {
             auto &v = st[w];

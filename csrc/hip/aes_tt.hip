@@ -413,6 +413,7 @@ __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_ke
 #pragma unroll 1
             for (uint32_t it = 0; it < CLAIM_UNIT / (64u * B); ++it) chunk(u0 + it * 64u * B + lane, true, 0);
         }
+        strace(5); /* trace builds: when the wave ran out of units (the claim tail) */
         return;
     }
     for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nfull; base += (uint64_t)gridDim.x * PER)
@@ -625,6 +626,7 @@ __device__ __forceinline__ void dec_tt_body(const DecParams &P, const otc_aes_ke
 #pragma unroll 1
             for (uint32_t it = 0; it < CLAIM_UNIT / (64u * B); ++it) chunk((uint64_t)u * CLAIM_UNIT + it * 64u * B + lane, true);
         }
+        strace(5);
         return;
     }
     for (uint64_t base = (uint64_t)blockIdx.x * PER; base < P.nfull; base += (uint64_t)gridDim.x * PER)
