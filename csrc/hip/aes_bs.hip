@@ -569,9 +569,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                                                                                                otc_aes_key K)
 {
     strace(3);
-    for (;;) {
-        const int64_t u = claim_unit(P.cl, false);
-        if (u < 0) break;
+    const uint32_t w = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int64_t u = first_unit(P.cl, false, w); u >= 0; u = claim_unit(P.cl, false)) {
         /* the buffers opaque per task, as the lane (task_of): nothing derived
          * from them is hoisted; laundered as global pointers, or the loads and
          * stores become flat ones */

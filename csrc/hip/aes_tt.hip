@@ -406,9 +406,8 @@ __device__ __forceinline__ void enc_tt_body(const EncParams &P, const otc_aes_ke
             for (uint64_t base = done; base < P.nfull; base += PER)
                 chunk(base + (uint64_t)wave * 64u * B + lane, false, P.nfull);
         }
-        for (;;) {
-            const int64_t u = claim_unit(P.cl, true);
-            if (u < 0) break;
+        const uint32_t wg = blockIdx.x * (THREADS / 64u) + __builtin_amdgcn_readfirstlane(wave);
+        for (int64_t u = first_unit(P.cl, true, wg); u >= 0; u = claim_unit(P.cl, true)) {
             const uint64_t u0 = (uint64_t)u * CLAIM_UNIT;
 #pragma unroll 1
             for (uint32_t it = 0; it < CLAIM_UNIT / (64u * B); ++it) chunk(u0 + it * 64u * B + lane, true, 0);
@@ -620,9 +619,8 @@ __device__ __forceinline__ void dec_tt_body(const DecParams &P, const otc_aes_ke
         const uint64_t done = (uint64_t)P.cl.nunits * CLAIM_UNIT;
         if (blockIdx.x == 0)
             for (uint64_t base = done; base < P.nfull; base += PER) chunk(base + (uint64_t)wave * 64u * B + lane, false);
-        for (;;) {
-            const int64_t u = claim_unit(P.cl, true);
-            if (u < 0) break;
+        const uint32_t wg = blockIdx.x * (THREADS / 64u) + __builtin_amdgcn_readfirstlane(wave);
+        for (int64_t u = first_unit(P.cl, true, wg); u >= 0; u = claim_unit(P.cl, true)) {
 #pragma unroll 1
             for (uint32_t it = 0; it < CLAIM_UNIT / (64u * B); ++it) chunk((uint64_t)u * CLAIM_UNIT + it * 64u * B + lane, true);
         }
@@ -831,11 +829,9 @@ __global__ __launch_bounds__(1024) OTC_CLAIM_ATTR void k_aes_seg_enc_tt_claim(Cb
         const uint64_t seg = done + threadIdx.x;
         seg_chain_g<NR, G, CFB, false>(P, K, DynTbl{}, lk, seg, seg < P.nseg);
     }
-    for (;;) {
-        const int64_t u = claim_unit(P.cl, true);
-        if (u < 0) break;
+    const uint32_t wg = blockIdx.x * 16u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int64_t u = first_unit(P.cl, true, wg); u >= 0; u = claim_unit(P.cl, true))
         seg_chain_g<NR, G, CFB, false>(P, K, DynTbl{}, lk, (uint64_t)u * SEG_UNIT + lane_id(), true);
-    }
 }
 
 /* CBC-decrypt over segments of ANY length: the plain CBC kernel XORs every

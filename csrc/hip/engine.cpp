@@ -345,7 +345,7 @@ __global__ void k_claim_snapshot(unsigned long long *ctr, unsigned long long *ho
     const unsigned long long v = __hip_atomic_fetch_add(ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-thread_local uint64_t g_split_word = 0, g_split_nunits = 0, g_split_ttwaves = 0;
+thread_local uint64_t g_split_word = 0, g_split_nunits = 0, g_split_ttwaves = 0, g_split_pb = 0;
 
 /* The split: tt(cl) launches the T-table claim kernel on st, bs(cl, aux) the
  * bitsliced claim kernel on the auxiliary stream, both over the whole buffer
@@ -390,8 +390,21 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
         (void)hipFreeAsync(ctr, st);
         return plain();
     }
-    const SplitClaim cl{ctr, (uint32_t)nunits, bs_wgs};
-    const SplitClaim cl_tt{bs_only ? ctr + 1 : ctr, (uint32_t)nunits, bs_only ? 1u : 0u};
+    /* first units handed out without a claim (otc_device.h SplitClaim): the
+     * last ones to the T-table waves (16 per workgroup, one workgroup per
+     * CU), the first ones to the bitsliced waves (4 per workgroup) */
+#ifndef OTC_CLAIM_NO_PREASSIGN /* A/B arm: every unit claimed (make variant VFLAGS=-DOTC_CLAIM_NO_PREASSIGN) */
+    const uint32_t pb = bs_only ? 0u : (uint32_t)std::min<uint64_t>(nunits, 16ull * (uint64_t)otc_dev::device_cus());
+    const uint32_t pf = (uint32_t)std::min<uint64_t>(nunits - pb, 4ull * bs_wgs);
+#else
+    const uint32_t pb = 0, pf = 0;
+#endif
+    SplitClaim cl{ctr, (uint32_t)nunits, bs_wgs};
+    cl.pf = pf;
+    cl.pb = pb;
+    SplitClaim cl_tt{bs_only ? ctr + 1 : ctr, (uint32_t)nunits, bs_only ? 1u : 0u};
+    cl_tt.pf = bs_only ? 0u : pf;
+    cl_tt.pb = pb;
     /* zeroed (bs_only: the T-table's word all ones -- front + back far past
      * nunits, so its claims fail; hipMemsetD32Async at a 4-byte offset cost
      * ~40 ms per call), then fork: the aux stream starts after everything
@@ -448,6 +461,7 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
                      * one per CU; each of their waves ends on one failed
                      * claim */
                     g_split_ttwaves = bs_only ? 0 : 16ull * (uint64_t)otc_dev::device_cus();
+                    g_split_pb = pb; /* the T-table's units taken without a claim */
                 }
             }
         } else if (fork) {
@@ -709,9 +723,10 @@ extern "C" int otc_split_last_units(uint64_t *front, uint64_t *back, uint64_t *n
 {
     if (!front || !back || !nunits) return set_err(OTC_ERR_ARG, "null argument");
     /* every T-table wave ends on one failed back claim (+1 each), so the
-     * back count less those is what the T-table took; the front took the rest */
+     * back count less those, plus the units the T-table waves started on
+     * without a claim, is what the T-table took; the front took the rest */
     const uint64_t b = g_split_word >> 32, n = g_split_nunits;
-    *back = b > g_split_ttwaves ? std::min(n, b - g_split_ttwaves) : 0;
+    *back = std::min(n, g_split_pb + (b > g_split_ttwaves ? b - g_split_ttwaves : 0));
     *front = n - *back;
     *nunits = n;
     return OTC_OK;

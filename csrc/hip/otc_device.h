@@ -127,12 +127,20 @@ enum : int { BS_CTR = 0, BS_ECB = 1, BS_ECB_DEC = 2, BS_CBC_DEC = 3, BS_CFB_DEC 
  * block units and a reserve left to the T-table measured 1-11% slower and
  * were removed, profiles/r4/claim_unit/); 64 segments for the persistent
  * segment-encryption kernel (one T-table wave, back claims only).
- * A wave claims with one lane (a vector-memory atomic) and broadcasts. */
+ * A wave claims with one lane (a vector-memory atomic) and broadcasts.
+ * First units without a claim: the host hands the first pf units to the
+ * bitsliced waves (wave j < pf starts on unit j) and the last pb units to the
+ * T-table waves (wave w < pb starts on unit nunits - 1 - w); the claim word
+ * covers the units between.  Otherwise every wave's FIRST claim lands on the
+ * word at once -- 4096 T-table waves queue ~45 us on one address (~90 atomics
+ * per us), the last of them idle that long (docs/PERF.md round 6). */
 constexpr uint32_t CLAIM_UNIT = 2048u;
 struct SplitClaim {
     unsigned long long *ctr; /* zeroed (stream-ordered) before the launches */
     uint32_t nunits;         /* full units */
     uint32_t wgs;            /* host side: workgroups of the kernel given this claim (0: one per CU) */
+    uint32_t pf = 0;         /* units [0, pf): the bitsliced waves' first units, unclaimed */
+    uint32_t pb = 0;         /* units [nunits - pb, nunits): the T-table waves' first units, unclaimed */
 };
 
 /* lane id from the exec-mask count: nothing to keep live across a loop
@@ -190,8 +198,16 @@ __device__ __forceinline__ int64_t claim_unit(const SplitClaim &c, bool back)
 {
     const uint64_t old = claim_add(c, back ? (1ull << 32) : 1ull);
     const uint32_t f = (uint32_t)old, b = (uint32_t)(old >> 32);
-    if ((uint64_t)f + b >= c.nunits) return -1;
-    return back ? (int64_t)(c.nunits - 1u - b) : (int64_t)f;
+    if ((uint64_t)f + b + c.pf + c.pb >= c.nunits) return -1;
+    return back ? (int64_t)(c.nunits - c.pb - 1u - b) : (int64_t)(c.pf + f);
+}
+
+/* a wave's first unit: its pre-assigned one (w: the wave's index among its
+ * kernel's waves, wave-uniform), else its first claim */
+__device__ __forceinline__ int64_t first_unit(const SplitClaim &c, bool back, uint32_t w)
+{
+    if (back ? w < c.pb : w < c.pf) return back ? (int64_t)(c.nunits - 1u - w) : (int64_t)w;
+    return claim_unit(c, back);
 }
 
 /* Wave-start trace of the splits (a diagnostic build: make variant
@@ -208,11 +224,17 @@ static __device__ unsigned int g_strace_n;
 __device__ __forceinline__ void strace(uint32_t tag)
 {
     if (lane_id() == 0) {
+        /* the clock first: thousands of waves queue on the slot counter's
+         * atomic (~90 per us on one word), and a time read after it measured
+         * that queue -- a 45-55 us "start ramp" the chip does not have
+         * (tools/ubench/launch_ramp.hip: 256 x 1024-thread workgroups with
+         * 128 KiB LDS start within 2.3 us) */
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
         const unsigned i = atomicAdd(&g_strace_n, 1u);
         if (i < STRACE_MAX) {
             uint32_t hw;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-            g_strace[2 * i] = __builtin_amdgcn_s_memrealtime();
+            g_strace[2 * i] = now;
             g_strace[2 * i + 1] = (unsigned long long)tag << 32 | hw;
         }
     }

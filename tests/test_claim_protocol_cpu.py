@@ -54,3 +54,41 @@ def test_bitsliced_only_mode():
             break
         seen += us
     assert seen == list(range(nunits))
+
+
+def claim_pre(counter, nunits, back, pf, pb):
+    """claim_unit with pre-assigned first units: the word covers the units
+    between the pf first and the pb last"""
+    f, b = counter & 0xFFFFFFFF, counter >> 32
+    counter += (1 << 32) if back else 1
+    if f + b + pf + pb >= nunits:
+        return counter, []
+    return counter, [nunits - pb - 1 - b] if back else [pf + f]
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_preassigned_first_units(seed):
+    """engine.cpp split_claim hands the T-table waves (w < pb) unit
+    nunits - 1 - w and the bitsliced waves (j < pf) unit j before any claim
+    (otc_device.h first_unit): with any interleaving every unit is still
+    taken exactly once, the front holds a prefix."""
+    rnd = random.Random(seed)
+    for _ in range(300):
+        nunits = rnd.randint(1, 300)
+        nb, nf = rnd.randint(1, 24), rnd.randint(0, 12)
+        pb = min(nunits, nb)
+        pf = min(nunits - pb, nf)
+        seen = [nunits - 1 - w for w in range(pb)] + list(range(pf))
+        front = list(range(pf))
+        counter = 0
+        live = ["b"] * nb + ["f"] * nf
+        while live:
+            w = rnd.randrange(len(live))
+            counter, us = claim_pre(counter, nunits, live[w] == "b", pf, pb)
+            if not us:
+                live.pop(w)
+            elif live[w] == "f":
+                front += us
+            seen += us
+        assert sorted(seen) == list(range(nunits)), (nunits, nb, nf)
+        assert sorted(front) == list(range(len(front)))
