@@ -2,7 +2,7 @@
 # kernel-trace profile of the whole bench (every extra pass).
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-D=gpurun_out/r6/final; mkdir -p $D
+D=gpurun_out/r6/${OUT:-final}; mkdir -p $D
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > $D/pytest_gpu.log 2>&1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1
 timeout -k 10 400 python bench.py > $D/bench.json 2> $D/bench.err
