@@ -1,12 +1,12 @@
 #!/bin/bash
 # Round 6: claim kernels with pre-assigned first units (the release) vs
-# every unit claimed (variants/nopre), interleaved reps, one box.  First:
+# every unit claimed (${ARM:-variants/nopre}), interleaved reps, one box.  First:
 # every claimed form verified on the release -- T-table alone (1 GiB + an odd
 # remainder), split (2 GiB + odd), bitsliced alone (impl bitslice), segment
 # encryption / decryption -- and the split / queue GPU tests.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-O=gpurun_out/r6/preassign
+O=gpurun_out/r6/${OUT:-preassign}
 mkdir -p $O
 B=our_tree_amd/lib
 V() { LD_LIBRARY_PATH=$B timeout -k 10 60 ./bin/otbench "$@" --iters 2 --warmup 1 --verify >> $O/verify.jsonl 2>&1 ||
@@ -27,7 +27,7 @@ timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thre
     { echo "PYTEST FAILED"; tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 for rep in 1 2 3; do
-  for lib in variants/nopre $B; do
+  for lib in ${ARM:-variants/nopre} $B; do
     for cfg in "ecb 128 1G" "ecb 256 1G" "cbc-dec 128 1G" "ecb 128 2G" "ecb 256 8G" "cbc-enc-seg 256 2G"; do
       set -- $cfg
       extra=""; [ $1 = cbc-enc-seg ] && extra="--seg 4096"
@@ -38,12 +38,12 @@ for rep in 1 2 3; do
 done
 python3 - <<'PY'
 import json, collections
-rows = [json.loads(l) for l in open("gpurun_out/r6/preassign/ab.jsonl") if l.startswith("{")]
+rows = [json.loads(l) for l in open("gpurun_out/r6/" + __import__("os").environ.get("OUT", "preassign") + "/ab.jsonl") if l.startswith("{")]
 by = collections.defaultdict(list)
 for r in rows:
     by[(r["mode"], r["bits"], r["bytes"] >> 20, r["ran"], r["lib"])].append(r["gbps"])
 for k in sorted(by):
     print(k, " ".join(f"{v:.1f}" for v in by[k]))
 PY
-LD_LIBRARY_PATH=variants/strace timeout -k 10 60 ./bin/otbench --mode ecb --bits 128 --bytes 1G --impl ttable --iters 10 \
-    --warmup 3 --strace > $O/trace.log 2>&1 && grep strace $O/trace.log
+[ -d variants/strace ] && LD_LIBRARY_PATH=variants/strace timeout -k 10 60 ./bin/otbench --mode ecb --bits 128 --bytes 1G --impl ttable --iters 10 \
+    --warmup 3 --strace > $O/trace.log 2>&1 && grep strace $O/trace.log || true
