@@ -486,9 +486,23 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
  * round 5 at 1000 MiB (midsize_persistent_vs_grid.jsonl, 2 reps): ECB-256
  * 1068-1074 vs 1027-1031, ECB-dec-256 1053-1056 vs 872-911, CBC / CFB-dec
  * +1%, ECB-128 +2-9%; 1.5 GiB -4..+7%; at 512 MiB and below it ties or
- * loses. */
+ * loses.  Round 6, with the first claim units handed out (no first-claim
+ * queue): from 512 MiB -- ECB-128 512 / 768 MiB +2.8 / +3.7%, ECB-256 +4.4 /
+ * +4.4%, ECB-dec-256 +2.8 / +5.5%, CBC-dec-128 -1 / +2.7%; at 256 MiB mixed
+ * (-4..+1.5%) (profiles/r6/xover/). */
 enum { FORM_SPLIT = 0, FORM_BS = 1, FORM_TT = 2 };
-size_t tt_persistent_min() { return (size_t)896 << 20; }
+/* OTC_TT_PERSISTENT_MIN_MIB / OTC_SEGENC_PERSISTENT_MIN_MIB: threshold
+ * sweeps only (read once; unset = the measured defaults) */
+size_t env_mib(const char *name, size_t dflt)
+{
+    const char *v = getenv(name);
+    return v && *v ? (size_t)strtoull(v, nullptr, 10) << 20 : dflt;
+}
+size_t tt_persistent_min()
+{
+    static const size_t m = env_mib("OTC_TT_PERSISTENT_MIN_MIB", (size_t)512 << 20);
+    return m;
+}
 int split_form(int picked, size_t nbytes)
 {
     if (picked == OTC_IMPL_SPLIT) return FORM_SPLIT;
@@ -592,7 +606,11 @@ thread_local int g_last_impl = OTC_IMPL_AUTO;
  * 1 KiB), where it beats the grid kernel by 4-15% (AES-256 4 KiB segments:
  * 2 GiB 1027 vs 986, 4 GiB 1040 vs 969, 32 GiB 1142 vs 995; 512 B at 1 GiB
  * 986 vs 951; AES-128 4 GiB 1383 vs 1267); below that the grid kernel (1 GiB
- * of 4 KiB segments: 916 vs 948; profiles/r5/split_thresholds/).  A VALU
+ * of 4 KiB segments: 916 vs 948; profiles/r5/split_thresholds/).  Round 6,
+ * first claim units handed out: from 1 GiB for every segment size (AES-256
+ * 4 KiB segments: 1 GiB 957-959 vs 948-950, 1.5 GiB 1036 vs 790-801 -- the
+ * grid kernel's 384 workgroups there are 1.5 per CU; 512 MiB 542 vs 554-558;
+ * profiles/r6/xover/).  A VALU
  * half for this mode (the row-sliced 8-chains-per-lane kernel of round 5)
  * lost at every size -- AES-256 4 GiB 775 vs 1040 GB/s for the claim kernel
  * alone (profiles/r5/split_ab/remeasure_int_lds.jsonl) -- and was removed
@@ -603,7 +621,9 @@ int pick_segenc_impl(int, size_t, size_t) { return OTC_IMPL_TTABLE; }
 
 bool segenc_persistent(size_t nbytes, size_t seg_bytes, size_t nseg)
 {
-    const size_t min_bytes = seg_bytes <= 1024 ? ((size_t)1 << 30) : ((size_t)2 << 30);
+    static const size_t env = env_mib("OTC_SEGENC_PERSISTENT_MIN_MIB", (size_t)1 << 30);
+    const size_t min_bytes = env;
+    (void)seg_bytes;
     return nbytes >= min_bytes && nseg / SEG_UNIT >= 16 && nseg / SEG_UNIT <= 0x7FFFFFFFull;
 }
 

@@ -61,8 +61,8 @@ int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 #define OTC_IMPL_AUTO 0     /* the measured winner (docs/PERF.md rounds 5-6): bitsliced for CTR calls >= 2 GiB
                                (AES-256: >= 1 GiB); for ECB / CBC / CFB decryption and the power-of-two segment
                                decryptions the split below from 2 GiB and the persistent T-table claim kernel
-                               alone from 896 MiB; segment encryption: the persistent T-table claim kernel from
-                               2 GiB (1 GiB for segments <= 1 KiB); the grid T-table otherwise
+                               alone from 512 MiB; segment encryption: the persistent T-table claim kernel from
+                               1 GiB; the grid T-table otherwise
                                (OTC_IMPL=ttable|bitslice|split env overrides for the whole process, each where it
                                applies: split for ECB and the decryptions only) */
 #define OTC_IMPL_TTABLE 1   /* LDS-resident replicated T-table kernel */
@@ -167,7 +167,7 @@ int otc_aes_cbc_encrypt_segments_impl(const void *in, void *out, size_t seg_byte
                                       const otc_aes_key *k, const uint8_t iv0[16], int impl, void *stream);
 /* Same, decryption side (fully parallel).  _impl: with a kernel choice --
  * "auto" runs the T-table + bitsliced split from 2 GiB of power-of-two
- * segments and the persistent T-table claim kernel alone from 896 MiB;
+ * segments and the persistent T-table claim kernel alone from 512 MiB;
  * OTC_IMPL_BITSLICE runs the bitsliced segment claim kernel alone; other
  * segment sizes: T-table. */
 int otc_aes_cbc_decrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
@@ -191,7 +191,7 @@ int otc_aes_cfb128_decrypt_segments_impl(const void *in, void *out, size_t seg_b
 /* CFB128 decryption (parallel): P_i = C_i ^ E(C_{i-1}), C_{-1} = iv;
  * nbytes % 16 == 0; encryption key.  _impl: with a kernel choice (the plain
  * form is OTC_IMPL_AUTO: the T-table + bitsliced split from 2 GiB, the
- * persistent T-table claim kernel from 896 MiB, like ECB encryption). */
+ * persistent T-table claim kernel from 512 MiB, like ECB encryption). */
 int otc_aes_cfb128_decrypt(const void *in, void *out, size_t nbytes, const otc_aes_key *k,
                            const uint8_t iv[16], void *stream);
 int otc_aes_cfb128_decrypt_impl(const void *in, void *out, size_t nbytes, const otc_aes_key *k,

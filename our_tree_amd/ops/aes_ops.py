@@ -476,7 +476,7 @@ def ecb_encrypt(x: torch.Tensor, key: bytes, out=None, impl="auto") -> torch.Ten
 def ecb_decrypt(x: torch.Tensor, key: bytes, out=None, impl="auto") -> torch.Tensor:
     """ECB decryption: the T-table inverse cipher, the bitsliced one (the
     forward S-box as S^-1 = L S L), or both concurrently ("split").  "auto":
-    the split from 2 GiB, the persistent T-table claim kernel alone from 896
+    the split from 2 GiB, the persistent T-table claim kernel alone from 512
     MiB, the grid T-table below (engine.cpp pick_ecb_impl / split_form)."""
     _check_dev(x, "x")
     out = _out_like(x, out)
@@ -507,7 +507,7 @@ def cbc_encrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes:
     """CBC encryption of independent contiguous segments; segment s uses
     IV = iv0 + s (128-bit BE), one serial chain per segment, one chain per
     lane on the T-table kernels for every ``impl`` (the persistent claim
-    kernel from 2 GiB -- 1 GiB for segments <= 1 KiB -- the grid kernel
+    kernel from 1 GiB, the grid kernel
     below; a VALU kernel for this mode lost at every size and was removed).  A
     single segment is exact serial CBC on ONE lane -- use
     ``models.AES.cbc_encrypt`` (routes exact single-stream encryption to the
@@ -520,7 +520,7 @@ def cbc_decrypt_segments(x: torch.Tensor, key: bytes, iv0: bytes, segment_bytes:
     """Inverse of ``cbc_encrypt_segments``: fully parallel.  ``impl``:
     "ttable", "bitslice" (the bitsliced claim kernel alone), "split" (both at
     once), "auto" = split from 2 GiB of power-of-two segments, the persistent
-    T-table claim kernel from 896 MiB (other segment sizes: the T-table)."""
+    T-table claim kernel from 512 MiB (other segment sizes: the T-table)."""
     _check_dev(x, "x")
     out = _out_like(x, out)
     n = _nbytes(x)
