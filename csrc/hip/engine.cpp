@@ -405,12 +405,14 @@ hipError_t split_claim(uint64_t nunits, uint64_t min_units, bool bs_only, unsign
     SplitClaim cl_tt{bs_only ? ctr + 1 : ctr, (uint32_t)nunits, bs_only ? 1u : 0u};
     cl_tt.pf = bs_only ? 0u : pf;
     cl_tt.pb = pb;
-    /* zeroed (bs_only: the T-table's word all ones -- front + back far past
-     * nunits, so its claims fail; hipMemsetD32Async at a 4-byte offset cost
-     * ~40 ms per call), then fork: the aux stream starts after everything
-     * queued on st */
+    /* word 0 zeroed; word 1 only where it is used (bs_only: the T-table's
+     * word, all ones -- front + back far past nunits, so its claims fail;
+     * hipMemsetD32Async at a 4-byte offset cost ~40 ms per call): one fill
+     * kernel per call instead of two (no measurable rate change at 0.5-2 GiB,
+     * profiles/r6/claim_tail/one_fill_ab.jsonl).  Then fork: the aux stream
+     * starts after everything queued on st */
     if ((e = hipMemsetAsync(ctr, 0, sizeof *ctr, st)) == hipSuccess &&
-        (e = hipMemsetAsync(ctr + 1, bs_only ? 0xFF : 0, sizeof *ctr, st)) == hipSuccess &&
+        (!bs_only || (e = hipMemsetAsync(ctr + 1, 0xFF, sizeof *ctr, st)) == hipSuccess) &&
         (!fork || ((e = hipEventRecord(a.fork, st)) == hipSuccess && (e = hipStreamWaitEvent(a.s, a.fork, 0)) == hipSuccess &&
                    (e = hipStreamWaitEvent(a.t, a.fork, 0)) == hipSuccess)) &&
         (e = tt(cl_tt, fork ? a.t : st)) == hipSuccess) {
