@@ -1,4 +1,6 @@
 #!/bin/bash
+# ARCHIVED: the A/B arm (variants/twomemset, OTC_CLAIM_TWO_MEMSETS) was removed
+# after this run (profiles/r6/claim_tail/one_fill_ab.jsonl).
 # Round 6: one claim-counter fill per call (the release) vs two
 # (variants/twomemset), 3 interleaved reps, mid sizes where a few us count;
 # the release verified on every claimed form first.
