@@ -32,6 +32,8 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -796,15 +798,30 @@ __device__ __forceinline__ void seg_chain_g(const CbcSegParams &P, const otc_aes
     }
 }
 
+/* One chain per thread; the workgroup size is chosen at launch (a multiple
+ * of 64 up to THREADS): with fewer chains than CUs x THREADS the launch
+ * shrinks the workgroups so that every CU gets chains, instead of filling
+ * nseg / THREADS CUs and leaving the rest idle (launch_seg_nr). */
 template <int NR, int THREADS, int G, bool CFB = false>
 __global__ __launch_bounds__(THREADS) void k_aes_cbc_enc_seg_g(CbcSegParams P, otc_aes_key K)
 {
     __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
-    fill_tbl4<THREADS>(tbl, g_tab.te0);
+    const uint32_t nt = blockDim.x;
+    if (nt == THREADS) {
+        fill_tbl4<THREADS>(tbl, g_tab.te0);
+    } else {
+        uint4 *l4 = reinterpret_cast<uint4 *>(tbl);
+        for (uint32_t q = threadIdx.x; q < 8192; q += nt) {
+            const uint32_t r = q >> 12, x = (q >> 4) & 255, half = (q >> 3) & 1, k = 2 * r + half;
+            const uint32_t t = g_tab.te0[x];
+            const uint32_t v = k ? ((t << (8 * k)) | (t >> (32 - 8 * k))) : t;
+            l4[q] = make_uint4(v, v, v, v);
+        }
+    }
     __syncthreads();
     uint32_t lk[4];
     tbl4_lane_consts(threadIdx.x & 63u, lk);
-    for (uint64_t base = (uint64_t)blockIdx.x * THREADS; base < P.nseg; base += (uint64_t)gridDim.x * THREADS) {
+    for (uint64_t base = (uint64_t)blockIdx.x * nt; base < P.nseg; base += (uint64_t)gridDim.x * nt) {
         const uint64_t seg = base + threadIdx.x;
         seg_chain_g<NR, G, CFB>(P, K, tbl, lk, seg, seg < P.nseg);
     }
@@ -1270,10 +1287,17 @@ hipError_t launch_seg_nr(const CbcSegParams &P, const otc_aes_key &K, hipStream_
      * profiles/r1/otbench_cbcenc_group_ab.jsonl); B = 1: two 8-block buffers
      * per segment fit without spills.  Segments shorter than 8 blocks take the
      * per-block kernel. */
-    if (P.seg_blocks >= OTC_SEG_G)
-        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, SEG_THREADS, OTC_SEG_G, CFB>),
-                           dim3(grid_for(P.nseg, (uint64_t)SEG_THREADS, 1)), dim3(SEG_THREADS), 0, st, P, K);
-    else
+    if (P.seg_blocks >= OTC_SEG_G) {
+        /* fewer chains than CUs x SEG_THREADS: smaller workgroups on every CU
+         * (e.g. 768 MiB of 4 KiB segments: 256 x 768 threads, not 192 x 1024) */
+        uint64_t nt = SEG_THREADS;
+        const uint64_t cus = (uint64_t)num_cus();
+#ifndef OTC_SEG_FIXED_WG /* A/B arm: 1024-thread workgroups at every size */
+        if (P.nseg < cus * SEG_THREADS) nt = std::max<uint64_t>(64, ((P.nseg + cus - 1) / cus + 63) / 64 * 64);
+#endif
+        hipLaunchKernelGGL((k_aes_cbc_enc_seg_g<NR, SEG_THREADS, OTC_SEG_G, CFB>), dim3(grid_for(P.nseg, nt, 1)),
+                           dim3((unsigned)nt), 0, st, P, K);
+    } else
         hipLaunchKernelGGL((k_aes_cbc_enc_seg<NR, SEG_B, SEG_THREADS, CFB>), dim3(grid), dim3(SEG_THREADS), 0, st, P,
                            K);
     return hipGetLastError();
