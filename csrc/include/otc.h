@@ -160,8 +160,9 @@ int otc_aes_cbc_decrypt_impl(const void *in, void *out, size_t nbytes, const otc
 int otc_aes_cbc_encrypt_segments(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                  const otc_aes_key *k, const uint8_t iv0[16], void *stream);
 /* _impl: accepted for symmetry; every impl runs the T-table kernels (one
- * serial chain per lane): the persistent claim kernel from 2 GiB (1 GiB for
- * segments <= 1 KiB, at least 1024 segments), the grid kernel below.  A VALU
+ * serial chain per lane): the persistent claim kernel from 1 GiB (at least
+ * 1024 segments), the grid kernel below (its workgroups sized so every CU
+ * gets chains).  A VALU
  * kernel for this mode lost at every size and was removed (round 6). */
 int otc_aes_cbc_encrypt_segments_impl(const void *in, void *out, size_t seg_bytes, size_t nseg,
                                       const otc_aes_key *k, const uint8_t iv0[16], int impl, void *stream);
