@@ -477,9 +477,71 @@ struct CtrParams {
     uint32_t wrap64;
     uint64_t shift;   /* ctr0.lo mod PER */
     Ctr128 cbase;     /* ctr0 - shift (low log2(PER) bits zero) */
+    SplitClaim cl;    /* k_aes_ctr_tt_persist: 2048-block units of the virtual range */
 };
 
 __device__ __forceinline__ uint32_t te_u(uint32_t idx) { return g_tab.te0[idx & 0xFFu]; } /* uniform lookup */
+
+/* one wave-iteration: the 64 x B blocks from virtual block vw (uniform,
+ * a multiple of 64 x B) */
+template <int NR, int B>
+__device__ __forceinline__ void ctr_cached_iter(const CtrParams &P, const otc_aes_key &K, const uint32_t *tbl,
+                                                const uint32_t (&lk)[4], uint32_t lane, uint64_t vw)
+{
+    /* uniform counter C = cbase + vw */
+    uint64_t clo = P.cbase.lo + vw;
+    uint64_t chi = P.cbase.hi + ((!P.wrap64 && clo < P.cbase.lo) ? 1u : 0u);
+    const uint32_t w0 = bswap32((uint32_t)(chi >> 32)) ^ K.rk[0];
+    const uint32_t w1 = bswap32((uint32_t)chi) ^ K.rk[1];
+    const uint32_t w2 = bswap32((uint32_t)(clo >> 32)) ^ K.rk[2];
+    const uint32_t w3u = bswap32((uint32_t)clo) ^ K.rk[3]; /* byte 15 (top byte) patched per block */
+    /* round 1, uniform parts */
+    const uint32_t U0 = te_u(w0) ^ rotl8(te_u(w1 >> 8)) ^ rotl16(te_u(w2 >> 16)) ^ K.rk[4];
+    const uint32_t t1 = te_u(w1) ^ rotl8(te_u(w2 >> 8)) ^ rotl16(te_u(w3u >> 16)) ^ rotl24(te_u(w0 >> 24)) ^ K.rk[5];
+    const uint32_t t2 = te_u(w2) ^ rotl8(te_u(w3u >> 8)) ^ rotl16(te_u(w0 >> 16)) ^ rotl24(te_u(w1 >> 24)) ^ K.rk[6];
+    const uint32_t t3 = te_u(w3u) ^ rotl8(te_u(w0 >> 8)) ^ rotl16(te_u(w1 >> 16)) ^ rotl24(te_u(w2 >> 24)) ^ K.rk[7];
+    /* round 2, uniform parts */
+    const uint32_t V0 = rotl8(te_u(t1 >> 8)) ^ rotl16(te_u(t2 >> 16)) ^ rotl24(te_u(t3 >> 24)) ^ K.rk[8];
+    const uint32_t V1 = te_u(t1) ^ rotl8(te_u(t2 >> 8)) ^ rotl16(te_u(t3 >> 16)) ^ K.rk[9];
+    const uint32_t V2 = te_u(t2) ^ rotl8(te_u(t3 >> 8)) ^ rotl24(te_u(t1 >> 24)) ^ K.rk[10];
+    const uint32_t V3 = te_u(t3) ^ rotl16(te_u(t1 >> 16)) ^ rotl24(te_u(t2 >> 24)) ^ K.rk[11];
+    const uint32_t b15 = (uint32_t)(clo & 0xFFu); /* low byte of C (low 6+log2(B) bits are 0) */
+
+    const int64_t i0 = (int64_t)vw - (int64_t)P.shift + lane; /* real block index of (b=0, lane) */
+    const bool full = vw >= P.shift && vw - P.shift + 64u * B <= P.nfull; /* uniform */
+    uint32_t s[B][4];
+    uint4 x[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const int64_t i = i0 + 64 * b;
+        const bool ok = full || (i >= 0 && (uint64_t)i < P.nfull);
+        x[b] = ok ? lds16(P.in, (uint64_t)i) : make_uint4(0, 0, 0, 0);
+        /* round 1: only T3[byte 15] varies */
+        const uint32_t c15 = (b15 | (uint32_t)(64 * b) | lane) ^ (K.rk[3] >> 24);
+        const uint32_t s0 = U0 ^ lds_at(tbl, (c15 << 8) | lk[3]);
+        /* round 2: the four lookups fed by s0 */
+        s[b][0] = V0 ^ lds_at(tbl, tt_addr(s0, lk[0], 0));
+        s[b][1] = V1 ^ lds_at(tbl, tt_addr(s0, lk[3], 3));
+        s[b][2] = V2 ^ lds_at(tbl, tt_addr(s0, lk[2], 2));
+        s[b][3] = V3 ^ lds_at(tbl, tt_addr(s0, lk[1], 1));
+    }
+    /* rounds 3..NR */
+    enc_rounds4_from<3, NR, B>(tbl, lk, K, s);
+
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const int64_t i = i0 + 64 * b;
+        const bool ok = full || (i >= 0 && (uint64_t)i < P.nfull);
+        if (ok) {
+            sts16(P.out, (uint64_t)i,
+                 make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
+        } else if (i >= 0 && (uint64_t)i == P.nfull && P.tail) {
+            const uint32_t ks[4] = {s[b][0], s[b][1], s[b][2], s[b][3]};
+            for (uint32_t n = 0; n < P.tail; ++n)
+                P.out[16 * (uint64_t)i + n] = P.in[16 * (uint64_t)i + n] ^ (uint8_t)(ks[n >> 2] >> (8 * (n & 3)));
+        }
+    }
+}
 
 template <int NR, int B, int THREADS>
 __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_aes_key K)
@@ -493,64 +555,34 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_tt_cached(CtrParams P, otc_
     uint32_t lk[4];
     tbl4_lane_consts(lane, lk);
     constexpr uint64_t PER = (uint64_t)THREADS * B;
-    const uint64_t ntotal = P.nfull + (P.tail ? 1u : 0u);
-    const uint64_t vtotal = ntotal + P.shift;
+    const uint64_t vtotal = P.nfull + (P.tail ? 1u : 0u) + P.shift;
+    for (uint64_t vbase = (uint64_t)blockIdx.x * PER; vbase < vtotal; vbase += (uint64_t)gridDim.x * PER)
+        ctr_cached_iter<NR, B>(P, K, tbl, lk, lane, vbase + (uint64_t)wave * 64u * B);
+}
 
-    for (uint64_t vbase = (uint64_t)blockIdx.x * PER; vbase < vtotal; vbase += (uint64_t)gridDim.x * PER) {
-        const uint64_t vw = vbase + (uint64_t)wave * 64u * B; /* wave's first virtual block (uniform) */
-        /* uniform counter C = cbase + vw */
-        uint64_t clo = P.cbase.lo + vw;
-        uint64_t chi = P.cbase.hi + ((!P.wrap64 && clo < P.cbase.lo) ? 1u : 0u);
-        const uint32_t w0 = bswap32((uint32_t)(chi >> 32)) ^ K.rk[0];
-        const uint32_t w1 = bswap32((uint32_t)chi) ^ K.rk[1];
-        const uint32_t w2 = bswap32((uint32_t)(clo >> 32)) ^ K.rk[2];
-        const uint32_t w3u = bswap32((uint32_t)clo) ^ K.rk[3]; /* byte 15 (top byte) patched per block */
-        /* round 1, uniform parts */
-        const uint32_t U0 = te_u(w0) ^ rotl8(te_u(w1 >> 8)) ^ rotl16(te_u(w2 >> 16)) ^ K.rk[4];
-        const uint32_t t1 = te_u(w1) ^ rotl8(te_u(w2 >> 8)) ^ rotl16(te_u(w3u >> 16)) ^ rotl24(te_u(w0 >> 24)) ^ K.rk[5];
-        const uint32_t t2 = te_u(w2) ^ rotl8(te_u(w3u >> 8)) ^ rotl16(te_u(w0 >> 16)) ^ rotl24(te_u(w1 >> 24)) ^ K.rk[6];
-        const uint32_t t3 = te_u(w3u) ^ rotl8(te_u(w0 >> 8)) ^ rotl16(te_u(w1 >> 16)) ^ rotl24(te_u(w2 >> 24)) ^ K.rk[7];
-        /* round 2, uniform parts */
-        const uint32_t V0 = rotl8(te_u(t1 >> 8)) ^ rotl16(te_u(t2 >> 16)) ^ rotl24(te_u(t3 >> 24)) ^ K.rk[8];
-        const uint32_t V1 = te_u(t1) ^ rotl8(te_u(t2 >> 8)) ^ rotl16(te_u(t3 >> 16)) ^ K.rk[9];
-        const uint32_t V2 = te_u(t2) ^ rotl8(te_u(t3 >> 8)) ^ rotl24(te_u(t1 >> 24)) ^ K.rk[10];
-        const uint32_t V3 = te_u(t3) ^ rotl16(te_u(t1 >> 16)) ^ rotl24(te_u(t2 >> 24)) ^ K.rk[11];
-        const uint32_t b15 = (uint32_t)(clo & 0xFFu); /* low byte of C (low 6+log2(B) bits are 0) */
-
-        const int64_t i0 = (int64_t)vw - (int64_t)P.shift + lane; /* real block index of (b=0, lane) */
-        const bool full = vw >= P.shift && vw - P.shift + 64u * B <= P.nfull; /* uniform */
-        uint32_t s[B][4];
-        uint4 x[B];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            const int64_t i = i0 + 64 * b;
-            const bool ok = full || (i >= 0 && (uint64_t)i < P.nfull);
-            x[b] = ok ? lds16(P.in, (uint64_t)i) : make_uint4(0, 0, 0, 0);
-            /* round 1: only T3[byte 15] varies */
-            const uint32_t c15 = (b15 | (uint32_t)(64 * b) | lane) ^ (K.rk[3] >> 24);
-            const uint32_t s0 = U0 ^ lds_at(tbl, (c15 << 8) | lk[3]);
-            /* round 2: the four lookups fed by s0 */
-            s[b][0] = V0 ^ lds_at(tbl, tt_addr(s0, lk[0], 0));
-            s[b][1] = V1 ^ lds_at(tbl, tt_addr(s0, lk[3], 3));
-            s[b][2] = V2 ^ lds_at(tbl, tt_addr(s0, lk[2], 2));
-            s[b][3] = V3 ^ lds_at(tbl, tt_addr(s0, lk[1], 1));
-        }
-        /* rounds 3..NR */
-        enc_rounds4_from<3, NR, B>(tbl, lk, K, s);
-
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            const int64_t i = i0 + 64 * b;
-            const bool ok = full || (i >= 0 && (uint64_t)i < P.nfull);
-            if (ok) {
-                sts16(P.out, (uint64_t)i,
-                     make_uint4(x[b].x ^ s[b][0], x[b].y ^ s[b][1], x[b].z ^ s[b][2], x[b].w ^ s[b][3]));
-            } else if (i >= 0 && (uint64_t)i == P.nfull && P.tail) {
-                const uint32_t ks[4] = {s[b][0], s[b][1], s[b][2], s[b][3]};
-                for (uint32_t n = 0; n < P.tail; ++n)
-                    P.out[16 * (uint64_t)i + n] = P.in[16 * (uint64_t)i + n] ^ (uint8_t)(ks[n >> 2] >> (8 * (n & 3)));
-            }
-        }
+/* The same cipher as a persistent claim kernel (one 1024-thread workgroup
+ * per CU, engine.cpp routes CTR calls from tt_persistent_min() to the T-table
+ * here): every wave takes 2048-block units of the virtual range -- its first
+ * one handed out (otc_device.h first_unit), the rest claimed from the back --
+ * so a call ends when the work does, not when the CU with the most static
+ * chunks does.  Blocks outside [0, nfull] are masked per iteration, as in
+ * the grid kernel.  It never runs beside the bitsliced kernel, so it keeps
+ * the grid kernel's static table (not a "_claim" kernel of the splits). */
+template <int NR>
+__global__ __launch_bounds__(1024) void k_aes_ctr_tt_persist(CtrParams P, otc_aes_key K)
+{
+    constexpr int B = OTC_TT_CTR_B;
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[2 * 256 * 64];
+    fill_tbl4<1024>(tbl, g_tab.te0);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t lk[4];
+    tbl4_lane_consts(lane, lk);
+    for (int64_t u = first_unit(P.cl, true, blockIdx.x * 16u + wave); u >= 0; u = claim_unit(P.cl, true)) {
+#pragma unroll 1
+        for (uint32_t it = 0; it < CLAIM_UNIT / (64u * B); ++it)
+            ctr_cached_iter<NR, B>(P, K, tbl, lk, lane, (uint64_t)u * CLAIM_UNIT + it * 64u * B);
     }
 }
 
@@ -1389,6 +1421,36 @@ hipError_t tt_ctr(const void *in, void *out, size_t nbytes, const otc_aes_key &K
     case 14: return launch_ctr_cached<14>(P, K, c.lo, st);
     default: return hipErrorInvalidValue;
     }
+}
+
+/* the persistent claim form of tt_ctr: its virtual range (the blocks plus
+ * ctr0 mod 4096 in front) in 2048-block units */
+uint64_t tt_ctr_claim_units(size_t nbytes, uint64_t ctr_lo)
+{
+    return (nbytes / 16 + (nbytes % 16 ? 1 : 0) + (ctr_lo & 4095u) + CLAIM_UNIT - 1) / CLAIM_UNIT;
+}
+
+hipError_t tt_ctr_claim(const void *in, void *out, size_t nbytes, const otc_aes_key &K, Ctr128 c, bool wrap64,
+                        SplitClaim cl, hipStream_t st)
+{
+    CtrParams P{};
+    P.in = (const uint8_t *)in;
+    P.out = (uint8_t *)out;
+    P.nfull = nbytes / 16;
+    P.tail = (uint32_t)(nbytes % 16);
+    P.wrap64 = wrap64 ? 1u : 0u;
+    P.cbase.hi = c.hi;
+    P.shift = c.lo & 4095u; /* as the grid kernel's bulk shape (PER = 1024 x 4) */
+    P.cbase.lo = c.lo - P.shift;
+    P.cl = cl;
+    const dim3 g(cl.wgs ? cl.wgs : (unsigned)num_cus()), b(1024);
+    switch (K.nr) {
+    case 10: hipLaunchKernelGGL(k_aes_ctr_tt_persist<10>, g, b, 0, st, P, K); break;
+    case 12: hipLaunchKernelGGL(k_aes_ctr_tt_persist<12>, g, b, 0, st, P, K); break;
+    case 14: hipLaunchKernelGGL(k_aes_ctr_tt_persist<14>, g, b, 0, st, P, K); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t tt_cfb_decrypt(const void *in, void *out, uint64_t nblocks, const otc_aes_key &K,

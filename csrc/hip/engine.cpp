@@ -49,6 +49,8 @@ namespace otc_impl {
 hipError_t tt_ecb_encrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
 hipError_t tt_ecb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, hipStream_t);
 hipError_t tt_ctr(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, hipStream_t);
+uint64_t tt_ctr_claim_units(size_t, uint64_t);
+hipError_t tt_ctr_claim(const void *, void *, size_t, const otc_aes_key &, Ctr128, bool, SplitClaim, hipStream_t);
 hipError_t tt_cfb_decrypt(const void *, void *, uint64_t, const otc_aes_key &, const uint32_t *, hipStream_t);
 hipError_t tt_cbc_decrypt(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
 hipError_t tt_cbc_decrypt_seg(const void *, void *, uint64_t, uint64_t, const otc_aes_key &, Ctr128, hipStream_t);
@@ -500,6 +502,13 @@ size_t env_mib(const char *name, size_t dflt)
     const char *v = getenv(name);
     return v && *v ? (size_t)strtoull(v, nullptr, 10) << 20 : dflt;
 }
+/* CTR on the T-table: the persistent claim kernel from this size (A/B and
+ * threshold sweeps: OTC_TT_CTR_PERSISTENT_MIN_MIB) */
+size_t tt_ctr_persistent_min()
+{
+    static const size_t m = env_mib("OTC_TT_CTR_PERSISTENT_MIN_MIB", (size_t)512 << 20);
+    return m;
+}
 size_t tt_persistent_min()
 {
     static const size_t m = env_mib("OTC_TT_PERSISTENT_MIN_MIB", (size_t)512 << 20);
@@ -792,8 +801,20 @@ static int ctr_common(const void *in, void *out, size_t nbytes, const otc_aes_ke
     hipStream_t st = (hipStream_t)stream;
     const int im = pick_impl(impl, k->bits, nbytes);
     g_last_impl = im;
-    hipError_t e = im == OTC_IMPL_BITSLICE ? otc_impl::bs_ctr(in, out, nbytes, *k, c, wrap64, st)
-                                           : otc_impl::tt_ctr(in, out, nbytes, *k, c, wrap64, st);
+    hipError_t e;
+    if (im == OTC_IMPL_BITSLICE) {
+        e = otc_impl::bs_ctr(in, out, nbytes, *k, c, wrap64, st);
+    } else if (nbytes >= tt_ctr_persistent_min()) {
+        /* the T-table as a persistent claim kernel (first units handed out,
+         * the rest claimed): no CU waits on another's static share */
+        e = split_claim(
+            otc_impl::tt_ctr_claim_units(nbytes, c.lo), 2, false, 0u, st, &g_last_impl,
+            [&](SplitClaim cl, hipStream_t ts) { return otc_impl::tt_ctr_claim(in, out, nbytes, *k, c, wrap64, cl, ts); },
+            [&](SplitClaim, hipStream_t) { return hipErrorInvalidValue; /* bs_wgs 0: no VALU half */ },
+            [&]() { return otc_impl::tt_ctr(in, out, nbytes, *k, c, wrap64, st); });
+    } else {
+        e = otc_impl::tt_ctr(in, out, nbytes, *k, c, wrap64, st);
+    }
     if (e != hipSuccess) return hip_fail(e, "aes_ctr launch");
     return OTC_OK;
 }

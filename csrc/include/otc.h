@@ -59,7 +59,7 @@ int otc_aes_key_init(otc_aes_key *k, const uint8_t *key, int bits, int dir);
 
 /* ---- implementation selection ------------------------------------------- */
 #define OTC_IMPL_AUTO 0     /* the measured winner (docs/PERF.md rounds 5-6): bitsliced for CTR calls >= 2 GiB
-                               (AES-256: >= 1 GiB); for ECB / CBC / CFB decryption and the power-of-two segment
+                               (AES-256: >= 1 GiB), the persistent T-table CTR kernel from 512 MiB; for ECB / CBC / CFB decryption and the power-of-two segment
                                decryptions the split below from 2 GiB and the persistent T-table claim kernel
                                alone from 512 MiB; segment encryption: the persistent T-table claim kernel from
                                1 GiB; the grid T-table otherwise

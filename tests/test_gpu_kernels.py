@@ -602,6 +602,32 @@ def test_ctr_split_request_runs_auto(gpu, bits):
     assert host(y) == cpu_ref.ctr(key, ctr, host(x))
 
 
+@pytest.mark.parametrize("bits", [128, 256])
+def test_persistent_ttable_ctr(gpu, bits):
+    """CTR on the T-table from 512 MiB runs the persistent claim kernel
+    (engine.cpp ctr_common, aes_tt.hip k_aes_ctr_tt_persist): byte-equal to
+    the bitsliced kernel over the whole buffer and to the oracle on samples,
+    with a counter that carries out of the low 64 bits inside the call, a
+    counter offset that is not 4096-aligned (the virtual range's masked
+    head) and a partial last block; in place too."""
+    key = os.urandom(bits // 8)
+    ctr = os.urandom(8) + (2**64 - 4096 * 40 - 77).to_bytes(8, "big")
+    n = (600 << 20) + 16 * 2048 * 3 + 16 * 9 + 11
+    x = torch.empty(n, dtype=torch.uint8, device=gpu)
+    ops.fill_random_(x, seed=n ^ bits)
+    y = ops.ctr(x, key, ctr, block_offset=1234567, impl="ttable")
+    assert ops.last_impl() == "ttable"
+    z = ops.ctr(x, key, ctr, block_offset=1234567, impl="bitslice")
+    torch.cuda.synchronize()
+    assert torch.equal(y, z)
+    for lo in (0, n // 2 - (n // 2) % 16, n - 16 * 9 - 11):
+        hi = min(n, lo + 16 * 64)
+        assert host(y[lo:hi]) == cpu_ref.ctr(key, ctr, host(x[lo:hi]), 1234567 + lo // 16), lo
+    ops.ctr(x, key, ctr, out=x, block_offset=1234567, impl="ttable")
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)
+
+
 def test_persistent_ttable_midsize(gpu):
     """ECB (both directions), CBC / CFB decryption and their segment forms
     between 896 MiB and 2 GiB run the persistent T-table claim kernel alone
