@@ -131,6 +131,18 @@ __device__ __forceinline__ uint4 seg_prev(const BsParams &P, const uint8_t *own,
     return v;
 }
 
+/* Waves per workgroup of the CTR launches (k_aes_bs_t3; the claim kernel
+ * keeps 4): each wave is an independent 2048-block task, so the workgroup
+ * only sets how many waves the dispatcher must place at once -- a 4-wave
+ * group needs a free slot on all four SIMDs and its 32 KiB of staging LDS.
+ * Smaller groups LOSE: AES-128 CTR 64 GiB 1705-1712 (1 wave) and 1710-1714
+ * (2) vs 1726-1752 GB/s (4), AES-256 and 4 GiB alike, same held clock
+ * (profiles/r6/wpg/, 3 interleaved reps). */
+#ifndef OTC_BS_WPG
+#define OTC_BS_WPG 4
+#endif
+constexpr uint32_t BS_WPG = OTC_BS_WPG;
+
 /* Task geometry shared by both kernels. */
 struct Task {
     uint32_t lane, wave;
@@ -158,10 +170,11 @@ __device__ __forceinline__ bool task_of(const BsParams &P, Task &t, int64_t clai
      * hoist loop-invariant plane/mask values out of it, which costs more
      * registers than the 128-plane state leaves.  Full blocks only; the host
      * routes a trailing partial CTR block to the T-table kernel. */
-    uint64_t task = claimed >= 0 ? (uint64_t)claimed : (uint64_t)blockIdx.x * 4u + t.wave;
+    const uint32_t gw = (uint32_t)blockIdx.x * BS_WPG + t.wave; /* the wave's index in the launch */
+    uint64_t task = claimed >= 0 ? (uint64_t)claimed : (uint64_t)gw;
     if (P.part == BS_EDGE_ONLY) {
-        if (t.wave > 1 || (t.wave == 1 && P.tasks < 2)) return false;
-        task = t.wave == 0 ? 0 : P.tasks - 1;
+        if (gw > 1 || (gw == 1 && P.tasks < 2)) return false;
+        task = gw == 0 ? 0 : P.tasks - 1;
     }
     t.vbase = task * 2048u;
     if (t.vbase >= P.nblocks + shift) return false;
@@ -555,7 +568,7 @@ template <int NR, int MODE, int LS, bool CACHE, bool FO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_aes_bs_t3(BsParams P,
                                                                                              otc_aes_key K)
 {
-    __shared__ uint4 stage[LS > 0 ? 4 * LS * 64 : 1];
+    __shared__ uint4 stage[LS > 0 ? BS_WPG * LS * 64 : 1];
     aes_bs_task<NR, MODE, LS, CACHE, FO>(P, K, stage);
 }
 
@@ -589,10 +602,10 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
 {
     const uint64_t vt = P.nblocks + (MODE == BS_CTR ? P.shift : 0);
     const uint64_t tasks = (vt + 2047) / 2048;
-    uint64_t wgs = (tasks + 3) / 4;
+    uint64_t wgs = (tasks + BS_WPG - 1) / BS_WPG;
     if (wgs < 1) wgs = 1;
     if (wgs > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    const dim3 g((unsigned)wgs), b(256);
+    const dim3 g((unsigned)wgs), b(64 * BS_WPG);
     /* CTR counter caching (+34% over no caching, profiles/r2/bitslice) */
     bool cache = MODE == BS_CTR;
     const uint64_t ngroups = cache ? (((P.cbase.lo >> 11) & 31u) + tasks + 31) >> 5 : 0;
@@ -637,7 +650,7 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
             return hipErrorInvalidValue;
         }
         hipLaunchKernelGGL((k_aes_bs_claim<NR, MODE>),
-                           dim3(P.cl.wgs ? P.cl.wgs : (unsigned)otc_dev::device_cus()), b, 0, st, Q, K);
+                           dim3(P.cl.wgs ? P.cl.wgs : (unsigned)otc_dev::device_cus()), dim3(256), 0, st, Q, K);
     } else {
         const bool edge = P.shift != 0 || vt % 2048 != 0;
         auto run = [&](auto cachec) {
@@ -646,7 +659,8 @@ hipError_t launch_nr(const BsParams &P, const otc_aes_key &K, hipStream_t st)
             hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, true>), g, b, 0, st, Q, K);
             if (edge) {
                 Q.part = BS_EDGE_ONLY;
-                hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, false>), dim3(1), b, 0, st, Q, K);
+                hipLaunchKernelGGL((k_aes_bs_t3<NR, MODE, LS, C, false>), dim3((2 + BS_WPG - 1) / BS_WPG), b, 0, st,
+                                   Q, K);
             }
         };
         if (cache) {
