@@ -1010,7 +1010,9 @@ struct BatchParams {
     const uint32_t *tile_msg;
     const uint64_t *tile_first;
     uint64_t ntiles;
+    SplitClaim cl; /* ctr != nullptr: BATCH_UNIT-tile units, first handed out, the rest claimed */
 };
+constexpr uint64_t BATCH_UNIT = 8; /* tiles per claimed unit (8 x 4 KiB at B = 4) */
 
 __device__ __forceinline__ uint32_t ufl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -1065,8 +1067,25 @@ __global__ __launch_bounds__(THREADS) void k_aes_ctr_batch_tt(BatchParams P)
      * tile-map / descriptor cache lines (and usually the message), so the
      * dependent scalar loads at a tile start hit the scalar cache */
     const uint64_t nw = (uint64_t)gridDim.x * WAVES, wid = (uint64_t)blockIdx.x * WAVES + wave;
-    const uint64_t t_end = (wid + 1) * P.ntiles / nw;
-    for (uint64_t t = wid * P.ntiles / nw; t < t_end; ++t) {
+    /* large batches (P.cl.ctr set, engine.cpp): runs of BATCH_UNIT tiles,
+     * the first handed out, the rest claimed, so the batch ends when the
+     * work does -- a static split left CUs idle behind the slowest share, as
+     * the T-table CTR grid did (docs/PERF.md round 6) */
+    const bool claimed = P.cl.ctr != nullptr;
+    uint64_t t = wid * P.ntiles / nw, t_end = (wid + 1) * P.ntiles / nw;
+    if (claimed) {
+        const int64_t u = first_unit(P.cl, true, (uint32_t)wid);
+        t = u < 0 ? 0 : (uint64_t)u * BATCH_UNIT;
+        t_end = u < 0 ? 0 : min((uint64_t)(u + 1) * BATCH_UNIT, P.ntiles);
+    }
+    for (;; ++t) {
+        if (t >= t_end) {
+            if (!claimed) break;
+            const int64_t u = claim_unit(P.cl, true);
+            if (u < 0) break;
+            t = (uint64_t)u * BATCH_UNIT;
+            t_end = min((uint64_t)(u + 1) * BATCH_UNIT, P.ntiles);
+        }
         /* descriptor, tile base and round keys through the constant address
          * space: wave-uniform addresses -> scalar loads (s_load_dwordx*) into
          * SGPRs, no VGPRs and no per-lane memory traffic */
@@ -1362,10 +1381,14 @@ namespace otc_impl {
 
 OTC_STRACE_READER(strace_read_tt)
 
+uint64_t tt_ctr_batch_units(uint64_t ntiles) { return (ntiles + BATCH_UNIT - 1) / BATCH_UNIT; }
+
 hipError_t tt_ctr_batch(const otc_ctr_msg *msgs, const otc_aes_key *keys, const uint32_t *tile_msg,
-                        const uint64_t *tile_first, uint64_t ntiles, int tile_blocks, int nr, hipStream_t st)
+                        const uint64_t *tile_first, uint64_t ntiles, int tile_blocks, int nr, hipStream_t st,
+                        const SplitClaim *cl)
 {
     BatchParams P{msgs, keys, tile_msg, tile_first, ntiles};
+    if (cl) P.cl = *cl;
     switch (nr) {
     case 10: return launch_ctr_batch_nr<10>(P, tile_blocks, st);
     case 12: return launch_ctr_batch_nr<12>(P, tile_blocks, st);

@@ -78,7 +78,8 @@ hipError_t tt_cbc_decrypt_seg_claim(const void *, void *, uint64_t, const otc_ae
 hipError_t tt_cfb_decrypt_seg_claim(const void *, void *, uint64_t, const otc_aes_key &, Ctr128, uint32_t, SplitClaim,
                                     hipStream_t);
 hipError_t tt_ctr_batch(const otc_ctr_msg *, const otc_aes_key *, const uint32_t *, const uint64_t *, uint64_t, int, int,
-                        hipStream_t);
+                        hipStream_t, const SplitClaim *);
+uint64_t tt_ctr_batch_units(uint64_t);
 hipError_t k_xor(const void *, const void *, void *, size_t, hipStream_t);
 hipError_t k_fill_random(void *, size_t, uint64_t, hipStream_t);
 hipError_t k_checksum(const void *, size_t, uint64_t *, hipStream_t);
@@ -940,8 +941,24 @@ extern "C" int otc_aes_ctr_batch(const otc_ctr_msg *msgs, const otc_aes_key *key
     if (nr != 10 && nr != 12 && nr != 14) return set_err(OTC_ERR_ARG, "ctr_batch: nr must be 10, 12 or 14");
     if ((((uintptr_t)msgs) | ((uintptr_t)keys) | ((uintptr_t)tile_first)) & 7u || ((uintptr_t)tile_msg & 3u))
         return set_err(OTC_ERR_ARG, "ctr_batch: misaligned descriptor arrays");
-    hipError_t e = otc_impl::tt_ctr_batch(msgs, keys, tile_msg, tile_first, ntiles, tile_blocks, nr,
-                                          (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    auto plain = [&]() { return otc_impl::tt_ctr_batch(msgs, keys, tile_msg, tile_first, ntiles, tile_blocks, nr, st, nullptr); };
+    /* large batches: claimed tile runs (first one handed out) instead of the
+     * static split over the waves (A/B: OTC_BATCH_CLAIM_MIN_TILES) */
+    static const uint64_t min_tiles = [] {
+        const char *v = getenv("OTC_BATCH_CLAIM_MIN_TILES");
+        return v && *v ? (uint64_t)strtoull(v, nullptr, 10) : (uint64_t)65536;
+    }();
+    int ran = 0;
+    hipError_t e = ntiles >= min_tiles
+                       ? split_claim(
+                             otc_impl::tt_ctr_batch_units(ntiles), 2, false, 0u, st, &ran,
+                             [&](SplitClaim cl, hipStream_t ts) {
+                                 return otc_impl::tt_ctr_batch(msgs, keys, tile_msg, tile_first, ntiles, tile_blocks, nr,
+                                                               ts, &cl);
+                             },
+                             [&](SplitClaim, hipStream_t) { return hipErrorInvalidValue; /* no VALU half */ }, plain)
+                       : plain();
     if (e != hipSuccess) return hip_fail(e, "ctr_batch launch");
     return OTC_OK;
 }
